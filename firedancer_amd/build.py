@@ -1,0 +1,74 @@
+"""Build the MI355X (gfx950) engine and the test-infrastructure oracle, in tree.
+
+    python -m firedancer_amd.build          # or __graft_entry__.build()
+
+Outputs:
+    firedancer_amd/libfd_ed25519_amd.so   the product: HIP kernels + C-ABI
+    oracle/liboracle.so                   CPU restatement (checker only)
+    oracle/_ref/libfdref.so               the reference's own sources, compiled
+                                          (only when /root/reference exists)
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "firedancer_amd")
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libfd_ed25519_amd.so")
+ARCH = os.environ.get("FD_AMD_ARCH", "gfx950")
+
+SOURCES = ["fd_ed25519_kernels.hip", "fd_ed25519_engine.cpp", "fd_ed25519_host.cpp"]
+HEADERS = ["fd_ed25519_dev.h", "fd_ed25519_kernels.h", "../../include/fd_ed25519_amd.h",
+           "../../tools/gen_consts.py"]
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: the engine is HIP-only (no CPU build)")
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build_engine(force=False, verbose=False):
+    consts = os.path.join(CSRC, "fd_ed25519_consts.h")
+    gen = os.path.join(ROOT, "tools", "gen_consts.py")
+    if force or _stale(consts, [gen]):
+        subprocess.check_call([sys.executable, gen, consts, "FD_AMD"])
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [consts]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    cmd = [_hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-function", "-o", LIB + ".tmp"]
+    cmd += [os.path.join(CSRC, s) for s in SOURCES]
+    cmd += ["-lpthread"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd, cwd=CSRC)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+def build_oracle(verbose=False):
+    od = os.path.join(ROOT, "oracle")
+    out = subprocess.DEVNULL if not verbose else None
+    subprocess.check_call(["make", "-C", od, "-j8", "all"], stdout=out)
+    if os.path.isdir("/root/reference/src"):
+        subprocess.check_call(["make", "-C", od, "-j8", "ref", "tools"], stdout=out)
+
+
+def build(force=False, verbose=False):
+    build_oracle(verbose)
+    return build_engine(force, verbose)
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,298 @@
+/* firedancer_amd/csrc/fd_ed25519_dev.h
+ *
+ * CDNA4 (gfx950) device arithmetic for the ed25519 verify engine: one
+ * signature per lane, every value in VGPRs.
+ *
+ * Field elements are the reference's representation (10 x int32 signed
+ * limbs, radix 2^25.5) and every field op reproduces the reference's AVX
+ * build limb for limb (src/ballet/ed25519/avx/
+ * fd_ed25519_fe_avx_inl.h:484-674): int32 pre-multiples with wrap-around,
+ * exact int64 column sums built from v_mad_i64_i32 chains, then the
+ * reference carry chain.  Limbs are never canonicalised except where the
+ * reference calls fe_tobytes (isnonzero / isnegative).
+ */
+#ifndef FD_ED25519_DEV_H
+#define FD_ED25519_DEV_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "fd_ed25519_consts.h"
+
+#define FD_DEV static __device__ __forceinline__
+
+typedef int32_t  i32;
+typedef uint32_t u32;
+typedef int64_t  i64;
+typedef uint64_t u64;
+typedef uint8_t  u8;
+
+struct fe { i32 v[10]; };
+
+FD_DEV fe fe_zero() { fe r; _Pragma("unroll") for( int i=0; i<10; i++ ) r.v[i] = 0; return r; }
+FD_DEV fe fe_one () { fe r = fe_zero(); r.v[0] = 1; return r; }
+
+FD_DEV i32 wmul( i32 a, i32 k ) { return (i32)((u32)a * (u32)k); }   /* int32 wrap: the low 32 bits the AVX mul sees */
+FD_DEV i64 mll ( i32 a, i32 b ) { return (i64)a * (i64)b; }            /* v_mad_i64_i32 */
+
+FD_DEV fe fe_add( fe const & f, fe const & g ) { fe h; _Pragma("unroll") for( int i=0; i<10; i++ ) h.v[i] = (i32)((u32)f.v[i] + (u32)g.v[i]); return h; }
+FD_DEV fe fe_sub( fe const & f, fe const & g ) { fe h; _Pragma("unroll") for( int i=0; i<10; i++ ) h.v[i] = (i32)((u32)f.v[i] - (u32)g.v[i]); return h; }
+FD_DEV fe fe_neg( fe const & f )               { fe h; _Pragma("unroll") for( int i=0; i<10; i++ ) h.v[i] = (i32)(0u - (u32)f.v[i]); return h; }
+
+/* Reference carry chain (avx/fd_ed25519_fe_avx_inl.h:570-584):
+   0,4 | 1,5 | 2,6 | 3,7 | 4,8 | 9(x19) | 0, rounding carries
+   c = (h + 2^(w-1)) >> w with an arithmetic shift. */
+FD_DEV fe fe_carry( i64 h0, i64 h1, i64 h2, i64 h3, i64 h4, i64 h5, i64 h6, i64 h7, i64 h8, i64 h9 ) {
+  i64 c;
+  c = (h0 + (1L<<25)) >> 26; h1 += c; h0 -= c << 26;
+  c = (h4 + (1L<<25)) >> 26; h5 += c; h4 -= c << 26;
+  c = (h1 + (1L<<24)) >> 25; h2 += c; h1 -= c << 25;
+  c = (h5 + (1L<<24)) >> 25; h6 += c; h5 -= c << 25;
+  c = (h2 + (1L<<25)) >> 26; h3 += c; h2 -= c << 26;
+  c = (h6 + (1L<<25)) >> 26; h7 += c; h6 -= c << 26;
+  c = (h3 + (1L<<24)) >> 25; h4 += c; h3 -= c << 25;
+  c = (h7 + (1L<<24)) >> 25; h8 += c; h7 -= c << 25;
+  c = (h4 + (1L<<25)) >> 26; h5 += c; h4 -= c << 26;
+  c = (h8 + (1L<<25)) >> 26; h9 += c; h8 -= c << 26;
+  c = (h9 + (1L<<24)) >> 25; h0 += c * 19; h9 -= c << 25;
+  c = (h0 + (1L<<25)) >> 26; h1 += c; h0 -= c << 26;
+  fe r;
+  r.v[0] = (i32)h0; r.v[1] = (i32)h1; r.v[2] = (i32)h2; r.v[3] = (i32)h3; r.v[4] = (i32)h4;
+  r.v[5] = (i32)h5; r.v[6] = (i32)h6; r.v[7] = (i32)h7; r.v[8] = (i32)h8; r.v[9] = (i32)h9;
+  return r;
+}
+
+/* f * 1 through the reference multiplier: the column sums are the limbs
+   themselves, so it is exactly the carry chain ("x1" renormalisation of
+   the AVX flow, avx/fd_ed25519_ge.c:440-446 and the madd lane 0). */
+FD_DEV fe fe_mul_one( fe const & f ) {
+  return fe_carry( f.v[0], f.v[1], f.v[2], f.v[3], f.v[4], f.v[5], f.v[6], f.v[7], f.v[8], f.v[9] );
+}
+
+/* FE_AVX_INL_MUL, one lane (avx/fd_ed25519_fe_avx_inl.h:484-585) */
+FD_DEV fe fe_mul( fe const & F, fe const & G ) {
+  i32 const * f = F.v; i32 const * g = G.v;
+  i32 g1_19 = wmul( g[1], 19 ), g2_19 = wmul( g[2], 19 ), g3_19 = wmul( g[3], 19 );
+  i32 g4_19 = wmul( g[4], 19 ), g5_19 = wmul( g[5], 19 ), g6_19 = wmul( g[6], 19 );
+  i32 g7_19 = wmul( g[7], 19 ), g8_19 = wmul( g[8], 19 ), g9_19 = wmul( g[9], 19 );
+  i32 f1_2 = wmul( f[1], 2 ), f3_2 = wmul( f[3], 2 ), f5_2 = wmul( f[5], 2 );
+  i32 f7_2 = wmul( f[7], 2 ), f9_2 = wmul( f[9], 2 );
+  i64 h0 = mll(f[0],g[0]) + mll(f1_2,g9_19) + mll(f[2],g8_19) + mll(f3_2,g7_19) + mll(f[4],g6_19)
+         + mll(f5_2,g5_19) + mll(f[6],g4_19) + mll(f7_2,g3_19) + mll(f[8],g2_19) + mll(f9_2,g1_19);
+  i64 h1 = mll(f[0],g[1]) + mll(f[1],g[0]) + mll(f[2],g9_19) + mll(f[3],g8_19) + mll(f[4],g7_19)
+         + mll(f[5],g6_19) + mll(f[6],g5_19) + mll(f[7],g4_19) + mll(f[8],g3_19) + mll(f[9],g2_19);
+  i64 h2 = mll(f[0],g[2]) + mll(f1_2,g[1]) + mll(f[2],g[0]) + mll(f3_2,g9_19) + mll(f[4],g8_19)
+         + mll(f5_2,g7_19) + mll(f[6],g6_19) + mll(f7_2,g5_19) + mll(f[8],g4_19) + mll(f9_2,g3_19);
+  i64 h3 = mll(f[0],g[3]) + mll(f[1],g[2]) + mll(f[2],g[1]) + mll(f[3],g[0]) + mll(f[4],g9_19)
+         + mll(f[5],g8_19) + mll(f[6],g7_19) + mll(f[7],g6_19) + mll(f[8],g5_19) + mll(f[9],g4_19);
+  i64 h4 = mll(f[0],g[4]) + mll(f1_2,g[3]) + mll(f[2],g[2]) + mll(f3_2,g[1]) + mll(f[4],g[0])
+         + mll(f5_2,g9_19) + mll(f[6],g8_19) + mll(f7_2,g7_19) + mll(f[8],g6_19) + mll(f9_2,g5_19);
+  i64 h5 = mll(f[0],g[5]) + mll(f[1],g[4]) + mll(f[2],g[3]) + mll(f[3],g[2]) + mll(f[4],g[1])
+         + mll(f[5],g[0]) + mll(f[6],g9_19) + mll(f[7],g8_19) + mll(f[8],g7_19) + mll(f[9],g6_19);
+  i64 h6 = mll(f[0],g[6]) + mll(f1_2,g[5]) + mll(f[2],g[4]) + mll(f3_2,g[3]) + mll(f[4],g[2])
+         + mll(f5_2,g[1]) + mll(f[6],g[0]) + mll(f7_2,g9_19) + mll(f[8],g8_19) + mll(f9_2,g7_19);
+  i64 h7 = mll(f[0],g[7]) + mll(f[1],g[6]) + mll(f[2],g[5]) + mll(f[3],g[4]) + mll(f[4],g[3])
+         + mll(f[5],g[2]) + mll(f[6],g[1]) + mll(f[7],g[0]) + mll(f[8],g9_19) + mll(f[9],g8_19);
+  i64 h8 = mll(f[0],g[8]) + mll(f1_2,g[7]) + mll(f[2],g[6]) + mll(f3_2,g[5]) + mll(f[4],g[4])
+         + mll(f5_2,g[3]) + mll(f[6],g[2]) + mll(f7_2,g[1]) + mll(f[8],g[0]) + mll(f9_2,g9_19);
+  i64 h9 = mll(f[0],g[9]) + mll(f[1],g[8]) + mll(f[2],g[7]) + mll(f[3],g[6]) + mll(f[4],g[5])
+         + mll(f[5],g[4]) + mll(f[6],g[3]) + mll(f[7],g[2]) + mll(f[8],g[1]) + mll(f[9],g[0]);
+  return fe_carry( h0, h1, h2, h3, h4, h5, h6, h7, h8, h9 );
+}
+
+/* FE_AVX_INL_SQN, one lane, n in {1,2} (avx/fd_ed25519_fe_avx_inl.h:592-674):
+   55 products; the column sums are doubled before the carry when n==2. */
+template<int N>
+FD_DEV fe fe_sqn( fe const & F ) {
+  i32 const * f = F.v;
+  i32 f0_2 = wmul( f[0], 2 ), f1_2 = wmul( f[1], 2 ), f2_2 = wmul( f[2], 2 ), f3_2 = wmul( f[3], 2 );
+  i32 f4_2 = wmul( f[4], 2 ), f5_2 = wmul( f[5], 2 ), f6_2 = wmul( f[6], 2 ), f7_2 = wmul( f[7], 2 );
+  i32 f5_38 = wmul( f[5], 38 ), f6_19 = wmul( f[6], 19 ), f7_38 = wmul( f[7], 38 );
+  i32 f8_19 = wmul( f[8], 19 ), f9_38 = wmul( f[9], 38 );
+  i64 h0 = mll(f[0],f[0]) + mll(f1_2,f9_38) + mll(f2_2,f8_19) + mll(f3_2,f7_38) + mll(f4_2,f6_19) + mll(f[5],f5_38);
+  i64 h1 = mll(f0_2,f[1]) + mll(f[2],f9_38) + mll(f3_2,f8_19) + mll(f[4],f7_38) + mll(f5_2,f6_19);
+  i64 h2 = mll(f0_2,f[2]) + mll(f1_2,f[1]) + mll(f3_2,f9_38) + mll(f4_2,f8_19) + mll(f5_2,f7_38) + mll(f[6],f6_19);
+  i64 h3 = mll(f0_2,f[3]) + mll(f1_2,f[2]) + mll(f[4],f9_38) + mll(f5_2,f8_19) + mll(f[6],f7_38);
+  i64 h4 = mll(f0_2,f[4]) + mll(f1_2,f3_2) + mll(f[2],f[2]) + mll(f5_2,f9_38) + mll(f6_2,f8_19) + mll(f[7],f7_38);
+  i64 h5 = mll(f0_2,f[5]) + mll(f1_2,f[4]) + mll(f2_2,f[3]) + mll(f[6],f9_38) + mll(f7_2,f8_19);
+  i64 h6 = mll(f0_2,f[6]) + mll(f1_2,f5_2) + mll(f2_2,f[4]) + mll(f3_2,f[3]) + mll(f7_2,f9_38) + mll(f[8],f8_19);
+  i64 h7 = mll(f0_2,f[7]) + mll(f1_2,f[6]) + mll(f2_2,f[5]) + mll(f3_2,f[4]) + mll(f[8],f9_38);
+  i64 h8 = mll(f0_2,f[8]) + mll(f1_2,f7_2) + mll(f2_2,f[6]) + mll(f3_2,f5_2) + mll(f[4],f[4]) + mll(f[9],f9_38);
+  i64 h9 = mll(f0_2,f[9]) + mll(f1_2,f[8]) + mll(f2_2,f[7]) + mll(f3_2,f[6]) + mll(f4_2,f[5]);
+  if( N==2 ) { h0 += h0; h1 += h1; h2 += h2; h3 += h3; h4 += h4; h5 += h5; h6 += h6; h7 += h7; h8 += h8; h9 += h9; }
+  return fe_carry( h0, h1, h2, h3, h4, h5, h6, h7, h8, h9 );
+}
+
+FD_DEV fe fe_sq( fe const & f ) { return fe_sqn<1>( f ); }
+
+FD_DEV fe fe_sq_iter( fe const & f, int n ) {
+  fe h = fe_sq( f );
+  for( int i=1; i<n; i++ ) h = fe_sq( h );
+  return h;
+}
+
+/* fe_avx_pow22523, avx/fd_ed25519_fe_avx.h:246-275: z^(2^252-3) */
+FD_DEV fe fe_pow22523( fe const & z ) {
+  fe t0, t1, t2;
+  t0 = fe_sq( z );
+  t1 = fe_sq_iter( t0, 2 );
+  t1 = fe_mul( z, t1 );
+  t0 = fe_mul( t0, t1 );
+  t0 = fe_sq( t0 );
+  t0 = fe_mul( t1, t0 );
+  t1 = fe_sq_iter( t0, 5 );
+  t0 = fe_mul( t1, t0 );
+  t1 = fe_sq_iter( t0, 10 );
+  t1 = fe_mul( t1, t0 );
+  t2 = fe_sq_iter( t1, 20 );
+  t1 = fe_mul( t2, t1 );
+  t1 = fe_sq_iter( t1, 10 );
+  t0 = fe_mul( t1, t0 );
+  t1 = fe_sq_iter( t0, 50 );
+  t1 = fe_mul( t1, t0 );
+  t2 = fe_sq_iter( t1, 100 );
+  t1 = fe_mul( t2, t1 );
+  t1 = fe_sq_iter( t1, 50 );
+  t0 = fe_mul( t1, t0 );
+  t0 = fe_sq_iter( t0, 2 );
+  return fe_mul( t0, z );
+}
+
+/* fd_ed25519_fe_frombytes (avx/fd_ed25519_fe.c:4-46).  s = 8 LE words. */
+FD_DEV fe fe_frombytes( u32 const w[8] ) {
+  /* byte-granular loads of the reference expressed on 32-bit words */
+  auto B = [&]( int k ) -> u64 { return (u64)((w[k>>2] >> (8*(k&3))) & 0xffu); };
+  auto L3 = [&]( int k ) -> u64 { return B(k) | (B(k+1)<<8) | (B(k+2)<<16); };
+  auto L4 = [&]( int k ) -> u64 { return L3(k) | (B(k+3)<<24); };
+  i64 h0 = (i64) L4(0);
+  i64 h1 = (i64) L3(4) << 6;
+  i64 h2 = (i64) L3(7) << 5;
+  i64 h3 = (i64) L3(10) << 3;
+  i64 h4 = (i64) L3(13) << 2;
+  i64 h5 = (i64) L4(16);
+  i64 h6 = (i64) L3(20) << 7;
+  i64 h7 = (i64) L3(23) << 5;
+  i64 h8 = (i64) L3(26) << 4;
+  i64 h9 = (i64)((L3(29) & 0x7fffffUL) << 2);
+  i64 c;
+  c = (h9 + (1L<<24)) >> 25; h0 += c*19; h9 -= c<<25;
+  c = (h1 + (1L<<24)) >> 25; h2 += c;    h1 -= c<<25;
+  c = (h3 + (1L<<24)) >> 25; h4 += c;    h3 -= c<<25;
+  c = (h5 + (1L<<24)) >> 25; h6 += c;    h5 -= c<<25;
+  c = (h7 + (1L<<24)) >> 25; h8 += c;    h7 -= c<<25;
+  c = (h0 + (1L<<25)) >> 26; h1 += c;    h0 -= c<<26;
+  c = (h2 + (1L<<25)) >> 26; h3 += c;    h2 -= c<<26;
+  c = (h4 + (1L<<25)) >> 26; h5 += c;    h4 -= c<<26;
+  c = (h6 + (1L<<25)) >> 26; h7 += c;    h6 -= c<<26;
+  c = (h8 + (1L<<25)) >> 26; h9 += c;    h8 -= c<<26;
+  fe r;
+  r.v[0]=(i32)h0; r.v[1]=(i32)h1; r.v[2]=(i32)h2; r.v[3]=(i32)h3; r.v[4]=(i32)h4;
+  r.v[5]=(i32)h5; r.v[6]=(i32)h6; r.v[7]=(i32)h7; r.v[8]=(i32)h8; r.v[9]=(i32)h9;
+  return r;
+}
+
+/* fd_ed25519_fe_tobytes canonicalisation (avx/fd_ed25519_fe.c:48-110),
+   returning the 10 reduced limbs (packing is only needed for the two
+   predicates below, which read bit 0 and "all zero"). */
+FD_DEV void fe_reduce( i32 h[10], fe const & f ) {
+  _Pragma("unroll") for( int i=0; i<10; i++ ) h[i] = f.v[i];
+  i32 q = (wmul( h[9], 19 ) + (1<<24)) >> 25;
+  _Pragma("unroll") for( int i=0; i<10; i++ ) q = (h[i] + q) >> ((i&1) ? 25 : 26);
+  h[0] += wmul( q, 19 );
+  _Pragma("unroll") for( int i=0; i<9; i++ ) {
+    int w = (i&1) ? 25 : 26;
+    h[i+1] += h[i] >> w; h[i] &= (i32)((1u<<w)-1u);
+  }
+  h[9] &= (i32)((1u<<25)-1u);
+}
+
+/* fd_ed25519_fe_isnonzero / isnegative (avx/fd_ed25519_fe.h:118-129) */
+FD_DEV bool fe_isnonzero( fe const & f ) {
+  i32 h[10]; fe_reduce( h, f );
+  i32 o = 0; _Pragma("unroll") for( int i=0; i<10; i++ ) o |= h[i];
+  return o != 0;
+}
+FD_DEV int fe_isnegative( fe const & f ) { i32 h[10]; fe_reduce( h, f ); return h[0] & 1; }
+
+/* ------------------------------------------------------------------ */
+/* SHA-512 (FIPS 180-4) of R || A || M, one message per lane.
+   Reference: src/ballet/sha512/fd_sha512.c:264-399. */
+
+__constant__ static u64 const SHA512_K[80] = FD_AMD_SHA512_K;
+
+FD_DEV u64 rotr64( u64 x, int n ) { return (x >> n) | (x << (64-n)); }
+
+FD_DEV void sha512_compress( u64 st[8], u64 w[16] ) {
+  u64 a=st[0], b=st[1], c=st[2], d=st[3], e=st[4], f=st[5], g=st[6], h=st[7];
+  _Pragma("unroll 16")
+  for( int i=0; i<80; i++ ) {
+    u64 wi;
+    if( i < 16 ) wi = w[i & 15];
+    else {
+      u64 w15 = w[(i-15) & 15], w2 = w[(i-2) & 15];
+      u64 s0 = rotr64( w15, 1 ) ^ rotr64( w15, 8 ) ^ (w15 >> 7);
+      u64 s1 = rotr64( w2, 19 ) ^ rotr64( w2, 61 ) ^ (w2 >> 6);
+      wi = w[i & 15] + s0 + w[(i-7) & 15] + s1;
+      w[i & 15] = wi;
+    }
+    u64 S1 = rotr64( e, 14 ) ^ rotr64( e, 18 ) ^ rotr64( e, 41 );
+    u64 ch = (e & f) ^ (~e & g);
+    u64 t1 = h + S1 + ch + SHA512_K[i] + wi;
+    u64 S0 = rotr64( a, 28 ) ^ rotr64( a, 34 ) ^ rotr64( a, 39 );
+    u64 mj = (a & b) ^ (a & c) ^ (b & c);
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+  }
+  st[0]+=a; st[1]+=b; st[2]+=c; st[3]+=d; st[4]+=e; st[5]+=f; st[6]+=g; st[7]+=h;
+}
+
+/* ------------------------------------------------------------------ */
+/* x mod L for a 512-bit x (fd_ed25519_sc_reduce, fd_ed25519_user.c:3-110:
+   canonical result, so any exact reduction is bit-identical). 32-bit word
+   serial Horner: r <- (2^32 r + w) mod L, r kept in 9 x 32-bit limbs. */
+
+FD_DEV void sc_reduce( u32 out[8], u32 const in[16] ) {
+  u32 const Lw[8] = { 0x5cf5d3edu, 0x5812631au, 0xa2f79cd6u, 0x14def9deu, 0u, 0u, 0u, 0x10000000u };
+  u32 r[9] = { 0,0,0,0,0,0,0,0,0 };
+  for( int k=15; k>=0; k-- ) {
+    /* r = r*2^32 + in[k]   (r < L < 2^253 -> r*2^32 < 2^285: 9 limbs) */
+    _Pragma("unroll") for( int i=8; i>0; i-- ) r[i] = r[i-1];
+    r[0] = in[k];
+    /* q ~= floor(r / 2^252) <= 2^33: estimate from the top limbs; it may
+       overshoot floor(r/L) by at most 1 (r/2^252 - r/L < 2^-120 r/2^252). */
+    u64 q = ((u64)r[8] << 4) | (r[7] >> 28);
+    /* r -= q*L */
+    i64 br = 0; u64 carry = 0;
+    _Pragma("unroll") for( int i=0; i<9; i++ ) {
+      u64 lw = (i < 8) ? (u64)Lw[i] : 0u;
+      /* q*L word i: 64x32 -> up to 97 bits; split q */
+      u64 plo = (q & 0xffffffffu) * lw;
+      u64 phi = (q >> 32) * lw;
+      u64 t = plo + carry;
+      u64 c2 = (t < plo) ? 1u : 0u;
+      u32 pw = (u32)t;
+      carry = (t >> 32) + (phi) + (c2 << 32);
+      i64 d = (i64)(u64)r[i] - (i64)(u64)pw + br;
+      r[i] = (u32)d; br = d >> 32;
+    }
+    if( br < 0 ) {   /* overshoot: add L back once */
+      u64 c = 0;
+      _Pragma("unroll") for( int i=0; i<9; i++ ) {
+        u64 s = (u64)r[i] + (i < 8 ? (u64)Lw[i] : 0u) + c; r[i] = (u32)s; c = s >> 32;
+      }
+    }
+  }
+  /* final: r < 2L possible -> conditional subtract */
+  {
+    bool ge = true;
+    _Pragma("unroll") for( int i=7; i>=0; i-- ) { /* lexicographic compare, r[8]==0 here */
+      if( r[i] != Lw[i] ) { ge = r[i] > Lw[i]; break; }
+    }
+    if( r[8] ) ge = true;
+    if( ge ) {
+      i64 br = 0;
+      _Pragma("unroll") for( int i=0; i<8; i++ ) { i64 d = (i64)(u64)r[i] - (i64)(u64)Lw[i] + br; r[i] = (u32)d; br = d >> 32; }
+    }
+  }
+  _Pragma("unroll") for( int i=0; i<8; i++ ) out[i] = r[i];
+}
+
+#endif /* FD_ED25519_DEV_H */

@@ -1,0 +1,209 @@
+"""Python mirror of the reference's ed25519 API over the MI355X engine.
+
+Reference interface: src/ballet/ed25519/fd_ed25519.h (fd_ed25519_verify,
+fd_ed25519_sign, fd_ed25519_public_from_private, fd_ed25519_strerror,
+FD_ED25519_SUCCESS / ERR_SIG / ERR_PUBKEY / ERR_MSG).  Same names, same
+argument meaning, same codes.  Everything here is a thin ctypes layer over
+firedancer_amd/libfd_ed25519_amd.so (include/fd_ed25519_amd.h); the verify
+work always runs in the HIP kernels.  If the library is missing this module
+raises at import of the first call -- there is no CPU fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+FD_ED25519_SUCCESS = 0
+FD_ED25519_ERR_SIG = -1
+FD_ED25519_ERR_PUBKEY = -2
+FD_ED25519_ERR_MSG = -3
+FD_ED25519_SIG_SZ = 64
+MSG_MAX = 1232
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfd_ed25519_amd.so")
+
+_lib = None
+
+c_ulong_p = ctypes.POINTER(ctypes.c_ulong)
+c_void_pp = ctypes.POINTER(ctypes.c_void_p)
+
+
+def lib():
+    """Load the engine library (once).  Raises if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            "firedancer_amd: %s missing -- build it with __graft_entry__.build() "
+            "(the verify engine is HIP-only; there is no CPU path)" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
+    vp, ul, ui, i = ctypes.c_void_p, ctypes.c_ulong, ctypes.c_uint, ctypes.c_int
+    L.fd_ed25519_verify.argtypes = [vp, ul, vp, vp, vp]
+    L.fd_ed25519_verify.restype = i
+    L.fd_ed25519_strerror.argtypes = [i]
+    L.fd_ed25519_strerror.restype = ctypes.c_char_p
+    L.fd_ed25519_public_from_private.argtypes = [vp, vp, vp]
+    L.fd_ed25519_public_from_private.restype = vp
+    L.fd_ed25519_sign.argtypes = [vp, vp, ul, vp, vp, vp]
+    L.fd_ed25519_sign.restype = vp
+    L.fd_ed25519_amd_new.argtypes = [i, ul, ul]
+    L.fd_ed25519_amd_new.restype = vp
+    L.fd_ed25519_amd_delete.argtypes = [vp]
+    L.fd_ed25519_amd_delete.restype = None
+    L.fd_ed25519_amd_verify_batch.argtypes = [vp, ul, c_void_pp, c_ulong_p, c_void_pp, c_void_pp, vp]
+    L.fd_ed25519_amd_verify_batch.restype = i
+    L.fd_ed25519_amd_verify_soa.argtypes = [vp, ul, vp, vp, vp, vp, vp, ul, vp]
+    L.fd_ed25519_amd_verify_soa.restype = i
+    L.fd_ed25519_amd_workspace_footprint.argtypes = [ul]
+    L.fd_ed25519_amd_workspace_footprint.restype = ul
+    L.fd_ed25519_amd_verify_dev.argtypes = [ul, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.fd_ed25519_amd_verify_dev.restype = i
+    L.fd_ed25519_amd_work_stats_dev.argtypes = [ul, vp, vp, vp]
+    L.fd_ed25519_amd_work_stats_dev.restype = i
+    L.fd_ed25519_amd_version.argtypes = []
+    L.fd_ed25519_amd_version.restype = ctypes.c_char_p
+    L.fd_ed25519_amd_sign_batch.argtypes = [ul, vp, vp, vp, vp, vp, vp, i]
+    L.fd_ed25519_amd_sign_batch.restype = i
+    _lib = L
+    return L
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None and a.size else ctypes.c_void_p(0)
+
+
+def _u8(b):
+    return np.frombuffer(bytes(b), np.uint8)
+
+
+# ---------------------------------------------------------------- reference API
+
+def strerror(err):
+    """fd_ed25519_strerror (fd_ed25519.h:108-109)."""
+    return lib().fd_ed25519_strerror(int(err)).decode()
+
+
+def verify(msg, sig, public_key):
+    """fd_ed25519_verify (fd_ed25519.h:96-101): returns 0 or FD_ED25519_ERR_*.
+    Runs on the GPU as a batch of one."""
+    m = bytes(msg)
+    s = bytes(sig)
+    p = bytes(public_key)
+    assert len(s) == 64 and len(p) == 32
+    mb = ctypes.create_string_buffer(m, max(len(m), 1))
+    return lib().fd_ed25519_verify(mb if m else None, len(m), s, p, None)
+
+
+def public_from_private(private_key):
+    """fd_ed25519_public_from_private (fd_ed25519.h:40-44)."""
+    out = ctypes.create_string_buffer(32)
+    lib().fd_ed25519_public_from_private(out, bytes(private_key), None)
+    return out.raw
+
+
+def sign(msg, public_key, private_key):
+    """fd_ed25519_sign (fd_ed25519.h:71-78) -> 64-byte signature."""
+    out = ctypes.create_string_buffer(64)
+    m = bytes(msg)
+    lib().fd_ed25519_sign(out, m if m else None, len(m), bytes(public_key), bytes(private_key), None)
+    return out.raw
+
+
+def sign_batch(prv, blob, msg_off, msg_sz, nthread=None):
+    """Keygen + sign n messages on host threads: prv (n,32) u8 -> pub (n,32), sig (n,64)."""
+    prv = np.ascontiguousarray(prv, np.uint8)
+    n = prv.shape[0]
+    blob = np.ascontiguousarray(blob, np.uint8)
+    off = np.ascontiguousarray(msg_off, np.uint32)
+    sz = np.ascontiguousarray(msg_sz, np.uint32)
+    pub = np.zeros((n, 32), np.uint8)
+    sig = np.zeros((n, 64), np.uint8)
+    if nthread is None:
+        nthread = min(16, os.cpu_count() or 1)
+    rc = lib().fd_ed25519_amd_sign_batch(n, _ptr(prv), _ptr(blob), _ptr(off), _ptr(sz), _ptr(pub), _ptr(sig), nthread)
+    assert rc == 0
+    return pub, sig
+
+
+# ---------------------------------------------------------------- batch engine
+
+class EngineError(RuntimeError):
+    pass
+
+
+class Engine:
+    """fd_ed25519_amd_t: one engine per device (multi-GPU = one per device)."""
+
+    def __init__(self, device=0, batch_max=1 << 16, blob_max=None):
+        if blob_max is None:
+            blob_max = max(batch_max * 256, MSG_MAX)
+        self._h = lib().fd_ed25519_amd_new(int(device), int(batch_max), int(blob_max))
+        if not self._h:
+            raise EngineError("fd_ed25519_amd_new(device=%d) failed (no HIP device?)" % device)
+        self.device = device
+
+    def close(self):
+        if self._h:
+            lib().fd_ed25519_amd_delete(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def verify_soa(self, pub, sig, msg_off, msg_sz, blob):
+        pub = np.ascontiguousarray(pub, np.uint8)
+        sig = np.ascontiguousarray(sig, np.uint8)
+        off = np.ascontiguousarray(msg_off, np.uint32)
+        sz = np.ascontiguousarray(msg_sz, np.uint32)
+        blob = np.ascontiguousarray(blob, np.uint8)
+        n = int(pub.shape[0])
+        err = np.zeros(n, np.int8)
+        rc = lib().fd_ed25519_amd_verify_soa(self._h, n, _ptr(pub), _ptr(sig), _ptr(off), _ptr(sz),
+                                             _ptr(blob), int(blob.size), _ptr(err))
+        if rc:
+            raise EngineError("fd_ed25519_amd_verify_soa rc=%d" % rc)
+        return err
+
+    def verify_batch(self, msgs, sigs, pubs):
+        """Pointer-array form: lists of bytes-like."""
+        n = len(msgs)
+        keep = [bytes(m) for m in msgs] + [bytes(s) for s in sigs] + [bytes(p) for p in pubs]
+        bufs = [ctypes.create_string_buffer(b, max(len(b), 1)) for b in keep]
+        mp = (ctypes.c_void_p * max(n, 1))(*[ctypes.cast(b, ctypes.c_void_p) for b in bufs[:n]])
+        sp = (ctypes.c_void_p * max(n, 1))(*[ctypes.cast(b, ctypes.c_void_p) for b in bufs[n:2 * n]])
+        pp = (ctypes.c_void_p * max(n, 1))(*[ctypes.cast(b, ctypes.c_void_p) for b in bufs[2 * n:]])
+        sz = (ctypes.c_ulong * max(n, 1))(*[len(b) for b in keep[:n]])
+        err = np.zeros(max(n, 1), np.int8)
+        rc = lib().fd_ed25519_amd_verify_batch(self._h, n, mp, sz, sp, pp, _ptr(err))
+        if rc:
+            raise EngineError("fd_ed25519_amd_verify_batch rc=%d" % rc)
+        return err[:n]
+
+
+# ---------------------------------------------------------------- device-resident path
+
+def workspace_footprint(n):
+    return int(lib().fd_ed25519_amd_workspace_footprint(int(n)))
+
+
+def verify_dev(n, d_pub, d_sig, d_off, d_sz, d_blob, d_err, d_ws, stream=0):
+    """All arguments are device pointers (ints, e.g. torch tensor .data_ptr());
+    enqueued on `stream` (hipStream_t as int), not synchronised."""
+    rc = lib().fd_ed25519_amd_verify_dev(int(n), d_pub, d_sig, d_off, d_sz, d_blob, d_err, d_ws, stream)
+    if rc:
+        raise EngineError("fd_ed25519_amd_verify_dev rc=%d" % rc)
+
+
+def work_stats_dev(n, d_ws, d_stats, stream=0):
+    rc = lib().fd_ed25519_amd_work_stats_dev(int(n), d_ws, d_stats, stream)
+    if rc:
+        raise EngineError("fd_ed25519_amd_work_stats_dev rc=%d" % rc)
+
+
+def version():
+    return lib().fd_ed25519_amd_version().decode()

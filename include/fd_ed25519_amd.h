@@ -1,0 +1,179 @@
+#ifndef HEADER_fd_ed25519_amd_h
+#define HEADER_fd_ed25519_amd_h
+
+/* MI355X ed25519 batch-verification engine -- the C-ABI drop-in boundary.
+ *
+ * Library: firedancer_amd/libfd_ed25519_amd.so (hipcc, gfx950).
+ *
+ * Part 1 reproduces the reference's public API for the verify path
+ * (lijunwangs/firedancer src/ballet/ed25519/fd_ed25519.h), same names,
+ * same argument meaning, same return codes, so an existing caller (the
+ * verify tile, the Rust re-export ffi/rust/firedancer-sys/src/ballet/
+ * ed25519.rs:1-10) relinks against this library unchanged.  Verdicts are
+ * bit-exact with the reference's DEFAULT x86_64 (AVX) build, including its
+ * documented non-strict behaviours.
+ *
+ * Part 2 is new: batch entry points (the reference only verifies one
+ * signature per call).  Every verdict they return equals what Part 1's
+ * fd_ed25519_verify returns for the same inputs.
+ *
+ * All verify work runs on the GPU.  There is no CPU fallback: without a
+ * usable HIP device every verify entry point returns FD_ED25519_AMD_ERR_DEVICE
+ * (batch API) or aborts with a message (drop-in API, which has no error code
+ * for "no device").
+ */
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef unsigned char uchar;
+typedef unsigned long ulong;
+typedef unsigned int  uint;
+typedef signed char   schar;
+
+/* ===== Part 1: reference API (src/ballet/ed25519/fd_ed25519.h) ===== */
+
+/* fd_ed25519.h:11-14 */
+#define FD_ED25519_SUCCESS    ( 0) /* Operation was succesful */
+#define FD_ED25519_ERR_SIG    (-1) /* signature obviously invalid (s check) */
+#define FD_ED25519_ERR_PUBKEY (-2) /* public key (or R) failed to decompress */
+#define FD_ED25519_ERR_MSG    (-3) /* message didn't match the signature */
+
+/* fd_ed25519.h:17-20 */
+#define FD_ED25519_SIG_SZ (64UL)
+typedef uchar fd_ed25519_sig_t[ FD_ED25519_SIG_SZ ];
+
+/* The reference passes a caller-owned SHA-512 calculator as scratch
+   (fd_ed25519.h:81-95; src/ballet/sha512/fd_sha512.h:15-16,56-77: 256 B,
+   128-aligned).  This library hashes on the GPU and only takes the
+   reference's write interest in it; it never dereferences it.  A caller
+   that already includes the reference's fd_sha512.h keeps its definition. */
+#ifndef FD_SHA512_ALIGN
+#define FD_SHA512_ALIGN     (128UL)
+#define FD_SHA512_FOOTPRINT (256UL)
+typedef struct fd_sha512_private fd_sha512_t;
+#endif
+
+/* fd_ed25519_verify -- replaces fd_ed25519.h:96-101 (impl
+   fd_ed25519_user.c:345-431).  Returns FD_ED25519_SUCCESS or an
+   FD_ED25519_ERR_* code, bit-exact with the reference.  Reentrant; runs as
+   a batch of one on the calling thread's default engine (device 0 unless
+   FD_ED25519_AMD_DEVICE is set).  msg==NULL fine when sz==0. */
+int
+fd_ed25519_verify( void const *  msg,
+                   ulong         sz,
+                   void const *  sig,
+                   void const *  public_key,
+                   fd_sha512_t * sha );
+
+/* fd_ed25519_strerror -- replaces fd_ed25519.h:108-109 (impl
+   fd_ed25519_user.c:433-443): same strings. */
+char const *
+fd_ed25519_strerror( int err );
+
+/* fd_ed25519_public_from_private / fd_ed25519_sign -- replace
+   fd_ed25519.h:40-78 (impl fd_ed25519_user.c:279-343).  Host-side (not
+   the verify hot path); deterministic RFC 8032 signing, so the bytes equal
+   the reference's. */
+void *
+fd_ed25519_public_from_private( void *        public_key,
+                                void const *  private_key,
+                                fd_sha512_t * sha );
+
+void *
+fd_ed25519_sign( void *        sig,
+                 void const *  msg,
+                 ulong         sz,
+                 void const *  public_key,
+                 void const *  private_key,
+                 fd_sha512_t * sha );
+
+/* ===== Part 2: batch engine (new) ===== */
+
+#define FD_ED25519_AMD_OK          ( 0)
+#define FD_ED25519_AMD_ERR_INVAL   (-10) /* bad argument (NULL, n too large, msg too large) */
+#define FD_ED25519_AMD_ERR_DEVICE  (-11) /* HIP error / no device */
+
+/* Largest message accepted per signature (Solana MTU). */
+#define FD_ED25519_AMD_MSG_MAX     (1232UL)
+
+typedef struct fd_ed25519_amd fd_ed25519_amd_t;
+
+/* Create an engine bound to HIP device `device`, able to verify up to
+   batch_max signatures whose messages total at most blob_max bytes per
+   call (larger calls are split internally).  Owns its HIP stream, device
+   buffers and pinned, double-buffered host staging.  NULL on failure.
+   One engine per host thread; engines on different devices run
+   independently (multi-GPU = one engine per device). */
+fd_ed25519_amd_t *
+fd_ed25519_amd_new( int device, ulong batch_max, ulong blob_max );
+
+void
+fd_ed25519_amd_delete( fd_ed25519_amd_t * eng );
+
+/* Pointer-array batch (the shape of n independent fd_ed25519_verify
+   calls): msg[i] (sz[i] bytes), sig[i] (64 B), pub[i] (32 B) -> err[i]
+   in {0,-1,-2,-3}.  Host memory, caller-owned, read-only except err.
+   Returns FD_ED25519_AMD_OK or a negative FD_ED25519_AMD_ERR_*. */
+int
+fd_ed25519_amd_verify_batch( fd_ed25519_amd_t *   eng,
+                             ulong                n,
+                             void const * const * msg,
+                             ulong const *        sz,
+                             void const * const * sig,
+                             void const * const * pub,
+                             schar *              err );
+
+/* SoA host batch: pub[n][32], sig[n][64], message i is
+   blob[msg_off[i] .. msg_off[i]+msg_sz[i]).  Staged through pinned memory
+   (double-buffered, copies overlap the previous chunk's kernels). */
+int
+fd_ed25519_amd_verify_soa( fd_ed25519_amd_t * eng,
+                           ulong              n,
+                           uchar const *      pub,
+                           uchar const *      sig,
+                           uint const *       msg_off,
+                           uint const *       msg_sz,
+                           uchar const *      blob,
+                           ulong              blob_sz,
+                           schar *            err );
+
+/* Device-resident batch: every pointer is HIP device memory, already
+   resident (the layout of fd_ed25519_amd_verify_soa).  Enqueues the
+   verify kernels on `stream` (hipStream_t, NULL = default stream) and
+   returns without synchronising.  `ws` is device scratch of at least
+   fd_ed25519_amd_workspace_footprint(n) bytes, 256-aligned. */
+ulong
+fd_ed25519_amd_workspace_footprint( ulong n );
+
+int
+fd_ed25519_amd_verify_dev( ulong         n,
+                           uchar const * d_pub,
+                           uchar const * d_sig,
+                           uint const *  d_msg_off,
+                           uint const *  d_msg_sz,
+                           uchar const * d_blob,
+                           schar *       d_err,
+                           void *        d_ws,
+                           void *        stream );
+
+/* Optional per-signature work statistics of the last device-resident call
+   on the same workspace (3 x uint per signature: double-scalar-multiply
+   loop iterations, nonzero h digits, nonzero s digits) -- used to report
+   the algorithmic multiply count.  Device pointer, n*3
+   uints; enqueued on `stream`. */
+int
+fd_ed25519_amd_work_stats_dev( ulong n, void const * d_ws, uint * d_stats, void * stream );
+
+/* Library version / build string. */
+char const *
+fd_ed25519_amd_version( void );
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HEADER_fd_ed25519_amd_h */
