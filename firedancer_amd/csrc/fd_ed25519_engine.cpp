@@ -140,7 +140,7 @@ slot_launch( slot_t * s, ulong n, ulong blob_sz, schar * out ) {
   HIPCHK( hipMemcpyAsync( s->d_off,  s->h_off,  4UL*n,  hipMemcpyHostToDevice, s->stream ) );
   HIPCHK( hipMemcpyAsync( s->d_sz,   s->h_sz,   4UL*n,  hipMemcpyHostToDevice, s->stream ) );
   if( blob_sz ) HIPCHK( hipMemcpyAsync( s->d_blob, s->h_blob, blob_sz, hipMemcpyHostToDevice, s->stream ) );
-  if( fd_amd_launch_verify( (uint32_t)n, s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_blob, s->d_err, s->d_ws, s->stream, 1 ) )
+  if( fd_amd_launch_verify( (uint32_t)n, s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_blob, s->d_err, s->d_ws, s->stream, 1, NULL ) )
     return FD_ED25519_AMD_ERR_DEVICE;
   HIPCHK( hipMemcpyAsync( s->h_err, s->d_err, n, hipMemcpyDeviceToHost, s->stream ) );
   HIPCHK( hipEventRecord( s->done, s->stream ) );
@@ -210,7 +210,20 @@ fd_ed25519_amd_verify_dev( ulong n, uchar const * d_pub, uchar const * d_sig, ui
   if( !n ) return FD_ED25519_AMD_OK;
   if( !d_pub || !d_sig || !d_msg_off || !d_msg_sz || !d_blob || !d_err || !d_ws ) return FD_ED25519_AMD_ERR_INVAL;
   if( fd_amd_launch_verify( (uint32_t)n, d_pub, d_sig, d_msg_off, d_msg_sz, d_blob, (int8_t *)d_err, d_ws,
-                            (hipStream_t)stream, 1 ) )
+                            (hipStream_t)stream, 1, NULL ) )
+    return FD_ED25519_AMD_ERR_DEVICE;
+  return FD_ED25519_AMD_OK;
+}
+
+extern "C" int
+fd_ed25519_amd_verify_dev_ev( ulong n, uchar const * d_pub, uchar const * d_sig, uint const * d_msg_off,
+                              uint const * d_msg_sz, uchar const * d_blob, schar * d_err, void * d_ws, void * stream,
+                              void * const * ev ) {
+  if( n > 0xFFFFFFFFUL ) return FD_ED25519_AMD_ERR_INVAL;
+  if( !n ) return FD_ED25519_AMD_OK;
+  if( !d_pub || !d_sig || !d_msg_off || !d_msg_sz || !d_blob || !d_err || !d_ws ) return FD_ED25519_AMD_ERR_INVAL;
+  if( fd_amd_launch_verify( (uint32_t)n, d_pub, d_sig, d_msg_off, d_msg_sz, d_blob, (int8_t *)d_err, d_ws,
+                            (hipStream_t)stream, 1, (hipEvent_t const *)ev ) )
     return FD_ED25519_AMD_ERR_DEVICE;
   return FD_ED25519_AMD_OK;
 }

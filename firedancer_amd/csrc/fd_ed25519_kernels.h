@@ -15,9 +15,10 @@ typedef struct {
 
 ws_layout_t fd_amd_ws_layout( size_t n );
 
-/* Enqueue k_prep -> k_decomp -> k_dsm on `stream`.  0 on success. */
+/* Enqueue k_prep -> k_decomp -> k_dsm on `stream`; when ev != NULL record
+   ev[0..3] before/between/after the three kernels.  0 on success. */
 int fd_amd_launch_verify( uint32_t n, uint8_t const * d_pub, uint8_t const * d_sig, uint32_t const * d_off,
                           uint32_t const * d_sz, uint8_t const * d_blob, int8_t * d_err, void * d_ws,
-                          hipStream_t stream, int want_stats );
+                          hipStream_t stream, int want_stats, hipEvent_t const * ev /* 4 or NULL */ );
 
 #endif

@@ -421,13 +421,18 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
 
 int
 fd_amd_launch_verify( u32 n, u8 const * d_pub, u8 const * d_sig, u32 const * d_off, u32 const * d_sz,
-                      u8 const * d_blob, i8 * d_err, void * d_ws, hipStream_t stream, int want_stats ) {
+                      u8 const * d_blob, i8 * d_err, void * d_ws, hipStream_t stream, int want_stats,
+                      hipEvent_t const * ev ) {
   if( !n ) return 0;
   ws_layout_t L = fd_amd_ws_layout( n );
   u8 * ws = (u8 *)d_ws;
   u32 nb = (n + 63u) / 64u;
+  if( ev ) (void)hipEventRecord( ev[0], stream );
   hipLaunchKernelGGL( k_prep,   dim3(nb),      dim3(64), 0, stream, n, d_pub, d_sig, d_off, d_sz, d_blob, d_err, ws, L );
+  if( ev ) (void)hipEventRecord( ev[1], stream );
   hipLaunchKernelGGL( k_decomp, dim3(2u*nb),   dim3(64), 0, stream, n, d_pub, d_sig, d_err, ws, L );
+  if( ev ) (void)hipEventRecord( ev[2], stream );
   hipLaunchKernelGGL( k_dsm,    dim3(nb),      dim3(64), 0, stream, n, d_err, ws, L, want_stats );
+  if( ev ) (void)hipEventRecord( ev[3], stream );
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

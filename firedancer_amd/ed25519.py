@@ -60,6 +60,8 @@ def lib():
     L.fd_ed25519_amd_workspace_footprint.restype = ul
     L.fd_ed25519_amd_verify_dev.argtypes = [ul, vp, vp, vp, vp, vp, vp, vp, vp]
     L.fd_ed25519_amd_verify_dev.restype = i
+    L.fd_ed25519_amd_verify_dev_ev.argtypes = [ul, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.fd_ed25519_amd_verify_dev_ev.restype = i
     L.fd_ed25519_amd_work_stats_dev.argtypes = [ul, vp, vp, vp]
     L.fd_ed25519_amd_work_stats_dev.restype = i
     L.fd_ed25519_amd_version.argtypes = []
@@ -197,6 +199,17 @@ def verify_dev(n, d_pub, d_sig, d_off, d_sz, d_blob, d_err, d_ws, stream=0):
     rc = lib().fd_ed25519_amd_verify_dev(int(n), d_pub, d_sig, d_off, d_sz, d_blob, d_err, d_ws, stream)
     if rc:
         raise EngineError("fd_ed25519_amd_verify_dev rc=%d" % rc)
+
+
+def verify_dev_ev(n, d_pub, d_sig, d_off, d_sz, d_blob, d_err, d_ws, stream, events):
+    """verify_dev recording 4 HIP events (hip.Event) around/between the
+    three kernels on `stream`."""
+    arr = None
+    if events is not None:
+        arr = (ctypes.c_void_p * 4)(*[e.handle for e in events])
+    rc = lib().fd_ed25519_amd_verify_dev_ev(int(n), d_pub, d_sig, d_off, d_sz, d_blob, d_err, d_ws, stream, arr)
+    if rc:
+        raise EngineError("fd_ed25519_amd_verify_dev_ev rc=%d" % rc)
 
 
 def work_stats_dev(n, d_ws, d_stats, stream=0):

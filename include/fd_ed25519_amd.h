@@ -160,13 +160,41 @@ fd_ed25519_amd_verify_dev( ulong         n,
                            void *        d_ws,
                            void *        stream );
 
+/* Same as fd_ed25519_amd_verify_dev; when ev != NULL it points to 4
+   hipEvent_t that are recorded on `stream` before k_prep, between the
+   stages and after k_dsm (per-stage kernel timing for the bench). */
+int
+fd_ed25519_amd_verify_dev_ev( ulong         n,
+                              uchar const * d_pub,
+                              uchar const * d_sig,
+                              uint const *  d_msg_off,
+                              uint const *  d_msg_sz,
+                              uchar const * d_blob,
+                              schar *       d_err,
+                              void *        d_ws,
+                              void *        stream,
+                              void * const * ev );
+
 /* Optional per-signature work statistics of the last device-resident call
-   on the same workspace (3 x uint per signature: double-scalar-multiply
-   loop iterations, nonzero h digits, nonzero s digits) -- used to report
-   the algorithmic multiply count.  Device pointer, n*3
-   uints; enqueued on `stream`. */
+   on the same workspace: d_stats is planar [3][n] uint (double-scalar-
+   multiply loop iterations, nonzero h digits, nonzero s digits; zeros for
+   signatures decided before the multiply) -- used to report the
+   algorithmic multiply count.  Enqueued on `stream`. */
 int
 fd_ed25519_amd_work_stats_dev( ulong n, void const * d_ws, uint * d_stats, void * stream );
+
+/* Host-side batch keygen + sign over the SoA layout (workload synthesis;
+   not the verify path): prv[n][32] -> pub[n][32], sig[n][64] over
+   blob[msg_off[i] .. +msg_sz[i]), on nthread host threads.  Returns 0. */
+int
+fd_ed25519_amd_sign_batch( ulong         n,
+                           uchar const * prv,
+                           uchar const * blob,
+                           uint const *  msg_off,
+                           uint const *  msg_sz,
+                           uchar *       pub,
+                           uchar *       sig,
+                           int           nthread );
 
 /* Library version / build string. */
 char const *

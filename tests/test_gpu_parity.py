@@ -108,29 +108,27 @@ def test_random_mixed_vs_oracle(engine):
 
 
 def test_device_resident_path_and_stats():
-    """fd_ed25519_amd_verify_dev on torch device buffers (the bench path),
-    plus the work statistics against the oracle's instrumented counts."""
-    import torch
-    from firedancer_amd import ed25519
+    """fd_ed25519_amd_verify_dev on device buffers (the bench path), plus the
+    work statistics against the oracle's instrumented counts."""
+    from firedancer_amd import ed25519, hip
     b = _sign_stream(99, 4096, 200, 200, True)
-    dev = torch.device("cuda", 0)
-    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
-         dict(pub=b.pub, sig=b.sig, off=b.msg_off.view(np.int32), sz=b.msg_sz.view(np.int32), blob=b.blob).items()}
     n = len(b)
-    err = torch.zeros(n, dtype=torch.int8, device=dev)
-    ws = torch.empty(ed25519.workspace_footprint(n), dtype=torch.uint8, device=dev)
-    stats = torch.zeros(3 * n, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    ed25519.verify_dev(n, t["pub"].data_ptr(), t["sig"].data_ptr(), t["off"].data_ptr(), t["sz"].data_ptr(),
-                       t["blob"].data_ptr(), err.data_ptr(), ws.data_ptr(), stream)
-    ed25519.work_stats_dev(n, ws.data_ptr(), stats.data_ptr(), stream)
-    torch.cuda.synchronize()
+    d = {k: hip.DeviceBuffer.from_array(v) for k, v in
+         dict(pub=b.pub, sig=b.sig, off=b.msg_off, sz=b.msg_sz, blob=b.blob).items()}
+    err = hip.DeviceBuffer(n)
+    ws = hip.DeviceBuffer(ed25519.workspace_footprint(n))
+    stats = hip.DeviceBuffer(4 * 3 * n)
+    stream = hip.Stream()
+    evs = [hip.Event() for _ in range(4)]
+    ed25519.verify_dev_ev(n, d["pub"].ptr, d["sig"].ptr, d["off"].ptr, d["sz"].ptr, d["blob"].ptr,
+                          err.ptr, ws.ptr, stream.handle, evs)
+    ed25519.work_stats_dev(n, ws.ptr, stats.ptr, stream.handle)
+    stream.synchronize()
+    assert all(evs[j].elapsed_ms(evs[j + 1]) > 0 for j in range(3))
     exp, st = _oracle.verify_batch(b, stats=True)
-    assert np.array_equal(err.cpu().numpy(), exp)
-    got = stats.cpu().numpy().view(np.uint32).reshape(3, n).T
-    pend = exp != -1
-    pend &= exp != -2
-    assert np.array_equal(got[pend], st[pend])
+    assert np.array_equal(err.to_array(np.int8, n), exp)
+    got = stats.to_array(np.uint32, 3 * n).reshape(3, n).T
+    assert np.array_equal(got, st)
 
 
 def test_large_batch_properties(engine):
