@@ -238,6 +238,16 @@ fd_ed25519_amd_work_stats_dev( ulong n, void const * d_ws, uint * d_stats, void 
   return FD_ED25519_AMD_OK;
 }
 
+extern "C" int
+fd_ed25519_amd_debug_digits_dev( ulong n, void const * d_ws, ushort * d_dig, int * d_top, void * stream ) {
+  if( !n ) return FD_ED25519_AMD_OK;
+  ws_layout_t L = fd_amd_ws_layout( n );
+  uint8_t const * ws = (uint8_t const *)d_ws;
+  HIPCHK( hipMemcpyAsync( d_dig, ws + L.dig, 512UL*n, hipMemcpyDeviceToDevice, (hipStream_t)stream ) );
+  HIPCHK( hipMemcpyAsync( d_top, ws + L.top, 4UL*n,   hipMemcpyDeviceToDevice, (hipStream_t)stream ) );
+  return FD_ED25519_AMD_OK;
+}
+
 /* ------------------------------------------------------------------ */
 /* drop-in reference API                                                */
 

@@ -11,16 +11,17 @@
  *            per point (A and R of a signature on adjacent lanes), then the
  *            A := -A negation (user.c:406-407).
  *   k_dsm    [h](-A) + [s]B with the reference's AVX op flow
- *            (avx/fd_ed25519_ge.c:408-527; the Ai table in a per-lane HBM
- *            slab, the Bi table in LDS) and the limb compare
- *            (user.c:417-425).
+ *            (avx/fd_ed25519_ge.c:408-527) run as a per-lane op stream (no
+ *            predicated adds; the Ai table in a per-lane HBM slab, the Bi
+ *            table in LDS) and the limb compare (user.c:417-425).
  *
  * Verdict per signature: err[i] in {0,-1,-2,-3}; 1 marks "still pending"
  * between kernels.
  *
  * Workspace layout (N = n rounded up to 64; every plane is [element][N] so
  * that the 64 lanes of a wave touch 64 consecutive elements):
- *   dig  : int8   [2][256][N]  slide digits of h (plane 0) and s (plane 1)
+ *   dig  : u16    [N][256]     slide digit pairs (a_p = h digit, b_p = s digit) as
+ *                              int8 (low, high), contiguous per lane
  *   top  : int32  [N]          highest nonzero digit position (-1 if none)
  *   A    : int32  [30][N]      -A.X, A.Y, -A.T   (A.Z == 1)
  *   R    : int32  [20][N]      R.X, R.Y
@@ -32,6 +33,7 @@
 #include "fd_ed25519_kernels.h"
 
 typedef int8_t i8;
+typedef uint16_t u16;
 
 /* ------------------------------------------------------------------ */
 /* workspace                                                            */
@@ -44,7 +46,7 @@ fd_amd_ws_layout( size_t n ) {
   size_t N = (n + 63UL) & ~(size_t)63UL; if( !N ) N = 64;
   size_t o = 0;
   L.N   = N;
-  L.dig = o; o = ws_al( o + 2UL*256UL*N );
+  L.dig = o; o = ws_al( o + 2UL*256UL*N );   /* u16 [N][256] */
   L.top = o; o = ws_al( o + 4UL*N );
   L.A   = o; o = ws_al( o + 4UL*30UL*N );
   L.R   = o; o = ws_al( o + 4UL*20UL*N );
@@ -57,44 +59,71 @@ fd_amd_ws_layout( size_t n ) {
 /* ------------------------------------------------------------------ */
 /* k_prep                                                               */
 
-/* byte p of the SHA input stream R || A || M || pad || len */
-__device__ __forceinline__ u32
-stream_byte( u32 p, u8 const * __restrict__ sig, u8 const * __restrict__ pub,
-             u8 const * __restrict__ msg, u32 sz, u32 padded ) {
-  if( p < 32u ) return sig[p];
-  if( p < 64u ) return pub[p-32u];
-  u32 m = p - 64u;
-  if( m < sz ) return msg[m];
-  if( m == sz ) return 0x80u;
-  if( p >= padded - 8u ) {                 /* low 64 bits of the 128-bit bit-length */
-    u64 bits = (u64)(64u + sz) << 3;
-    u32 k = padded - 1u - p;               /* byte k of the big-endian length, from the end */
-    return (u32)(bits >> (8u*k)) & 0xffu;
-  }
-  return 0u;
+/* 8 bytes of the padded message starting at message offset o (multiple of
+   8), little-endian: message bytes, the 0x80 terminator at offset sz, zeros
+   after.  Only dwords that intersect [0, sz) are loaded. */
+__device__ __forceinline__ u64
+msg_word( u8 const * __restrict__ m, u32 sz, u32 o ) {
+  uintptr_t a  = (uintptr_t)(m + o);
+  u32 sh = (u32)(a & 3u);
+  u32 const * p = (u32 const *)(a - sh);   /* dword j covers message bytes [o-sh+4j, o-sh+4j+4) */
+  u32 d0 = (o       < sz + sh)         ? p[0] : 0u;
+  u32 d1 = (o + 4u  < sz + sh)         ? p[1] : 0u;
+  u32 d2 = (sh && o + 8u < sz + sh)    ? p[2] : 0u;
+  u32 lo = __builtin_amdgcn_alignbyte( d1, d0, sh );
+  u32 hi = __builtin_amdgcn_alignbyte( d2, d1, sh );
+  u64 w = ((u64)hi << 32) | lo;
+  if( sz >= o + 8u ) return w;                                /* 8 message bytes */
+  if( sz <  o      ) return 0UL;                              /* past the terminator */
+  u32 nv = sz - o;                                            /* 0..7 message bytes, then 0x80 */
+  return (w & ((1UL << (8u*nv)) - 1UL)) | (0x80UL << (8u*nv));
 }
 
-/* fd_ed25519_ge_slide (avx/fd_ed25519_ge.c:378-400) on an LDS column:
-   r[i] lives at lds[i*64 + lane]. */
+__device__ __forceinline__ u64 bswap64( u64 x ) {
+  return ((u64)__builtin_bswap32( (u32)x ) << 32) | (u64)__builtin_bswap32( (u32)(x >> 32) );
+}
+
+/* fd_ed25519_ge_slide (avx/fd_ed25519_ge.c:378-400) on a 256-bit register
+   shift window: bit 0 of w0 is always position `pos`, so every look-ahead
+   index is static.  The reference's carry loop "for k>=i+b: if !r[k] set,
+   break; else clear" is the big-integer increment B += 2^(i+b).  Scalars
+   are < 2^253 so no carry leaves position 255.  emit(pos, digit). */
+template<typename EMIT>
 __device__ __forceinline__ void
-slide_lds( i8 * lds, int lane, u32 const a[8] ) {
-  for( int i=0; i<256; i++ ) lds[i*64 + lane] = (i8)((a[i>>5] >> (i&31)) & 1u);
-  for( int i=0; i<256; i++ ) {
-    int ri = lds[i*64 + lane];
-    if( !ri ) continue;
-    for( int b=1; b<=6 && i+b<256; b++ ) {
-      int rb = lds[(i+b)*64 + lane];
-      if( !rb ) continue;
-      if( ri + (rb << b) <= 15 ) { ri += rb << b; lds[(i+b)*64 + lane] = 0; }
-      else if( ri - (rb << b) >= -15 ) {
-        ri -= rb << b;
-        for( int k=i+b; k<256; k++ ) {
-          if( !lds[k*64 + lane] ) { lds[k*64 + lane] = 1; break; }
-          lds[k*64 + lane] = 0;
-        }
-      } else break;
+slide_reg( u32 const a[8], EMIT emit ) {
+  u64 w0 = ((u64)a[1] << 32) | a[0], w1 = ((u64)a[3] << 32) | a[2];
+  u64 w2 = ((u64)a[5] << 32) | a[4], w3 = ((u64)a[7] << 32) | a[6];
+  int pos = 0;
+  while( (w0 | w1 | w2 | w3) != 0UL ) {
+    /* skip to the next set bit */
+    while( w0 == 0UL ) { w0 = w1; w1 = w2; w2 = w3; w3 = 0UL; pos += 64; }
+    int tz = __builtin_ctzll( w0 );
+    if( tz ) {
+      w0 = (w0 >> tz) | (w1 << (64 - tz));
+      w1 = (w1 >> tz) | (w2 << (64 - tz));
+      w2 = (w2 >> tz) | (w3 << (64 - tz));
+      w3 = (w3 >> tz);
+      pos += tz;
     }
-    lds[i*64 + lane] = (i8)ri;
+    int r = 1; w0 &= ~1UL;
+    bool stop = false;
+    _Pragma("unroll")
+    for( int b=1; b<=6; b++ ) {
+      bool bit = !stop && ((w0 >> b) & 1UL);
+      if( bit ) {
+        if( r + (1 << b) <= 15 ) { r += 1 << b; w0 &= ~(1UL << b); }
+        else if( r - (1 << b) >= -15 ) {
+          r -= 1 << b;
+          u64 n0 = w0 + (1UL << b);                 /* B += 2^b (carry chain) */
+          u64 c  = n0 < w0;
+          w0 = n0; w1 += c; c = c && w1 == 0UL; w2 += c; c = c && w2 == 0UL; w3 += c;
+        } else stop = true;
+      }
+    }
+    emit( pos, r );
+    /* step past pos */
+    w0 = (w0 >> 1) | (w1 << 63); w1 = (w1 >> 1) | (w2 << 63); w2 = (w2 >> 1) | (w3 << 63); w3 >>= 1;
+    pos += 1;
   }
 }
 
@@ -102,85 +131,74 @@ __global__ void __launch_bounds__(64)
 k_prep( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
         u32 const * __restrict__ msg_off, u32 const * __restrict__ msg_sz,
         u8 const * __restrict__ blob, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L ) {
-  __shared__ i8 lds[256*64];
-  int lane = (int)threadIdx.x;
-  u32 i = blockIdx.x * 64u + (u32)lane;
-  bool live = i < n;
+  u32 i = blockIdx.x * 64u + threadIdx.x;
+  if( i >= n ) return;
 
-  u8 const * S  = sig + 64UL*(size_t)(live ? i : 0u);
-  u8 const * P  = pub + 32UL*(size_t)(live ? i : 0u);
-  u8 const * s  = S + 32;
-  int code = 1;   /* pending */
+  /* R || A as 16 LE dwords (sig / pub records are 64- / 32-byte aligned) */
+  uint4 const * S4 = (uint4 const *)(sig + 64UL*i);
+  uint4 const * P4 = (uint4 const *)(pub + 32UL*i);
+  uint4 r0 = S4[0], r1 = S4[1], s0 = S4[2], s1 = S4[3], a0 = P4[0], a1 = P4[1];
+  u32 sw[8] = { s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w };
 
   /* s-range check with the reference's early "return 0" window (user.c:373-379) */
-  if( live ) {
-    u8 s31 = s[31];
-    if( s31 > 0x10 ) code = -1;
-    else if( s31 == 0x10 ) {
-      u32 any = 0; for( int k=16; k<31; k++ ) any |= s[k];
-      if( any ) code = 0;
+  int code = 1;   /* pending */
+  {
+    u32 s31 = sw[7] >> 24;
+    if( s31 > 0x10u ) code = -1;
+    else if( s31 == 0x10u ) {
+      if( (sw[4] | sw[5] | sw[6] | (sw[7] & 0x00ffffffu)) != 0u ) code = 0;   /* s[16..30] != 0 */
       else {
-        const u8 l_low[16] = { 0xED,0xD3,0xF5,0x5C,0x1A,0x63,0x12,0x58,0xD6,0x9C,0xF7,0xA2,0xDE,0xF9,0xDE,0x14 };
-        int k;
-        for( k=15; k>=0; k-- ) {
-          if( s[k] < l_low[k] ) break;
-          if( s[k] > l_low[k] ) { code = -1; break; }
+        /* s[0..15] vs l_low, compared from the top byte: s < l_low passes */
+        u32 const ll[4] = { 0x5cf5d3edu, 0x5812631au, 0xa2f79cd6u, 0x14def9deu };
+        bool less = false, decided = false;
+        _Pragma("unroll") for( int k=3; k>=0; k-- ) {
+          if( !decided && sw[k] != ll[k] ) { less = sw[k] < ll[k]; decided = true; }
         }
-        if( k<0 ) code = -1;
+        if( !less ) code = -1;
       }
     }
-  } else code = 0;
+  }
 
-  u32 h[16]; u32 sw[8];
-  _Pragma("unroll") for( int k=0; k<8; k++ ) sw[k] = 0;
+  u16 * dig = (u16 *)(ws + L.dig) + (size_t)i*256u;
+  int top = -1;
   if( code == 1 ) {
     u32 sz = msg_sz[i];
     u8 const * M = blob + msg_off[i];
-    u32 padded = ((64u + sz + 17u + 127u) / 128u) * 128u;
+    u32 nblk = (64u + sz + 17u + 127u) / 128u;
     u64 st[8] = FD_AMD_SHA512_H0;
-    for( u32 blk=0; blk<padded; blk+=128u ) {
+    u64 const ra[8] = { ((u64)r0.y << 32) | r0.x, ((u64)r0.w << 32) | r0.z, ((u64)r1.y << 32) | r1.x, ((u64)r1.w << 32) | r1.z,
+                        ((u64)a0.y << 32) | a0.x, ((u64)a0.w << 32) | a0.z, ((u64)a1.y << 32) | a1.x, ((u64)a1.w << 32) | a1.z };
+    u64 bitlen = (u64)(64u + sz) << 3;
+    for( u32 blk=0; blk<nblk; blk++ ) {
       u64 w[16];
       _Pragma("unroll") for( int k=0; k<16; k++ ) {
-        u64 v = 0;
-        _Pragma("unroll") for( int j=0; j<8; j++ ) v = (v << 8) | (u64)stream_byte( blk + 8u*(u32)k + (u32)j, S, P, M, sz, padded );
+        u32 kk = blk*16u + (u32)k;                 /* stream word index */
+        u64 v;
+        if( kk < 8u ) v = ra[k & 7];               /* only block 0 */
+        else          v = msg_word( M, sz, 8u*(kk - 8u) );
+        v = bswap64( v );
+        if( blk == nblk-1u && k == 15 ) v |= bitlen;
         w[k] = v;
       }
       sha512_compress( st, w );
     }
-    /* digest bytes little-endian into 16 words: byte 8a+b of the digest is
-       byte (7-b) of st[a] */
     u32 hd[16];
     _Pragma("unroll") for( int a=0; a<8; a++ ) {
-      u64 x = st[a];
-      u32 bswhi = __builtin_bswap32( (u32)(x >> 32) );
-      u32 bswlo = __builtin_bswap32( (u32)x );
-      hd[2*a] = bswhi; hd[2*a+1] = bswlo;
+      hd[2*a]   = __builtin_bswap32( (u32)(st[a] >> 32) );
+      hd[2*a+1] = __builtin_bswap32( (u32)st[a] );
     }
-    sc_reduce( h, hd );   /* h[0..7] */
-    _Pragma("unroll") for( int k=0; k<8; k++ )
-      sw[k] = (u32)s[4*k] | ((u32)s[4*k+1] << 8) | ((u32)s[4*k+2] << 16) | ((u32)s[4*k+3] << 24);
-  } else {
-    _Pragma("unroll") for( int k=0; k<16; k++ ) h[k] = 0;
-  }
+    u32 h[8];
+    sc_reduce( h, hd );
 
-  size_t N = L.N;
-  i8 * dig = (i8 *)(ws + L.dig);
-  int top = -1;
-  /* h digits (plane 0) then s digits (plane 1); non-pending lanes write zeros */
-  for( int plane=0; plane<2; plane++ ) {
-    slide_lds( lds, lane, plane ? sw : h );
-    if( live ) {
-      for( int p=0; p<256; p++ ) {
-        i8 d = lds[p*64 + lane];
-        dig[((size_t)plane*256u + (size_t)p)*N + i] = d;
-        if( d ) top = max( top, p );
-      }
-    }
+    /* digits: per-lane contiguous (da, db) u16 pairs, zero-filled first */
+    uint4 * d4 = (uint4 *)dig;
+    _Pragma("unroll 8") for( int k=0; k<32; k++ ) d4[k] = make_uint4( 0u, 0u, 0u, 0u );
+    u8 * db8 = (u8 *)dig;
+    slide_reg( h,  [&]( int pos, int r ) { db8[2*pos]     = (u8)(i8)r; top = max( top, pos ); } );
+    slide_reg( sw, [&]( int pos, int r ) { db8[2*pos + 1] = (u8)(i8)r; top = max( top, pos ); } );
   }
-  if( live ) {
-    ((int *)(ws + L.top))[i] = top;
-    err[i] = (i8)code;
-  }
+  ((int *)(ws + L.top))[i] = top;
+  err[i] = (i8)code;
 }
 
 /* ------------------------------------------------------------------ */
@@ -304,31 +322,56 @@ ge_to_cached( fe & cZ, fe & cYmX, fe & cYpX, fe & cT2d, p3 const & u ) {
   cZ = Z1; cYmX = fe_sub( Y1, X1 ); cYpX = fe_add( Y1, X1 );
 }
 
-__device__ __forceinline__ int wave_max( int v ) {
-  _Pragma("unroll") for( int o=32; o>0; o>>=1 ) v = max( v, __shfl_xor( v, o, 64 ) );
-  return v;
-}
-
+/* Base-point table in LDS, rows [Z(=1), Y-X, Y+X, 2dT] x 10 limbs per entry
+   (table/fd_ed25519_ge_bi_precomp_avx.c:30-112 lane order). */
 __constant__ static i32 const BI_TABLE[8][3][10] = FD_AMD_BI_PRECOMP;   /* rows y+x, y-x, 2dxy */
 
+enum { PH_DBL = 0, PH_ADDA = 1, PH_ADDB = 2, PH_FIN = 3, PH_DONE = 4 };
+
+/* k_dsm: [h](-A) + [s]B as a per-lane STEP STREAM.
+ *
+ * The reference loop (avx/fd_ed25519_ge.c:488-523) is, per bit position p
+ * from the top:  DBL ; [ADD Ai[|a_p|/2] if a_p] ; [MADD Bi[|b_p|/2] if b_p] ;
+ * with p1p1->p3 before every add and p1p1->p2 before every doubling.
+ * p1p1->p2 computes exactly the first three products of p1p1->p3
+ * (X*T, Y*Z, Z*T), so every op of the stream has the same shape:
+ *
+ *     u  = p1p1->p3(t)                        4 field muls
+ *     m0..m3 = op-specific 4 field muls        DBL: (X+Y)^2, Y^2, X^2, Z*2Z
+ *                                              ADD: Z*qZ, (Y-X)*qM, (Y+X)*qP, T*qT
+ *     t  = op-specific linear mix
+ *
+ * so each lane walks ITS OWN op sequence and every step does 8 useful field
+ * muls on every lane (no predicated adds).  Bit-exactness: sq(f) == mul(f,f),
+ * sq2(f) == mul(f,f+f) and mul(f,1) == carry(f) at the integer level
+ * (SURVEY.md s7 "Measured equivalences"), so a uniform mul is the
+ * reference's sq / sq2 / madd Z*1 bit for bit.  A lane whose last op is done
+ * takes one more step (PH_FIN): its p1p1->p2 result is R', compared with
+ * the limb memcmp of fd_ed25519_user.c:417-425, then it idles (PH_DONE).
+ */
 __global__ void __launch_bounds__(64)
 k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats ) {
-  __shared__ i32 bi[8][3][10];
-  for( int k=threadIdx.x; k<8*3*10; k+=64 ) (&bi[0][0][0])[k] = (&BI_TABLE[0][0][0])[k];
+  __shared__ i32 bi[8][40];
+  for( int k=threadIdx.x; k<8*40; k+=64 ) {
+    int e = k / 40, c = (k % 40) / 10, l = k % 10;
+    i32 v;
+    if( c == 0 ) v = (l == 0);                         /* Z = 1 */
+    else if( c == 1 ) v = BI_TABLE[e][1][l];           /* Y-X */
+    else if( c == 2 ) v = BI_TABLE[e][0][l];           /* Y+X */
+    else v = BI_TABLE[e][2][l];                        /* 2dxy */
+    bi[e][c*10 + l] = v;
+  }
   __syncthreads();
 
   u32 i = blockIdx.x * 64u + threadIdx.x;
   bool act = (i < n) && (err[i] == 1);
   size_t N = L.N;
   u32 ii = (i < n) ? i : 0u;
-
-  i8 const * dig = (i8 const *)(ws + L.dig);
   i32 * Aiw = (i32 *)(ws + L.Ai);
-  int top = act ? ((int const *)(ws + L.top))[ii] : -1;
 
-  /* -A (p3, Z = 1) */
-  p3 A;
+  /* -A (p3, Z = 1) and its odd multiples Ai (:423-481) -> HBM */
   {
+    p3 A;
     i32 const * Aw = (i32 const *)(ws + L.A);
     _Pragma("unroll") for( int k=0; k<10; k++ ) {
       A.X.v[k] = act ? Aw[(size_t)(k   )*N + ii] : 0;
@@ -336,10 +379,6 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
       A.T.v[k] = act ? Aw[(size_t)(20+k)*N + ii] : 0;
       A.Z.v[k] = (k==0);
     }
-  }
-
-  /* Ai = {1,3,...,15}(-A) in cached form (:423-481) -> HBM slab */
-  {
     fe cZ, cYmX, cYpX, cT2d;
     ge_to_cached( cZ, cYmX, cYpX, cT2d, A );
 #   define AI_STORE( e ) do {                                                       \
@@ -353,67 +392,126 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
     p1p1 t = ge_dbl( A.X, A.Y, A.Z );
     p3 A2 = ge_p1p1_to_p3( t );
     for( int e=0; e<7; e++ ) {
-      p1p1 s = ge_add<false>( A2, cZ, cYmX, cYpX, cT2d, false );
-      p3 u = ge_p1p1_to_p3( s );
+      p1p1 s2 = ge_add<false>( A2, cZ, cYmX, cYpX, cT2d, false );
+      p3 u = ge_p1p1_to_p3( s2 );
       ge_to_cached( cZ, cYmX, cYpX, cT2d, u );
       if( act ) AI_STORE( e+1 );
     }
 #   undef AI_STORE
   }
 
-  fe X = fe_zero(), Y = fe_one(), Z = fe_one();
-  int itop = wave_max( top );
-  u32 nit = 0, nha = 0, nhb = 0;
-  for( int p=itop; p>=0; p-- ) {
-    p1p1 t = ge_dbl( X, Y, Z );
-    int da = act ? (int)dig[(size_t)p*N + ii] : 0;
-    int db = act ? (int)dig[((size_t)256 + (size_t)p)*N + ii] : 0;
-    if( p <= top ) nit++;
-    if( da ) {
+  /* lane state */
+  u64 const * dg = (u64 const *)((u16 const *)(ws + L.dig) + (size_t)ii*256u);
+  int p   = act ? ((int const *)(ws + L.top))[ii] : -1;
+  int ph  = act ? (p >= 0 ? PH_DBL : PH_FIN) : PH_DONE;
+  u64 dc  = (p >= 0) ? dg[p >> 2] : 0UL;             /* digits of the 4-position group of p */
+  int cur = (int)((dc >> (16 * (p & 3))) & 0xffffu); /* (a_p, b_p) as int8 pair */
+  u32 nha = 0, nhb = 0;
+  u32 nit = (u32)(p + 1);
+  bool qneg = false;
+  fe qZ, qM, qP, qT;
+  _Pragma("unroll") for( int k=0; k<10; k++ ) { qZ.v[k] = 0; qM.v[k] = 0; qP.v[k] = 0; qT.v[k] = 0; }
+  p1p1 t;   /* identity as a completed point: p1p1->p3 gives (0,1,1,0) */
+  t.X = fe_zero(); t.Y = fe_one(); t.Z = fe_one(); t.T = fe_one();
+
+  for( ;; ) {
+    /* p1p1 -> p3 (its X,Y,Z are the reference's p1p1 -> p2) */
+    p3 u = ge_p1p1_to_p3( t );
+
+    bool fin = (ph == PH_FIN);
+    if( __any( fin ) ) {
+      if( fin ) {
+        i32 const * Rw = (i32 const *)(ws + L.R);
+        fe RX, RY;
+        _Pragma("unroll") for( int k=0; k<10; k++ ) { RX.v[k] = Rw[(size_t)k*N + ii]; RY.v[k] = Rw[(size_t)(10+k)*N + ii]; }
+        fe xZ = fe_mul( u.Z, RX );
+        fe yZ = fe_mul( u.Z, RY );
+        bool eq = true;
+        _Pragma("unroll") for( int k=0; k<8; k++ ) eq = eq && (xZ.v[k] == u.X.v[k]) && (yZ.v[k] == u.Y.v[k]);
+        err[i] = (i8)(eq ? 0 : -3);
+        ph = PH_DONE;
+      }
+    }
+    if( __all( ph == PH_DONE ) ) break;
+
+    /* op body: 4 field muls with per-lane operands */
+    bool isD = (ph == PH_DBL);
+    fe a0, b0, a1, b1, a2, b2, a3, b3;
+    _Pragma("unroll") for( int k=0; k<10; k++ ) {
+      i32 X = u.X.v[k], Y = u.Y.v[k], Z = u.Z.v[k], T = u.T.v[k];
+      i32 xy = X + Y, ymx = Y - X;
+      a0.v[k] = isD ? xy : Z;    b0.v[k] = isD ? xy : qZ.v[k];
+      a1.v[k] = isD ? Y  : ymx;  b1.v[k] = isD ? Y  : qM.v[k];
+      a2.v[k] = isD ? X  : xy;   b2.v[k] = isD ? X  : qP.v[k];
+      a3.v[k] = isD ? Z  : T;    b3.v[k] = isD ? Z + Z : qT.v[k];
+    }
+    fe m0 = fe_mul( a0, b0 );
+    fe m1 = fe_mul( a1, b1 );
+    fe m2 = fe_mul( a2, b2 );
+    fe m3 = fe_mul( a3, b3 );
+    _Pragma("unroll") for( int k=0; k<10; k++ ) {
+      i32 A0 = m0.v[k], A1 = m1.v[k], A2 = m2.v[k], A3 = m3.v[k];
+      /* DBL mix [a-b-c, b+c, b-c, d-b+c]; ADD mix [P-M, P+M, 2Z+-T, 2Z-+T] */
+      i32 z2 = A0 + A0;
+      i32 dX = A0 - A1 - A2, dY = A1 + A2, dZ = A1 - A2, dT = A3 - A1 + A2;
+      i32 aX = A2 - A1,      aY = A2 + A1;
+      i32 aZ = qneg ? z2 - A3 : z2 + A3, aT = qneg ? z2 + A3 : z2 - A3;
+      bool idle = (ph == PH_DONE);
+      t.X.v[k] = idle ? 0       : (isD ? dX : aX);
+      t.Y.v[k] = idle ? (k==0)  : (isD ? dY : aY);
+      t.Z.v[k] = idle ? (k==0)  : (isD ? dZ : aZ);
+      t.T.v[k] = idle ? (k==0)  : (isD ? dT : aT);
+    }
+
+    /* advance the lane's op stream */
+    int da = (int)(i8)(cur & 0xff), db = (int)(i8)(cur >> 8);
+    int nph;
+    if( ph == PH_DBL )       nph = da ? PH_ADDA : (db ? PH_ADDB : -1);
+    else if( ph == PH_ADDA ) nph = db ? PH_ADDB : -1;
+    else if( ph == PH_ADDB ) nph = -1;
+    else                     nph = PH_DONE;
+    if( nph == -1 ) {
+      p--;
+      if( p < 0 ) nph = PH_FIN;
+      else {
+        if( (p & 3) == 3 ) dc = dg[p >> 2];
+        cur = (int)((dc >> (16 * (p & 3))) & 0xffffu);
+        nph = PH_DBL;
+      }
+    }
+    ph = nph;
+
+    /* prefetch the next op's table entry (consumed one step later, after
+       the next p1p1->p3, so the load latency hides under 4 muls) */
+    if( ph == PH_ADDA ) {
       nha++;
-      p3 u = ge_p1p1_to_p3( t );
       int e = (da < 0 ? -da : da) >> 1;
-      fe qZ, qYmX, qYpX, qT2d;
+      qneg = da < 0;
+      size_t rZ = (size_t)e*40, rM = rZ + (qneg ? 20 : 10), rP = rZ + (qneg ? 10 : 20), rT = rZ + 30;
       _Pragma("unroll") for( int k=0; k<10; k++ ) {
-        qZ.v[k]   = Aiw[((size_t)e*40 + 0 + k)*N + ii];
-        qYmX.v[k] = Aiw[((size_t)e*40 + 10 + k)*N + ii];
-        qYpX.v[k] = Aiw[((size_t)e*40 + 20 + k)*N + ii];
-        qT2d.v[k] = Aiw[((size_t)e*40 + 30 + k)*N + ii];
+        qZ.v[k] = Aiw[(rZ + k)*N + ii];
+        qM.v[k] = Aiw[(rM + k)*N + ii];
+        qP.v[k] = Aiw[(rP + k)*N + ii];
+        qT.v[k] = Aiw[(rT + k)*N + ii];
       }
-      t = ge_add<false>( u, qZ, qYmX, qYpX, qT2d, da < 0 );
-    }
-    if( db ) {
+    } else if( ph == PH_ADDB ) {
       nhb++;
-      p3 u = ge_p1p1_to_p3( t );
       int e = (db < 0 ? -db : db) >> 1;
-      fe qYmX, qYpX, qT2d;
+      qneg = db < 0;
+      int oM = qneg ? 20 : 10, oP = qneg ? 10 : 20;
       _Pragma("unroll") for( int k=0; k<10; k++ ) {
-        qYpX.v[k] = bi[e][0][k];
-        qYmX.v[k] = bi[e][1][k];
-        qT2d.v[k] = bi[e][2][k];
+        qZ.v[k] = bi[e][k];
+        qM.v[k] = bi[e][oM + k];
+        qP.v[k] = bi[e][oP + k];
+        qT.v[k] = bi[e][30 + k];
       }
-      t = ge_add<true>( u, qYmX /*unused*/, qYmX, qYpX, qT2d, db < 0 );
     }
-    X = fe_mul( t.X, t.T );
-    Y = fe_mul( t.Y, t.Z );
-    Z = fe_mul( t.Z, t.T );
   }
 
   if( want_stats && i < n ) {
     u32 * st = (u32 *)(ws + L.st);
-    st[i] = act ? nit : 0u; st[N + i] = nha; st[2*N + i] = nhb;
+    st[i] = act ? nit : 0u; st[N + i] = act ? nha : 0u; st[2*N + i] = act ? nhb : 0u;
   }
-  if( !act ) return;
-  fe RX, RY;
-  {
-    i32 const * Rw = (i32 const *)(ws + L.R);
-    _Pragma("unroll") for( int k=0; k<10; k++ ) { RX.v[k] = Rw[(size_t)k*N + ii]; RY.v[k] = Rw[(size_t)(10+k)*N + ii]; }
-  }
-  fe xZ = fe_mul( Z, RX );
-  fe yZ = fe_mul( Z, RY );
-  bool eq = true;
-  _Pragma("unroll") for( int k=0; k<8; k++ ) eq = eq && (xZ.v[k] == X.v[k]) && (yZ.v[k] == Y.v[k]);   /* limbs 0..7 (user.c:424-425) */
-  err[i] = (i8)(eq ? 0 : -3);
 }
 
 /* ------------------------------------------------------------------ */

@@ -64,6 +64,8 @@ def lib():
     L.fd_ed25519_amd_verify_dev_ev.restype = i
     L.fd_ed25519_amd_work_stats_dev.argtypes = [ul, vp, vp, vp]
     L.fd_ed25519_amd_work_stats_dev.restype = i
+    L.fd_ed25519_amd_debug_digits_dev.argtypes = [ul, vp, vp, vp, vp]
+    L.fd_ed25519_amd_debug_digits_dev.restype = i
     L.fd_ed25519_amd_version.argtypes = []
     L.fd_ed25519_amd_version.restype = ctypes.c_char_p
     L.fd_ed25519_amd_sign_batch.argtypes = [ul, vp, vp, vp, vp, vp, vp, i]
@@ -216,6 +218,12 @@ def work_stats_dev(n, d_ws, d_stats, stream=0):
     rc = lib().fd_ed25519_amd_work_stats_dev(int(n), d_ws, d_stats, stream)
     if rc:
         raise EngineError("fd_ed25519_amd_work_stats_dev rc=%d" % rc)
+
+
+def debug_digits_dev(n, d_ws, d_dig, d_top, stream=0):
+    rc = lib().fd_ed25519_amd_debug_digits_dev(int(n), d_ws, d_dig, d_top, stream)
+    if rc:
+        raise EngineError("fd_ed25519_amd_debug_digits_dev rc=%d" % rc)
 
 
 def version():

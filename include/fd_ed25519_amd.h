@@ -183,6 +183,13 @@ fd_ed25519_amd_verify_dev_ev( ulong         n,
 int
 fd_ed25519_amd_work_stats_dev( ulong n, void const * d_ws, uint * d_stats, void * stream );
 
+/* Debug: copy the signed sliding-window digits (u16 [n][256], low byte =
+   digit of h = SHA-512(R||A||M) mod L, high byte = digit of s; recoding of
+   avx/fd_ed25519_ge.c:378-400) and the top digit position (int [n]) that
+   the last device-resident call left in workspace `d_ws`. */
+int
+fd_ed25519_amd_debug_digits_dev( ulong n, void const * d_ws, unsigned short * d_dig, int * d_top, void * stream );
+
 /* Host-side batch keygen + sign over the SoA layout (workload synthesis;
    not the verify path): prv[n][32] -> pub[n][32], sig[n][64] over
    blob[msg_off[i] .. +msg_sz[i]), on nthread host threads.  Returns 0. */

@@ -1,0 +1,89 @@
+"""CPU tests of the C-ABI boundary: the engine library loads without a GPU,
+exports every symbol include/fd_ed25519_amd.h declares, and its host-side
+(non-verify) entry points behave like the reference's.  No verify call is
+made here -- those need a GPU and live in test_gpu_parity.py."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "fd_ed25519_amd.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b(fd_ed25519_\w+)\s*\(", src)
+    return sorted(set(names))
+
+
+def test_library_exports_every_declared_symbol():
+    from firedancer_amd import ed25519
+    L = ed25519.lib()
+    names = declared_functions()
+    assert "fd_ed25519_verify" in names and "fd_ed25519_amd_verify_dev" in names
+    for n in names:
+        assert hasattr(L, n), n
+    # and as real dynamic symbols (a C / Rust / Go caller links by name)
+    out = subprocess.run(["nm", "-D", "--defined-only", ed25519.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(l.split()[-1] for l in out.splitlines() if l.strip())
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+
+
+def test_reference_codes_and_strerror():
+    from firedancer_amd import ed25519
+    assert (ed25519.FD_ED25519_SUCCESS, ed25519.FD_ED25519_ERR_SIG, ed25519.FD_ED25519_ERR_PUBKEY,
+            ed25519.FD_ED25519_ERR_MSG) == (0, -1, -2, -3)
+    # fd_ed25519_user.c:433-443
+    assert ed25519.strerror(0) == "success"
+    assert ed25519.strerror(-1) == "bad signature"
+    assert ed25519.strerror(-2) == "bad public key"
+    assert ed25519.strerror(-3) == "bad message"
+    assert ed25519.strerror(7) == "unknown"
+    hdr = open(HEADER).read()
+    for name, val in (("FD_ED25519_SUCCESS", 0), ("FD_ED25519_ERR_SIG", -1), ("FD_ED25519_ERR_PUBKEY", -2),
+                      ("FD_ED25519_ERR_MSG", -3)):
+        assert re.search(r"#define %s\s+\(\s*%d\)" % (name, val), hdr), name
+
+
+def test_workspace_footprint_monotone():
+    from firedancer_amd import ed25519
+    a, b, c = (ed25519.workspace_footprint(n) for n in (1, 64, 1 << 20))
+    assert 0 < a <= b < c
+    assert c >= (1 << 20) * 2000        # ~2 KB of scratch per signature
+    assert c % 256 == 0
+
+
+def test_engine_fails_loudly_without_device():
+    """On a host without a HIP device the engine must refuse, not fall back."""
+    from firedancer_amd import ed25519, hip
+    if hip.device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(ed25519.EngineError):
+        ed25519.Engine(device=0)
+
+
+def test_c_caller_compiles_against_header(tmp_path):
+    """A plain C caller (the reference's own calling convention) compiles and
+    links against the header + library."""
+    from firedancer_amd import ed25519
+    c = tmp_path / "caller.c"
+    c.write_text('''
+#include "fd_ed25519_amd.h"
+#include <stdio.h>
+int main( void ) {
+  printf( "%s\\n", fd_ed25519_strerror( FD_ED25519_ERR_MSG ) );
+  printf( "%lu\\n", fd_ed25519_amd_workspace_footprint( 64UL ) );
+  return 0;
+}
+''')
+    exe = tmp_path / "caller"
+    libdir = os.path.dirname(ed25519.LIB_PATH)
+    subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(c),
+                           "-L", libdir, "-lfd_ed25519_amd", "-Wl,-rpath," + libdir, "-o", str(exe)])
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    assert out[0] == "bad" and out[1] == "message"

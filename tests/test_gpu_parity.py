@@ -150,3 +150,44 @@ def test_large_batch_properties(engine):
         assert _oracle.verify(bytes(blob[off[i]:off[i] + 200]), bytes(sig[i]), bytes(pub[i])) == int(err[i])
     err2 = engine.verify_soa(pub, sig, off, sz, blob)
     assert np.array_equal(err, err2)
+
+
+def test_prep_digits_vs_python(golden):
+    """k_prep output (the slide digits of h and s, and the top position) vs a
+    pure-Python restatement with hashlib SHA-512, on the golden vectors that
+    pass the s check."""
+    import _slide
+    from firedancer_amd import ed25519, hip
+    sel = [i for i in range(len(golden)) if golden.expect[i] in (0, -3)][:300]
+    b = _golden.Batch(golden.pub[sel], golden.sig[sel], None, golden.msg_sz[sel], None)
+    msgs = [golden.msg(i) for i in sel]
+    off = np.cumsum([0] + [len(m) for m in msgs[:-1]]).astype(np.uint32)
+    blob = np.frombuffer(b"".join(msgs) + b"\0" * 16, np.uint8)
+    n = len(sel)
+    d = {k: hip.DeviceBuffer.from_array(v) for k, v in
+         dict(pub=b.pub, sig=b.sig, off=off, sz=b.msg_sz, blob=blob).items()}
+    err = hip.DeviceBuffer(n)
+    ws = hip.DeviceBuffer(ed25519.workspace_footprint(n))
+    dig = hip.DeviceBuffer(512 * n)
+    top = hip.DeviceBuffer(4 * n)
+    stream = hip.Stream()
+    ed25519.verify_dev(n, d["pub"].ptr, d["sig"].ptr, d["off"].ptr, d["sz"].ptr, d["blob"].ptr, err.ptr, ws.ptr,
+                       stream.handle)
+    ed25519.debug_digits_dev(n, ws.ptr, dig.ptr, top.ptr, stream.handle)
+    stream.synchronize()
+    dg = dig.to_array(np.uint16, 256 * n).reshape(n, 256)
+    tp = top.to_array(np.int32, n)
+    for j in range(n):
+        s = bytes(b.sig[j][32:])
+        if s[31] == 0x10 and any(s[16:31]):
+            continue                                   # decided by the s check, no digits
+        h = _slide.h_scalar(b.sig[j], b.pub[j], msgs[j])
+        ea = _slide.slide(h)
+        eb = _slide.slide(int.from_bytes(s, "little"))
+        ga = (dg[j] & 0xff).astype(np.uint8).view(np.int8).tolist()
+        gb = (dg[j] >> 8).astype(np.uint8).view(np.int8).tolist()
+        assert gb == eb, ("s digits", j)
+        hv = sum(d << p for p, d in enumerate(ga))
+        assert ga == ea, ("h digits", j, "gpu digits encode %x, want %x" % (hv, h))
+        nz = [p for p in range(256) if ea[p] or eb[p]]
+        assert tp[j] == (max(nz) if nz else -1)
