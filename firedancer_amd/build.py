@@ -38,23 +38,24 @@ def _stale(out, deps):
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build_engine(force=False, verbose=False):
+def build_engine(force=False, verbose=False, out=None, defines=()):
     consts = os.path.join(CSRC, "fd_ed25519_consts.h")
     gen = os.path.join(ROOT, "tools", "gen_consts.py")
     if force or _stale(consts, [gen]):
         subprocess.check_call([sys.executable, gen, consts, "FD_AMD"])
+    lib = out or LIB
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [consts]
-    if not force and not _stale(LIB, deps):
-        return LIB
+    if not force and not defines and not _stale(lib, deps):
+        return lib
     cmd = [_hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-o", LIB + ".tmp"]
+           "-Wall", "-Wno-unused-function", "-o", lib + ".tmp"] + ["-D" + d for d in defines]
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     cmd += ["-lpthread"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd, cwd=CSRC)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
 
 
 def build_oracle(verbose=False):
@@ -71,4 +72,10 @@ def build(force=False, verbose=False):
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    # python -m firedancer_amd.build [--force] [--variant OUT.so DEF1,DEF2]  (A/B experiment builds)
+    if "--variant" in sys.argv:
+        k = sys.argv.index("--variant")
+        out, defs = sys.argv[k + 1], [d for d in sys.argv[k + 2].split(",") if d]
+        print(build_engine(force=True, verbose=True, out=os.path.abspath(out), defines=defs))
+    else:
+        print(build(force="--force" in sys.argv, verbose=True))

@@ -61,6 +61,49 @@ FD_DEV fe fe_carry( i64 h0, i64 h1, i64 h2, i64 h3, i64 h4, i64 h5, i64 h6, i64 
   return r;
 }
 
+/* The same carry chain on PRE-BIASED column sums h_k' = h_k + 2^(w_k-1)
+   (2^25 for even k, 2^24 for odd k), the bias being folded into the first
+   v_mad_i64_i32 of each column for free.  Each rounding carry is then a
+   plain arithmetic shift c = h' >> w, the bias cancels in the second carry
+   of limbs 4 and 0, and every output limb is (h' mod 2^w) - 2^(w-1) in
+   32-bit arithmetic.  Identical limbs to fe_carry on the unbiased sums. */
+FD_DEV fe fe_carry_b( i64 h0, i64 h1, i64 h2, i64 h3, i64 h4, i64 h5, i64 h6, i64 h7, i64 h8, i64 h9 ) {
+  i64 const M26 = (1L<<26) - 1, M25 = (1L<<25) - 1;
+  h1 += h0 >> 26;
+  h5 += h4 >> 26;
+  h2 += h1 >> 25;
+  h6 += h5 >> 25;
+  h3 += h2 >> 26;
+  h7 += h6 >> 26;
+  i64 t4 = (h4 & M26) + (h3 >> 25);
+  h8 += h7 >> 25;
+  i32 c4b = (i32)(t4 >> 26);
+  h9 += h8 >> 26;
+  i64 t0 = (h0 & M26) + (h9 >> 25) * 19;
+  i32 c0b = (i32)(t0 >> 26);
+  fe r;
+  r.v[0] = (i32)((u32)t0 & (u32)M26) - (1<<25);
+  r.v[1] = (i32)((u32)h1 & (u32)M25) - (1<<24) + c0b;
+  r.v[2] = (i32)((u32)h2 & (u32)M26) - (1<<25);
+  r.v[3] = (i32)((u32)h3 & (u32)M25) - (1<<24);
+  r.v[4] = (i32)((u32)t4 & (u32)M26) - (1<<25);
+  r.v[5] = (i32)((u32)h5 & (u32)M25) - (1<<24) + c4b;
+  r.v[6] = (i32)((u32)h6 & (u32)M26) - (1<<25);
+  r.v[7] = (i32)((u32)h7 & (u32)M25) - (1<<24);
+  r.v[8] = (i32)((u32)h8 & (u32)M26) - (1<<25);
+  r.v[9] = (i32)((u32)h9 & (u32)M25) - (1<<24);
+  return r;
+}
+
+/* The column biases as OPAQUE wave-uniform values: LLVM canonicalises an
+   integer constant to the end of an add chain, which would cost one extra
+   64-bit add per column; an opaque SGPR value stays first and becomes the
+   src2 of the column's first v_mad_i64_i32. */
+FD_DEV i64 fd_opaque( i64 x ) { asm( "" : "+s"(x) ); return x; }
+#define FD_B26 b26
+#define FD_B25 b25
+#define FD_BIAS_DECL i64 const b26 = fd_opaque( 1L<<25 ), b25 = fd_opaque( 1L<<24 )
+
 /* f * 1 through the reference multiplier: the column sums are the limbs
    themselves, so it is exactly the carry chain ("x1" renormalisation of
    the AVX flow, avx/fd_ed25519_ge.c:440-446 and the madd lane 0). */
@@ -71,32 +114,33 @@ FD_DEV fe fe_mul_one( fe const & f ) {
 /* FE_AVX_INL_MUL, one lane (avx/fd_ed25519_fe_avx_inl.h:484-585) */
 FD_DEV fe fe_mul( fe const & F, fe const & G ) {
   i32 const * f = F.v; i32 const * g = G.v;
+  FD_BIAS_DECL;
   i32 g1_19 = wmul( g[1], 19 ), g2_19 = wmul( g[2], 19 ), g3_19 = wmul( g[3], 19 );
   i32 g4_19 = wmul( g[4], 19 ), g5_19 = wmul( g[5], 19 ), g6_19 = wmul( g[6], 19 );
   i32 g7_19 = wmul( g[7], 19 ), g8_19 = wmul( g[8], 19 ), g9_19 = wmul( g[9], 19 );
   i32 f1_2 = wmul( f[1], 2 ), f3_2 = wmul( f[3], 2 ), f5_2 = wmul( f[5], 2 );
   i32 f7_2 = wmul( f[7], 2 ), f9_2 = wmul( f[9], 2 );
-  i64 h0 = mll(f[0],g[0]) + mll(f1_2,g9_19) + mll(f[2],g8_19) + mll(f3_2,g7_19) + mll(f[4],g6_19)
+  i64 h0 = FD_B26 + mll(f[0],g[0]) + mll(f1_2,g9_19) + mll(f[2],g8_19) + mll(f3_2,g7_19) + mll(f[4],g6_19)
          + mll(f5_2,g5_19) + mll(f[6],g4_19) + mll(f7_2,g3_19) + mll(f[8],g2_19) + mll(f9_2,g1_19);
-  i64 h1 = mll(f[0],g[1]) + mll(f[1],g[0]) + mll(f[2],g9_19) + mll(f[3],g8_19) + mll(f[4],g7_19)
+  i64 h1 = FD_B25 + mll(f[0],g[1]) + mll(f[1],g[0]) + mll(f[2],g9_19) + mll(f[3],g8_19) + mll(f[4],g7_19)
          + mll(f[5],g6_19) + mll(f[6],g5_19) + mll(f[7],g4_19) + mll(f[8],g3_19) + mll(f[9],g2_19);
-  i64 h2 = mll(f[0],g[2]) + mll(f1_2,g[1]) + mll(f[2],g[0]) + mll(f3_2,g9_19) + mll(f[4],g8_19)
+  i64 h2 = FD_B26 + mll(f[0],g[2]) + mll(f1_2,g[1]) + mll(f[2],g[0]) + mll(f3_2,g9_19) + mll(f[4],g8_19)
          + mll(f5_2,g7_19) + mll(f[6],g6_19) + mll(f7_2,g5_19) + mll(f[8],g4_19) + mll(f9_2,g3_19);
-  i64 h3 = mll(f[0],g[3]) + mll(f[1],g[2]) + mll(f[2],g[1]) + mll(f[3],g[0]) + mll(f[4],g9_19)
+  i64 h3 = FD_B25 + mll(f[0],g[3]) + mll(f[1],g[2]) + mll(f[2],g[1]) + mll(f[3],g[0]) + mll(f[4],g9_19)
          + mll(f[5],g8_19) + mll(f[6],g7_19) + mll(f[7],g6_19) + mll(f[8],g5_19) + mll(f[9],g4_19);
-  i64 h4 = mll(f[0],g[4]) + mll(f1_2,g[3]) + mll(f[2],g[2]) + mll(f3_2,g[1]) + mll(f[4],g[0])
+  i64 h4 = FD_B26 + mll(f[0],g[4]) + mll(f1_2,g[3]) + mll(f[2],g[2]) + mll(f3_2,g[1]) + mll(f[4],g[0])
          + mll(f5_2,g9_19) + mll(f[6],g8_19) + mll(f7_2,g7_19) + mll(f[8],g6_19) + mll(f9_2,g5_19);
-  i64 h5 = mll(f[0],g[5]) + mll(f[1],g[4]) + mll(f[2],g[3]) + mll(f[3],g[2]) + mll(f[4],g[1])
+  i64 h5 = FD_B25 + mll(f[0],g[5]) + mll(f[1],g[4]) + mll(f[2],g[3]) + mll(f[3],g[2]) + mll(f[4],g[1])
          + mll(f[5],g[0]) + mll(f[6],g9_19) + mll(f[7],g8_19) + mll(f[8],g7_19) + mll(f[9],g6_19);
-  i64 h6 = mll(f[0],g[6]) + mll(f1_2,g[5]) + mll(f[2],g[4]) + mll(f3_2,g[3]) + mll(f[4],g[2])
+  i64 h6 = FD_B26 + mll(f[0],g[6]) + mll(f1_2,g[5]) + mll(f[2],g[4]) + mll(f3_2,g[3]) + mll(f[4],g[2])
          + mll(f5_2,g[1]) + mll(f[6],g[0]) + mll(f7_2,g9_19) + mll(f[8],g8_19) + mll(f9_2,g7_19);
-  i64 h7 = mll(f[0],g[7]) + mll(f[1],g[6]) + mll(f[2],g[5]) + mll(f[3],g[4]) + mll(f[4],g[3])
+  i64 h7 = FD_B25 + mll(f[0],g[7]) + mll(f[1],g[6]) + mll(f[2],g[5]) + mll(f[3],g[4]) + mll(f[4],g[3])
          + mll(f[5],g[2]) + mll(f[6],g[1]) + mll(f[7],g[0]) + mll(f[8],g9_19) + mll(f[9],g8_19);
-  i64 h8 = mll(f[0],g[8]) + mll(f1_2,g[7]) + mll(f[2],g[6]) + mll(f3_2,g[5]) + mll(f[4],g[4])
+  i64 h8 = FD_B26 + mll(f[0],g[8]) + mll(f1_2,g[7]) + mll(f[2],g[6]) + mll(f3_2,g[5]) + mll(f[4],g[4])
          + mll(f5_2,g[3]) + mll(f[6],g[2]) + mll(f7_2,g[1]) + mll(f[8],g[0]) + mll(f9_2,g9_19);
-  i64 h9 = mll(f[0],g[9]) + mll(f[1],g[8]) + mll(f[2],g[7]) + mll(f[3],g[6]) + mll(f[4],g[5])
+  i64 h9 = FD_B25 + mll(f[0],g[9]) + mll(f[1],g[8]) + mll(f[2],g[7]) + mll(f[3],g[6]) + mll(f[4],g[5])
          + mll(f[5],g[4]) + mll(f[6],g[3]) + mll(f[7],g[2]) + mll(f[8],g[1]) + mll(f[9],g[0]);
-  return fe_carry( h0, h1, h2, h3, h4, h5, h6, h7, h8, h9 );
+  return fe_carry_b( h0, h1, h2, h3, h4, h5, h6, h7, h8, h9 );
 }
 
 /* FE_AVX_INL_SQN, one lane, n in {1,2} (avx/fd_ed25519_fe_avx_inl.h:592-674):
@@ -104,29 +148,33 @@ FD_DEV fe fe_mul( fe const & F, fe const & G ) {
 template<int N>
 FD_DEV fe fe_sqn( fe const & F ) {
   i32 const * f = F.v;
+  FD_BIAS_DECL;
   i32 f0_2 = wmul( f[0], 2 ), f1_2 = wmul( f[1], 2 ), f2_2 = wmul( f[2], 2 ), f3_2 = wmul( f[3], 2 );
   i32 f4_2 = wmul( f[4], 2 ), f5_2 = wmul( f[5], 2 ), f6_2 = wmul( f[6], 2 ), f7_2 = wmul( f[7], 2 );
   i32 f5_38 = wmul( f[5], 38 ), f6_19 = wmul( f[6], 19 ), f7_38 = wmul( f[7], 38 );
   i32 f8_19 = wmul( f[8], 19 ), f9_38 = wmul( f[9], 38 );
-  i64 h0 = mll(f[0],f[0]) + mll(f1_2,f9_38) + mll(f2_2,f8_19) + mll(f3_2,f7_38) + mll(f4_2,f6_19) + mll(f[5],f5_38);
-  i64 h1 = mll(f0_2,f[1]) + mll(f[2],f9_38) + mll(f3_2,f8_19) + mll(f[4],f7_38) + mll(f5_2,f6_19);
-  i64 h2 = mll(f0_2,f[2]) + mll(f1_2,f[1]) + mll(f3_2,f9_38) + mll(f4_2,f8_19) + mll(f5_2,f7_38) + mll(f[6],f6_19);
-  i64 h3 = mll(f0_2,f[3]) + mll(f1_2,f[2]) + mll(f[4],f9_38) + mll(f5_2,f8_19) + mll(f[6],f7_38);
-  i64 h4 = mll(f0_2,f[4]) + mll(f1_2,f3_2) + mll(f[2],f[2]) + mll(f5_2,f9_38) + mll(f6_2,f8_19) + mll(f[7],f7_38);
-  i64 h5 = mll(f0_2,f[5]) + mll(f1_2,f[4]) + mll(f2_2,f[3]) + mll(f[6],f9_38) + mll(f7_2,f8_19);
-  i64 h6 = mll(f0_2,f[6]) + mll(f1_2,f5_2) + mll(f2_2,f[4]) + mll(f3_2,f[3]) + mll(f7_2,f9_38) + mll(f[8],f8_19);
-  i64 h7 = mll(f0_2,f[7]) + mll(f1_2,f[6]) + mll(f2_2,f[5]) + mll(f3_2,f[4]) + mll(f[8],f9_38);
-  i64 h8 = mll(f0_2,f[8]) + mll(f1_2,f7_2) + mll(f2_2,f[6]) + mll(f3_2,f5_2) + mll(f[4],f[4]) + mll(f[9],f9_38);
-  i64 h9 = mll(f0_2,f[9]) + mll(f1_2,f[8]) + mll(f2_2,f[7]) + mll(f3_2,f[6]) + mll(f4_2,f[5]);
-  if( N==2 ) { h0 += h0; h1 += h1; h2 += h2; h3 += h3; h4 += h4; h5 += h5; h6 += h6; h7 += h7; h8 += h8; h9 += h9; }
-  return fe_carry( h0, h1, h2, h3, h4, h5, h6, h7, h8, h9 );
+  i64 h0 = (N==1 ? FD_B26 : 0L) + mll(f[0],f[0]) + mll(f1_2,f9_38) + mll(f2_2,f8_19) + mll(f3_2,f7_38) + mll(f4_2,f6_19) + mll(f[5],f5_38);
+  i64 h1 = (N==1 ? FD_B25 : 0L) + mll(f0_2,f[1]) + mll(f[2],f9_38) + mll(f3_2,f8_19) + mll(f[4],f7_38) + mll(f5_2,f6_19);
+  i64 h2 = (N==1 ? FD_B26 : 0L) + mll(f0_2,f[2]) + mll(f1_2,f[1]) + mll(f3_2,f9_38) + mll(f4_2,f8_19) + mll(f5_2,f7_38) + mll(f[6],f6_19);
+  i64 h3 = (N==1 ? FD_B25 : 0L) + mll(f0_2,f[3]) + mll(f1_2,f[2]) + mll(f[4],f9_38) + mll(f5_2,f8_19) + mll(f[6],f7_38);
+  i64 h4 = (N==1 ? FD_B26 : 0L) + mll(f0_2,f[4]) + mll(f1_2,f3_2) + mll(f[2],f[2]) + mll(f5_2,f9_38) + mll(f6_2,f8_19) + mll(f[7],f7_38);
+  i64 h5 = (N==1 ? FD_B25 : 0L) + mll(f0_2,f[5]) + mll(f1_2,f[4]) + mll(f2_2,f[3]) + mll(f[6],f9_38) + mll(f7_2,f8_19);
+  i64 h6 = (N==1 ? FD_B26 : 0L) + mll(f0_2,f[6]) + mll(f1_2,f5_2) + mll(f2_2,f[4]) + mll(f3_2,f[3]) + mll(f7_2,f9_38) + mll(f[8],f8_19);
+  i64 h7 = (N==1 ? FD_B25 : 0L) + mll(f0_2,f[7]) + mll(f1_2,f[6]) + mll(f2_2,f[5]) + mll(f3_2,f[4]) + mll(f[8],f9_38);
+  i64 h8 = (N==1 ? FD_B26 : 0L) + mll(f0_2,f[8]) + mll(f1_2,f7_2) + mll(f2_2,f[6]) + mll(f3_2,f5_2) + mll(f[4],f[4]) + mll(f[9],f9_38);
+  i64 h9 = (N==1 ? FD_B25 : 0L) + mll(f0_2,f[9]) + mll(f1_2,f[8]) + mll(f2_2,f[7]) + mll(f3_2,f[6]) + mll(f4_2,f[5]);
+  if( N==2 ) {
+    h0 += h0; h1 += h1; h2 += h2; h3 += h3; h4 += h4; h5 += h5; h6 += h6; h7 += h7; h8 += h8; h9 += h9;
+    return fe_carry( h0, h1, h2, h3, h4, h5, h6, h7, h8, h9 );
+  }
+  return fe_carry_b( h0, h1, h2, h3, h4, h5, h6, h7, h8, h9 );
 }
 
 FD_DEV fe fe_sq( fe const & f ) { return fe_sqn<1>( f ); }
 
-FD_DEV fe fe_sq_iter( fe const & f, int n ) {
-  fe h = fe_sq( f );
-  for( int i=1; i<n; i++ ) h = fe_sq( h );
+FD_DEV fe fe_sq_iter( fe h, int n ) {
+  _Pragma("unroll 1")
+  for( int i=0; i<n; i++ ) h = fe_sq( h );
   return h;
 }
 

@@ -349,7 +349,19 @@ enum { PH_DBL = 0, PH_ADDA = 1, PH_ADDB = 2, PH_FIN = 3, PH_DONE = 4 };
  * takes one more step (PH_FIN): its p1p1->p2 result is R', compared with
  * the limb memcmp of fd_ed25519_user.c:417-425, then it idles (PH_DONE).
  */
-__global__ void __launch_bounds__(64)
+#ifndef FD_DSM_QLDS
+#define FD_DSM_QLDS 0      /* 1: stage the next op's table operand in LDS (LDS-DMA) instead of VGPRs */
+#endif
+#ifndef FD_DSM_WAVES
+#define FD_DSM_WAVES 0     /* >0: __launch_bounds__ min waves per SIMD */
+#endif
+#if FD_DSM_WAVES
+#define FD_DSM_LB __launch_bounds__(64, FD_DSM_WAVES)
+#else
+#define FD_DSM_LB __launch_bounds__(64)
+#endif
+
+__global__ void FD_DSM_LB
 k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats ) {
   __shared__ i32 bi[8][40];
   for( int k=threadIdx.x; k<8*40; k+=64 ) {
@@ -405,25 +417,49 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
   int p   = act ? ((int const *)(ws + L.top))[ii] : -1;
   int ph  = act ? (p >= 0 ? PH_DBL : PH_FIN) : PH_DONE;
   u64 dc  = (p >= 0) ? dg[p >> 2] : 0UL;             /* digits of the 4-position group of p */
+  u64 dn  = (p >= 4) ? dg[(p >> 2) - 1] : 0UL;       /* next (lower) group, prefetched */
   int cur = (int)((dc >> (16 * (p & 3))) & 0xffffu); /* (a_p, b_p) as int8 pair */
+  i32 const * Rw = (i32 const *)(ws + L.R);
   u32 nha = 0, nhb = 0;
   u32 nit = (u32)(p + 1);
   bool qneg = false;
-  fe qZ, qM, qP, qT;
-  _Pragma("unroll") for( int k=0; k<10; k++ ) { qZ.v[k] = 0; qM.v[k] = 0; qP.v[k] = 0; qT.v[k] = 0; }
+
+  /* The next op's table operand q = [qZ | qM | qP | qT] (40 limbs) lives in
+     LDS, qs[limb][lane], not in VGPRs: ADD(A) entries arrive by LDS-DMA
+     (global_load_lds, per-lane source row) one step ahead, ADD(B) entries
+     are copied from the LDS base table, R.X / R.Y land in rows 0..19 for
+     the final compare.  Freed VGPRs buy a third wave per SIMD. */
+#if FD_DSM_QLDS
+  int lane = (int)threadIdx.x;
+  __shared__ i32 qs[40][64];
+# define QV( R_, K_ ) qs[(R_)*10 + (K_)][lane]
+# define Q_SET( R_, K_, V_ ) ( qs[(R_)*10 + (K_)][lane] = (V_) )
+# define Q_GLOBAL( R_, K_, S_ ) __builtin_amdgcn_global_load_lds( (void const *)(S_), (void __attribute__((address_space(3))) *)&qs[(R_)*10 + (K_)][0], 4, 0, 0 )
+#else
+  fe q[4];
+  _Pragma("unroll") for( int r=0; r<4; r++ ) q[r] = fe_zero();
+# define QV( R_, K_ ) q[R_].v[K_]
+# define Q_SET( R_, K_, V_ ) ( q[R_].v[K_] = (V_) )
+# define Q_GLOBAL( R_, K_, S_ ) ( q[R_].v[K_] = *(S_) )
+#endif
+  if( ph == PH_FIN ) {   /* both scalars zero: R' = (0:1:1) */
+    _Pragma("unroll") for( int k=0; k<10; k++ ) { Q_SET( 0, k, Rw[(size_t)k*N + ii] ); Q_SET( 1, k, Rw[(size_t)(10+k)*N + ii] ); }
+  }
   p1p1 t;   /* identity as a completed point: p1p1->p3 gives (0,1,1,0) */
   t.X = fe_zero(); t.Y = fe_one(); t.Z = fe_one(); t.T = fe_one();
 
   for( ;; ) {
     /* p1p1 -> p3 (its X,Y,Z are the reference's p1p1 -> p2) */
     p3 u = ge_p1p1_to_p3( t );
+#if FD_DSM_QLDS
+    asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );   /* LDS-DMA of q (issued last step) has landed */
+#endif
 
     bool fin = (ph == PH_FIN);
     if( __any( fin ) ) {
       if( fin ) {
-        i32 const * Rw = (i32 const *)(ws + L.R);
         fe RX, RY;
-        _Pragma("unroll") for( int k=0; k<10; k++ ) { RX.v[k] = Rw[(size_t)k*N + ii]; RY.v[k] = Rw[(size_t)(10+k)*N + ii]; }
+        _Pragma("unroll") for( int k=0; k<10; k++ ) { RX.v[k] = QV( 0, k ); RY.v[k] = QV( 1, k ); }
         fe xZ = fe_mul( u.Z, RX );
         fe yZ = fe_mul( u.Z, RY );
         bool eq = true;
@@ -436,19 +472,19 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
 
     /* op body: 4 field muls with per-lane operands */
     bool isD = (ph == PH_DBL);
-    fe a0, b0, a1, b1, a2, b2, a3, b3;
-    _Pragma("unroll") for( int k=0; k<10; k++ ) {
-      i32 X = u.X.v[k], Y = u.Y.v[k], Z = u.Z.v[k], T = u.T.v[k];
-      i32 xy = X + Y, ymx = Y - X;
-      a0.v[k] = isD ? xy : Z;    b0.v[k] = isD ? xy : qZ.v[k];
-      a1.v[k] = isD ? Y  : ymx;  b1.v[k] = isD ? Y  : qM.v[k];
-      a2.v[k] = isD ? X  : xy;   b2.v[k] = isD ? X  : qP.v[k];
-      a3.v[k] = isD ? Z  : T;    b3.v[k] = isD ? Z + Z : qT.v[k];
+    fe m0, m1, m2, m3;
+    {
+      fe a, b;
+      _Pragma("unroll") for( int k=0; k<10; k++ ) { i32 xy = u.X.v[k] + u.Y.v[k]; a.v[k] = isD ? xy : u.Z.v[k]; b.v[k] = isD ? xy : QV( 0, k ); }
+      m0 = fe_mul( a, b );
+      _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = isD ? u.Y.v[k] : u.Y.v[k] - u.X.v[k]; b.v[k] = isD ? u.Y.v[k] : QV( 1, k ); }
+      m1 = fe_mul( a, b );
+      _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = isD ? u.X.v[k] : u.X.v[k] + u.Y.v[k]; b.v[k] = isD ? u.X.v[k] : QV( 2, k ); }
+      m2 = fe_mul( a, b );
+      _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = isD ? u.Z.v[k] : u.T.v[k]; b.v[k] = isD ? u.Z.v[k] + u.Z.v[k] : QV( 3, k ); }
+      m3 = fe_mul( a, b );
     }
-    fe m0 = fe_mul( a0, b0 );
-    fe m1 = fe_mul( a1, b1 );
-    fe m2 = fe_mul( a2, b2 );
-    fe m3 = fe_mul( a3, b3 );
+    bool idle = (ph == PH_DONE);
     _Pragma("unroll") for( int k=0; k<10; k++ ) {
       i32 A0 = m0.v[k], A1 = m1.v[k], A2 = m2.v[k], A3 = m3.v[k];
       /* DBL mix [a-b-c, b+c, b-c, d-b+c]; ADD mix [P-M, P+M, 2Z+-T, 2Z-+T] */
@@ -456,7 +492,6 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
       i32 dX = A0 - A1 - A2, dY = A1 + A2, dZ = A1 - A2, dT = A3 - A1 + A2;
       i32 aX = A2 - A1,      aY = A2 + A1;
       i32 aZ = qneg ? z2 - A3 : z2 + A3, aT = qneg ? z2 + A3 : z2 - A3;
-      bool idle = (ph == PH_DONE);
       t.X.v[k] = idle ? 0       : (isD ? dX : aX);
       t.Y.v[k] = idle ? (k==0)  : (isD ? dY : aY);
       t.Z.v[k] = idle ? (k==0)  : (isD ? dZ : aZ);
@@ -474,39 +509,44 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
       p--;
       if( p < 0 ) nph = PH_FIN;
       else {
-        if( (p & 3) == 3 ) dc = dg[p >> 2];
+        if( (p & 3) == 3 ) { dc = dn; dn = (p >= 4) ? dg[(p >> 2) - 1] : 0UL; }
         cur = (int)((dc >> (16 * (p & 3))) & 0xffffu);
         nph = PH_DBL;
       }
     }
     ph = nph;
 
-    /* prefetch the next op's table entry (consumed one step later, after
-       the next p1p1->p3, so the load latency hides under 4 muls) */
+    /* stage the next op's operand into qs (consumed after the next
+       p1p1->p3, so the DMA latency hides under 4 field muls) */
     if( ph == PH_ADDA ) {
       nha++;
       int e = (da < 0 ? -da : da) >> 1;
       qneg = da < 0;
       size_t rZ = (size_t)e*40, rM = rZ + (qneg ? 20 : 10), rP = rZ + (qneg ? 10 : 20), rT = rZ + 30;
       _Pragma("unroll") for( int k=0; k<10; k++ ) {
-        qZ.v[k] = Aiw[(rZ + k)*N + ii];
-        qM.v[k] = Aiw[(rM + k)*N + ii];
-        qP.v[k] = Aiw[(rP + k)*N + ii];
-        qT.v[k] = Aiw[(rT + k)*N + ii];
+        Q_GLOBAL( 0, k, Aiw + (rZ + k)*N + ii );
+        Q_GLOBAL( 1, k, Aiw + (rM + k)*N + ii );
+        Q_GLOBAL( 2, k, Aiw + (rP + k)*N + ii );
+        Q_GLOBAL( 3, k, Aiw + (rT + k)*N + ii );
       }
+    } else if( ph == PH_FIN ) {
+      _Pragma("unroll") for( int k=0; k<10; k++ ) { Q_GLOBAL( 0, k, Rw + (size_t)k*N + ii ); Q_GLOBAL( 1, k, Rw + (size_t)(10+k)*N + ii ); }
     } else if( ph == PH_ADDB ) {
       nhb++;
       int e = (db < 0 ? -db : db) >> 1;
       qneg = db < 0;
       int oM = qneg ? 20 : 10, oP = qneg ? 10 : 20;
       _Pragma("unroll") for( int k=0; k<10; k++ ) {
-        qZ.v[k] = bi[e][k];
-        qM.v[k] = bi[e][oM + k];
-        qP.v[k] = bi[e][oP + k];
-        qT.v[k] = bi[e][30 + k];
+        Q_SET( 0, k, bi[e][k] );
+        Q_SET( 1, k, bi[e][oM + k] );
+        Q_SET( 2, k, bi[e][oP + k] );
+        Q_SET( 3, k, bi[e][30 + k] );
       }
     }
   }
+# undef QV
+# undef Q_SET
+# undef Q_GLOBAL
 
   if( want_stats && i < n ) {
     u32 * st = (u32 *)(ws + L.st);

@@ -21,7 +21,7 @@ FD_ED25519_SIG_SZ = 64
 MSG_MAX = 1232
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfd_ed25519_amd.so")
+LIB_PATH = os.environ.get("FD_AMD_LIB") or os.path.join(_HERE, "libfd_ed25519_amd.so")   # override: A/B builds only
 
 _lib = None
 
