@@ -25,7 +25,9 @@
  *   top  : int32  [N]          highest nonzero digit position (-1 if none)
  *   A    : int32  [30][N]      -A.X, A.Y, -A.T   (A.Z == 1)
  *   R    : int32  [20][N]      R.X, R.Y
- *   Ai   : int32  [8][40][N]   cached odd multiples of -A, lanes [Z,Y-X,Y+X,2dT]
+ *   Ai   : int32  [N][8][4][12] cached odd multiples of -A, rows [Z,Y-X,Y+X,2dT] of
+ *                              10 limbs padded to 12: per-lane contiguous (one ADD gathers
+ *                              192 contiguous bytes instead of 40 scattered dwords)
  *   st   : uint32 [3][N]       work statistics (iterations, nnz h, nnz s)
  */
 
@@ -50,7 +52,7 @@ fd_amd_ws_layout( size_t n ) {
   L.top = o; o = ws_al( o + 4UL*N );
   L.A   = o; o = ws_al( o + 4UL*30UL*N );
   L.R   = o; o = ws_al( o + 4UL*20UL*N );
-  L.Ai  = o; o = ws_al( o + 4UL*320UL*N );
+  L.Ai  = o; o = ws_al( o + 4UL*384UL*N );
   L.st  = o; o = ws_al( o + 4UL*3UL*N );
   L.total = o;
   return L;
@@ -379,7 +381,7 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
   bool act = (i < n) && (err[i] == 1);
   size_t N = L.N;
   u32 ii = (i < n) ? i : 0u;
-  i32 * Aiw = (i32 *)(ws + L.Ai);
+  i32 * Ail = (i32 *)(ws + L.Ai) + (size_t)ii*384u;   /* this lane's 8 x 4 x 12 table */
 
   /* -A (p3, Z = 1) and its odd multiples Ai (:423-481) -> HBM */
   {
@@ -393,13 +395,13 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
     }
     fe cZ, cYmX, cYpX, cT2d;
     ge_to_cached( cZ, cYmX, cYpX, cT2d, A );
-#   define AI_STORE( e ) do {                                                       \
-      _Pragma("unroll") for( int k=0; k<10; k++ ) {                                 \
-        Aiw[((size_t)(e)*40 + 0 + k)*N + ii] = cZ.v[k];                             \
-        Aiw[((size_t)(e)*40 + 10 + k)*N + ii] = cYmX.v[k];                          \
-        Aiw[((size_t)(e)*40 + 20 + k)*N + ii] = cYpX.v[k];                          \
-        Aiw[((size_t)(e)*40 + 30 + k)*N + ii] = cT2d.v[k];                          \
-      } } while(0)
+#   define AI_ROW( e, r, f ) do {                                                   \
+      int4 * d_ = (int4 *)(Ail + (e)*48 + (r)*12);                                  \
+      d_[0] = make_int4( f.v[0], f.v[1], f.v[2], f.v[3] );                          \
+      d_[1] = make_int4( f.v[4], f.v[5], f.v[6], f.v[7] );                          \
+      d_[2] = make_int4( f.v[8], f.v[9], 0, 0 );                                    \
+    } while(0)
+#   define AI_STORE( e ) do { AI_ROW( e, 0, cZ ); AI_ROW( e, 1, cYmX ); AI_ROW( e, 2, cYpX ); AI_ROW( e, 3, cT2d ); } while(0)
     if( act ) AI_STORE( 0 );
     p1p1 t = ge_dbl( A.X, A.Y, A.Z );
     p3 A2 = ge_p1p1_to_p3( t );
@@ -410,6 +412,7 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
       if( act ) AI_STORE( e+1 );
     }
 #   undef AI_STORE
+#   undef AI_ROW
   }
 
   /* lane state */
@@ -522,13 +525,16 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
       nha++;
       int e = (da < 0 ? -da : da) >> 1;
       qneg = da < 0;
-      size_t rZ = (size_t)e*40, rM = rZ + (qneg ? 20 : 10), rP = rZ + (qneg ? 10 : 20), rT = rZ + 30;
-      _Pragma("unroll") for( int k=0; k<10; k++ ) {
-        Q_GLOBAL( 0, k, Aiw + (rZ + k)*N + ii );
-        Q_GLOBAL( 1, k, Aiw + (rM + k)*N + ii );
-        Q_GLOBAL( 2, k, Aiw + (rP + k)*N + ii );
-        Q_GLOBAL( 3, k, Aiw + (rT + k)*N + ii );
-      }
+      int4 const * src = (int4 const *)(Ail + e*48);
+      int rowM = qneg ? 2 : 1, rowP = qneg ? 1 : 2;
+#     define Q_ROW( r, c ) do {                                                      \
+        int4 x0 = src[3*(c)], x1 = src[3*(c)+1], x2 = src[3*(c)+2];                \
+        Q_SET( r, 0, x0.x ); Q_SET( r, 1, x0.y ); Q_SET( r, 2, x0.z ); Q_SET( r, 3, x0.w ); \
+        Q_SET( r, 4, x1.x ); Q_SET( r, 5, x1.y ); Q_SET( r, 6, x1.z ); Q_SET( r, 7, x1.w ); \
+        Q_SET( r, 8, x2.x ); Q_SET( r, 9, x2.y );                                  \
+      } while(0)
+      Q_ROW( 0, 0 ); Q_ROW( 1, rowM ); Q_ROW( 2, rowP ); Q_ROW( 3, 3 );
+#     undef Q_ROW
     } else if( ph == PH_FIN ) {
       _Pragma("unroll") for( int k=0; k<10; k++ ) { Q_GLOBAL( 0, k, Rw + (size_t)k*N + ii ); Q_GLOBAL( 1, k, Rw + (size_t)(10+k)*N + ii ); }
     } else if( ph == PH_ADDB ) {
