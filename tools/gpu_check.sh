@@ -1,0 +1,14 @@
+#!/bin/bash
+# One GPU-box session: parity tests, bench line, rocprof kernel stats.
+# usage: tools/gpu_check.sh <tag>
+set -o pipefail
+TAG=${1:-run}
+O=gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { echo "tests failed"; tail -30 $O/tests.log; exit 1; }
+tail -3 $O/tests.log
+timeout -k 10 300 python3 bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
+cat $O/bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-latency > $O/prof.log 2>&1 || { echo "rocprof failed"; tail -20 $O/prof.log; exit 1; }
+find $O/prof -name "*kernel_stats.csv" -exec cat {} ;
