@@ -206,7 +206,10 @@ k_prep( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
 /* ------------------------------------------------------------------ */
 /* k_decomp: lane 2i -> A = pub[i], lane 2i+1 -> R = sig[i][0:32]       */
 
-__global__ void __launch_bounds__(64)
+#ifndef FD_DECOMP_WAVES
+#define FD_DECOMP_WAVES 2
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FD_DECOMP_WAVES)))
 k_decomp( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
           i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L ) {
   u32 t = blockIdx.x * 64u + threadIdx.x;
@@ -286,8 +289,10 @@ ge_dbl( fe const & X, fe const & Y, fe const & Z ) {
 __device__ __forceinline__ p3
 ge_p1p1_to_p3( p1p1 const & t ) {
   p3 u;
+  /* operand order chosen so the products share pre-multiples: g in {T, Y}
+     (x19) and f in {Z, X} (x2); mul is commutative at the integer level */
   u.Z = fe_mul( t.Z, t.T );
-  u.Y = fe_mul( t.Y, t.Z );
+  u.Y = fe_mul( t.Z, t.Y );
   u.X = fe_mul( t.X, t.T );
   u.T = fe_mul( t.X, t.Y );
   return u;
@@ -327,6 +332,15 @@ ge_to_cached( fe & cZ, fe & cYmX, fe & cYpX, fe & cT2d, p3 const & u ) {
 /* Base-point table in LDS, rows [Z(=1), Y-X, Y+X, 2dT] x 10 limbs per entry
    (table/fd_ed25519_ge_bi_precomp_avx.c:30-112 lane order). */
 __constant__ static i32 const BI_TABLE[8][3][10] = FD_AMD_BI_PRECOMP;   /* rows y+x, y-x, 2dxy */
+
+/* Branch-free per-lane select: v_cndmask_b32 on a wave lane mask (ballot).
+   Plain ?: on the op-stream selects lets LLVM re-form divergent branches
+   around the field muls (both sides then run with copies in between). */
+__device__ __forceinline__ i32 vsel( u64 m, i32 t, i32 f ) {
+  i32 r;
+  asm( "v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m) );
+  return r;
+}
 
 enum { PH_DBL = 0, PH_ADDA = 1, PH_ADDB = 2, PH_FIN = 3, PH_DONE = 4 };
 
@@ -473,32 +487,38 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
     }
     if( __all( ph == PH_DONE ) ) break;
 
-    /* op body: 4 field muls with per-lane operands */
+    /* op body: 4 field muls with per-lane operands, paired so that DBL and
+       ADD share what they can: m0 = (X+Y)*[(X+Y) | qP], m1 = [Y | Y-X]*[Y | qM],
+       m2 = [X | Z]*[X | qZ], m3 = [Z | T]*[2Z | qT] */
     bool isD = (ph == PH_DBL);
+    u64 mD = __builtin_amdgcn_ballot_w64( isD ), mN = __builtin_amdgcn_ballot_w64( qneg );
     fe m0, m1, m2, m3;
     {
       fe a, b;
-      _Pragma("unroll") for( int k=0; k<10; k++ ) { i32 xy = u.X.v[k] + u.Y.v[k]; a.v[k] = isD ? xy : u.Z.v[k]; b.v[k] = isD ? xy : QV( 0, k ); }
+      _Pragma("unroll") for( int k=0; k<10; k++ ) { i32 xy = u.X.v[k] + u.Y.v[k]; a.v[k] = xy; b.v[k] = vsel( mD, xy, QV( 2, k ) ); }
       m0 = fe_mul( a, b );
-      _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = isD ? u.Y.v[k] : u.Y.v[k] - u.X.v[k]; b.v[k] = isD ? u.Y.v[k] : QV( 1, k ); }
+      _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = vsel( mD, u.Y.v[k], u.Y.v[k] - u.X.v[k] ); b.v[k] = vsel( mD, u.Y.v[k], QV( 1, k ) ); }
       m1 = fe_mul( a, b );
-      _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = isD ? u.X.v[k] : u.X.v[k] + u.Y.v[k]; b.v[k] = isD ? u.X.v[k] : QV( 2, k ); }
+      _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = vsel( mD, u.X.v[k], u.Z.v[k] ); b.v[k] = vsel( mD, u.X.v[k], QV( 0, k ) ); }
       m2 = fe_mul( a, b );
-      _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = isD ? u.Z.v[k] : u.T.v[k]; b.v[k] = isD ? u.Z.v[k] + u.Z.v[k] : QV( 3, k ); }
+      _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = vsel( mD, u.Z.v[k], u.T.v[k] ); b.v[k] = vsel( mD, u.Z.v[k] + u.Z.v[k], QV( 3, k ) ); }
       m3 = fe_mul( a, b );
     }
-    bool idle = (ph == PH_DONE);
+    /* lanes that are done (PH_DONE) keep computing on don't-care values:
+       nothing they compute is stored */
     _Pragma("unroll") for( int k=0; k<10; k++ ) {
       i32 A0 = m0.v[k], A1 = m1.v[k], A2 = m2.v[k], A3 = m3.v[k];
-      /* DBL mix [a-b-c, b+c, b-c, d-b+c]; ADD mix [P-M, P+M, 2Z+-T, 2Z-+T] */
-      i32 z2 = A0 + A0;
+      /* DBL mix [a-b-c, b+c, b-c, d-b+c] with a=m0 b=m1 c=m2 d=m3;
+         ADD mix [P-M, P+M, 2Z+-T, 2Z-+T] with P=m0 M=m1 Z=m2 T=m3 */
+      i32 z2 = A2 + A2;
       i32 dX = A0 - A1 - A2, dY = A1 + A2, dZ = A1 - A2, dT = A3 - A1 + A2;
-      i32 aX = A2 - A1,      aY = A2 + A1;
-      i32 aZ = qneg ? z2 - A3 : z2 + A3, aT = qneg ? z2 + A3 : z2 - A3;
-      t.X.v[k] = idle ? 0       : (isD ? dX : aX);
-      t.Y.v[k] = idle ? (k==0)  : (isD ? dY : aY);
-      t.Z.v[k] = idle ? (k==0)  : (isD ? dZ : aZ);
-      t.T.v[k] = idle ? (k==0)  : (isD ? dT : aT);
+      i32 aX = A0 - A1,      aY = A0 + A1;
+      i32 zp = z2 + A3, zm = z2 - A3;
+      i32 aZ = vsel( mN, zm, zp ), aT = vsel( mN, zp, zm );
+      t.X.v[k] = vsel( mD, dX, aX );
+      t.Y.v[k] = vsel( mD, dY, aY );
+      t.Z.v[k] = vsel( mD, dZ, aZ );
+      t.T.v[k] = vsel( mD, dT, aT );
     }
 
     /* advance the lane's op stream */
