@@ -18,6 +18,7 @@
 #include <mutex>
 
 #include "../../include/fd_ed25519_amd.h"
+#include "../../include/fd_txn_amd.h"
 #include "fd_ed25519_kernels.h"
 
 #define HIPCHK( x ) do { hipError_t _e = (x); if( _e != hipSuccess ) {                          \
@@ -40,6 +41,16 @@ struct slot_t {
   schar *    out;
   ulong      n;
   int        busy;
+  /* transaction front end (allocated on first use): per-transaction
+     payload offset/size, footprint, signature-slot base, verdict; per-slot
+     skip plane */
+  uint32_t * d_toff; uint32_t * d_tsz; uint32_t * d_fp; uint32_t * d_tbase; int8_t * d_terr; int8_t * d_skip;
+  uint32_t * h_toff; uint32_t * h_tsz; uint32_t * h_tbase; int8_t * h_terr;
+  /* transaction chunk in flight */
+  schar *    t_out;      /* per-transaction verdicts */
+  ulong      t_n;
+  schar *    s_out;      /* per-signature verdicts (optional) */
+  ulong      s_n;
 };
 
 } /* namespace */
@@ -66,6 +77,16 @@ slot_free( slot_t * s ) {
   if( s->h_off  ) (void)hipHostFree( s->h_off );
   if( s->h_sz   ) (void)hipHostFree( s->h_sz );
   if( s->h_err  ) (void)hipHostFree( s->h_err );
+  if( s->d_toff ) (void)hipFree( s->d_toff );
+  if( s->d_tsz  ) (void)hipFree( s->d_tsz );
+  if( s->d_fp   ) (void)hipFree( s->d_fp );
+  if( s->d_tbase) (void)hipFree( s->d_tbase );
+  if( s->d_terr ) (void)hipFree( s->d_terr );
+  if( s->d_skip ) (void)hipFree( s->d_skip );
+  if( s->h_toff ) (void)hipHostFree( s->h_toff );
+  if( s->h_tsz  ) (void)hipHostFree( s->h_tsz );
+  if( s->h_tbase) (void)hipHostFree( s->h_tbase );
+  if( s->h_terr ) (void)hipHostFree( s->h_terr );
   if( s->stream ) (void)hipStreamDestroy( s->stream );
   if( s->done   ) (void)hipEventDestroy( s->done );
   memset( s, 0, sizeof(*s) );
@@ -122,12 +143,31 @@ fd_ed25519_amd_delete( fd_ed25519_amd_t * e ) {
   free( e );
 }
 
+static int
+slot_alloc_txn( slot_t * s, ulong cap ) {
+  if( s->d_toff ) return FD_ED25519_AMD_OK;
+  HIPCHK( hipMalloc( (void **)&s->d_toff,  4UL*cap ) );
+  HIPCHK( hipMalloc( (void **)&s->d_tsz,   4UL*cap ) );
+  HIPCHK( hipMalloc( (void **)&s->d_fp,    4UL*cap ) );
+  HIPCHK( hipMalloc( (void **)&s->d_tbase, 4UL*(cap+1UL) ) );
+  HIPCHK( hipMalloc( (void **)&s->d_terr,  cap ) );
+  HIPCHK( hipMalloc( (void **)&s->d_skip,  cap ) );
+  HIPCHK( hipHostMalloc( (void **)&s->h_toff,  4UL*cap, hipHostMallocDefault ) );
+  HIPCHK( hipHostMalloc( (void **)&s->h_tsz,   4UL*cap, hipHostMallocDefault ) );
+  HIPCHK( hipHostMalloc( (void **)&s->h_tbase, 4UL*(cap+1UL), hipHostMallocDefault ) );
+  HIPCHK( hipHostMalloc( (void **)&s->h_terr,  cap, hipHostMallocDefault ) );
+  return FD_ED25519_AMD_OK;
+}
+
 /* Wait for a slot's chunk and deliver its verdicts. */
 static int
 slot_drain( slot_t * s ) {
   if( !s->busy ) return FD_ED25519_AMD_OK;
   HIPCHK( hipEventSynchronize( s->done ) );
-  memcpy( s->out, s->h_err, s->n );
+  if( s->out   ) memcpy( s->out,   s->h_err,  s->n );
+  if( s->t_out ) memcpy( s->t_out, s->h_terr, s->t_n );
+  if( s->s_out ) memcpy( s->s_out, s->h_err,  s->s_n );
+  s->out = s->t_out = s->s_out = NULL;
   s->busy = 0;
   return FD_ED25519_AMD_OK;
 }
@@ -145,6 +185,32 @@ slot_launch( slot_t * s, ulong n, ulong blob_sz, schar * out ) {
   HIPCHK( hipMemcpyAsync( s->h_err, s->d_err, n, hipMemcpyDeviceToHost, s->stream ) );
   HIPCHK( hipEventRecord( s->done, s->stream ) );
   s->out = out; s->n = n; s->busy = 1;
+  return FD_ED25519_AMD_OK;
+}
+
+/* Launch a staged transaction chunk: c transactions (payload bytes in
+   h_blob, rebased offsets in h_toff/h_tsz, signature-slot bases in
+   h_tbase[0..c]), nslot = h_tbase[c] signature slots. */
+static int
+slot_launch_txn( slot_t * s, ulong c, ulong nslot, ulong blob_sz, schar * t_out, schar * s_out ) {
+  HIPCHK( hipMemcpyAsync( s->d_toff,  s->h_toff,  4UL*c,        hipMemcpyHostToDevice, s->stream ) );
+  HIPCHK( hipMemcpyAsync( s->d_tsz,   s->h_tsz,   4UL*c,        hipMemcpyHostToDevice, s->stream ) );
+  HIPCHK( hipMemcpyAsync( s->d_tbase, s->h_tbase, 4UL*(c+1UL),  hipMemcpyHostToDevice, s->stream ) );
+  if( blob_sz ) HIPCHK( hipMemcpyAsync( s->d_blob, s->h_blob, blob_sz, hipMemcpyHostToDevice, s->stream ) );
+  if( fd_amd_launch_txn_parse( (uint32_t)c, s->d_blob, s->d_toff, s->d_tsz, s->d_fp, NULL, 0, s->d_tbase,
+                               s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_skip, s->stream ) )
+    return FD_ED25519_AMD_ERR_DEVICE;
+  if( nslot && fd_amd_launch_verify( (uint32_t)nslot, s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_blob, s->d_err,
+                                     s->d_ws, s->stream, 0, NULL, s->d_skip ) )
+    return FD_ED25519_AMD_ERR_DEVICE;
+  if( fd_amd_launch_txn_reduce( (uint32_t)c, s->d_fp, s->d_tbase, s->d_err, s->d_terr, s->stream ) )
+    return FD_ED25519_AMD_ERR_DEVICE;
+  HIPCHK( hipMemcpyAsync( s->h_terr, s->d_terr, c, hipMemcpyDeviceToHost, s->stream ) );
+  if( s_out && nslot ) HIPCHK( hipMemcpyAsync( s->h_err, s->d_err, nslot, hipMemcpyDeviceToHost, s->stream ) );
+  HIPCHK( hipEventRecord( s->done, s->stream ) );
+  s->t_out = t_out; s->t_n = c;
+  s->s_out = nslot ? s_out : NULL; s->s_n = nslot;
+  s->busy = 1;
   return FD_ED25519_AMD_OK;
 }
 
@@ -196,6 +262,66 @@ fd_ed25519_amd_verify_soa( fd_ed25519_amd_t * e, ulong n, uchar const * pub, uch
   return run_chunked( e, n, err, [&]( ulong i, uint8_t const ** m, ulong * s, uint8_t const ** g, uint8_t const ** p ) {
     *m = blob + msg_off[i]; *s = msg_sz[i]; *g = sig + 64UL*i; *p = pub + 32UL*i;
   } );
+}
+
+/* Signature slots the engine reserves for a payload: its first byte when
+   that is a plausible signature count (fd_txn_parse.c:79-82 accept it),
+   else 0.  Exact for every payload that parses. */
+static inline ulong
+txn_slots( uchar const * p, ulong sz ) {
+  if( !sz ) return 0UL;
+  ulong k = p[0];
+  return ( k >= 1UL && k <= FD_TXN_SIG_MAX && 64UL*k <= sz - 1UL ) ? k : 0UL;
+}
+
+extern "C" int
+fd_ed25519_amd_verify_txns( fd_ed25519_amd_t * e, ulong txn_cnt, uchar const * payload, uint const * txn_off,
+                            uint const * txn_sz, ulong payload_sz, schar * txn_err, uint * sig_base, schar * sig_err ) {
+  if( !e || (txn_cnt && (!payload || !txn_off || !txn_sz || !txn_err)) ) return FD_ED25519_AMD_ERR_INVAL;
+  if( sig_err && !sig_base ) return FD_ED25519_AMD_ERR_INVAL;
+  for( ulong t=0; t<txn_cnt; t++ )
+    if( txn_sz[t] > FD_TXN_AMD_MTU || (ulong)txn_off[t] + txn_sz[t] > payload_sz ) return FD_ED25519_AMD_ERR_INVAL;
+  if( hipSetDevice( e->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  int rc;
+  for( int k=0; k<2; k++ ) if( (rc = slot_alloc_txn( &e->slot[k], e->cap )) ) return rc;
+  /* global signature numbering (the caller-visible sig_base) */
+  uint acc = 0U;
+  if( sig_base ) {
+    for( ulong t=0; t<txn_cnt; t++ ) { sig_base[t] = acc; acc += (uint)txn_slots( payload + txn_off[t], txn_sz[t] ); }
+    sig_base[txn_cnt] = acc;
+  }
+  ulong t = 0, gsig = 0; int k = 0;
+  while( t < txn_cnt ) {
+    slot_t * s = &e->slot[k];
+    if( (rc = slot_drain( s )) ) return rc;
+    ulong c = 0, bsz = 0, ns = 0;
+    while( t + c < txn_cnt && c < e->cap ) {
+      uchar const * p = payload + txn_off[t+c];
+      ulong sz = txn_sz[t+c], k2 = txn_slots( p, sz );
+      if( bsz + sz > e->blob_cap || ns + k2 > e->cap ) break;
+      if( sz ) memcpy( s->h_blob + bsz, p, sz );
+      s->h_toff[c] = (uint32_t)bsz; s->h_tsz[c] = (uint32_t)sz; s->h_tbase[c] = (uint32_t)ns;
+      bsz += sz; ns += k2; c++;
+    }
+    s->h_tbase[c] = (uint32_t)ns;
+    if( (rc = slot_launch_txn( s, c, ns, bsz, txn_err + t, sig_err ? sig_err + gsig : NULL )) ) return rc;
+    t += c; gsig += ns; k ^= 1;
+  }
+  for( int j=0; j<2; j++ ) if( (rc = slot_drain( &e->slot[j] )) ) return rc;
+  return FD_ED25519_AMD_OK;
+}
+
+extern "C" int
+fd_txn_amd_parse_dev( ulong txn_cnt, uchar const * d_payload, uint const * d_txn_off, uint const * d_txn_sz,
+                      uint * d_footprint, uchar * d_out, ulong out_stride, void * stream ) {
+  if( txn_cnt > 0xFFFFFFFFUL ) return FD_ED25519_AMD_ERR_INVAL;
+  if( !txn_cnt ) return FD_ED25519_AMD_OK;
+  if( !d_payload || !d_txn_off || !d_txn_sz || !d_footprint ) return FD_ED25519_AMD_ERR_INVAL;
+  if( d_out && (out_stride < FD_TXN_MAX_SZ || (out_stride & 1UL)) ) return FD_ED25519_AMD_ERR_INVAL;
+  if( fd_amd_launch_txn_parse( (uint32_t)txn_cnt, d_payload, d_txn_off, d_txn_sz, d_footprint, d_out, out_stride,
+                               NULL, NULL, NULL, NULL, NULL, NULL, (hipStream_t)stream ) )
+    return FD_ED25519_AMD_ERR_DEVICE;
+  return FD_ED25519_AMD_OK;
 }
 
 extern "C" ulong

@@ -16,9 +16,29 @@ typedef struct {
 ws_layout_t fd_amd_ws_layout( size_t n );
 
 /* Enqueue k_prep -> k_decomp -> k_dsm on `stream`; when ev != NULL record
-   ev[0..3] before/between/after the three kernels.  0 on success. */
+   ev[0..3] before/between/after the three kernels.  d_skip (NULL = none):
+   per-signature int8, nonzero = do not verify, the verdict is that value
+   (transaction slots whose payload failed to parse).  0 on success. */
 int fd_amd_launch_verify( uint32_t n, uint8_t const * d_pub, uint8_t const * d_sig, uint32_t const * d_off,
                           uint32_t const * d_sz, uint8_t const * d_blob, int8_t * d_err, void * d_ws,
-                          hipStream_t stream, int want_stats, hipEvent_t const * ev /* 4 or NULL */ );
+                          hipStream_t stream, int want_stats, hipEvent_t const * ev /* 4 or NULL */,
+                          int8_t const * d_skip = NULL );
+
+/* Transaction front end (fd_txn_kernels.hip).
+   k_txn_parse: one lane per transaction t = d_payload[d_toff[t] .. +d_tsz[t]).
+     d_fp[t] = fd_txn_parse return value; d_out (optional) + t*out_stride gets
+     the fd_txn_t descriptor.  When d_tbase != NULL it also lays out the
+     transaction's signatures for the verify kernels at slots
+     [d_tbase[t], d_tbase[t+1]): pub/sig copied from the payload, msg_off/msg_sz
+     pointing at the shared message inside d_payload, skip = 0; a payload that
+     fails to parse marks its slots skip = FD_TXN_AMD_ERR_PARSE.
+   k_txn_reduce: d_terr[t] = parse failure code, or the first nonzero
+     verdict among the transaction's slots, or 0. */
+int fd_amd_launch_txn_parse( uint32_t txn_cnt, uint8_t const * d_payload, uint32_t const * d_toff,
+                             uint32_t const * d_tsz, uint32_t * d_fp, uint8_t * d_out, size_t out_stride,
+                             uint32_t const * d_tbase, uint8_t * d_pub, uint8_t * d_sig, uint32_t * d_off,
+                             uint32_t * d_sz, int8_t * d_skip, hipStream_t stream );
+int fd_amd_launch_txn_reduce( uint32_t txn_cnt, uint32_t const * d_fp, uint32_t const * d_tbase,
+                              int8_t const * d_err, int8_t * d_terr, hipStream_t stream );
 
 #endif

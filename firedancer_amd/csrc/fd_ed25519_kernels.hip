@@ -132,9 +132,15 @@ slide_reg( u32 const a[8], EMIT emit ) {
 __global__ void __launch_bounds__(64)
 k_prep( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
         u32 const * __restrict__ msg_off, u32 const * __restrict__ msg_sz,
-        u8 const * __restrict__ blob, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L ) {
+        u8 const * __restrict__ blob, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L,
+        i8 const * __restrict__ skip ) {
   u32 i = blockIdx.x * 64u + threadIdx.x;
   if( i >= n ) return;
+  if( skip && skip[i] ) {   /* slot of a transaction that failed to parse (fd_txn_kernels.hip) */
+    ((int *)(ws + L.top))[i] = -1;
+    err[i] = (i8)skip[i];
+    return;
+  }
 
   /* R || A as 16 LE dwords (sig / pub records are 64- / 32-byte aligned) */
   uint4 const * S4 = (uint4 const *)(sig + 64UL*i);
@@ -586,13 +592,13 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
 int
 fd_amd_launch_verify( u32 n, u8 const * d_pub, u8 const * d_sig, u32 const * d_off, u32 const * d_sz,
                       u8 const * d_blob, i8 * d_err, void * d_ws, hipStream_t stream, int want_stats,
-                      hipEvent_t const * ev ) {
+                      hipEvent_t const * ev, i8 const * d_skip ) {
   if( !n ) return 0;
   ws_layout_t L = fd_amd_ws_layout( n );
   u8 * ws = (u8 *)d_ws;
   u32 nb = (n + 63u) / 64u;
   if( ev ) (void)hipEventRecord( ev[0], stream );
-  hipLaunchKernelGGL( k_prep,   dim3(nb),      dim3(64), 0, stream, n, d_pub, d_sig, d_off, d_sz, d_blob, d_err, ws, L );
+  hipLaunchKernelGGL( k_prep,   dim3(nb),      dim3(64), 0, stream, n, d_pub, d_sig, d_off, d_sz, d_blob, d_err, ws, L, d_skip );
   if( ev ) (void)hipEventRecord( ev[1], stream );
   hipLaunchKernelGGL( k_decomp, dim3(2u*nb),   dim3(64), 0, stream, n, d_pub, d_sig, d_err, ws, L );
   if( ev ) (void)hipEventRecord( ev[2], stream );

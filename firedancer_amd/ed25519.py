@@ -70,6 +70,10 @@ def lib():
     L.fd_ed25519_amd_version.restype = ctypes.c_char_p
     L.fd_ed25519_amd_sign_batch.argtypes = [ul, vp, vp, vp, vp, vp, vp, i]
     L.fd_ed25519_amd_sign_batch.restype = i
+    L.fd_ed25519_amd_verify_txns.argtypes = [vp, ul, vp, vp, vp, ul, vp, vp, vp]
+    L.fd_ed25519_amd_verify_txns.restype = i
+    L.fd_txn_amd_parse_dev.argtypes = [ul, vp, vp, vp, vp, vp, ul, vp]
+    L.fd_txn_amd_parse_dev.restype = i
     _lib = L
     return L
 
@@ -188,6 +192,27 @@ class Engine:
             raise EngineError("fd_ed25519_amd_verify_batch rc=%d" % rc)
         return err[:n]
 
+    def verify_txns(self, payload, txn_off, txn_sz, want_sigs=False):
+        """Wire-format transaction batch (include/fd_txn_amd.h): parse on the
+        GPU, verify every signature (multi-signer rule), one verdict per
+        transaction in {0, -1, -2, -3, FD_TXN_AMD_ERR_PARSE}.  With
+        want_sigs, also returns (sig_base, sig_err)."""
+        payload = np.ascontiguousarray(payload, np.uint8)
+        off = np.ascontiguousarray(txn_off, np.uint32)
+        sz = np.ascontiguousarray(txn_sz, np.uint32)
+        n = int(off.size)
+        terr = np.zeros(max(n, 1), np.int8)
+        base = np.zeros(n + 1, np.uint32) if want_sigs else None
+        serr = np.zeros(max(payload.size // 65 + 1, 1), np.int8) if want_sigs else None
+        rc = lib().fd_ed25519_amd_verify_txns(self._h, n, _ptr(payload), _ptr(off), _ptr(sz), int(payload.size),
+                                              _ptr(terr), _ptr(base) if want_sigs else None,
+                                              _ptr(serr) if want_sigs else None)
+        if rc:
+            raise EngineError("fd_ed25519_amd_verify_txns rc=%d" % rc)
+        if want_sigs:
+            return terr[:n], base, serr[:int(base[-1])]
+        return terr[:n]
+
 
 # ---------------------------------------------------------------- device-resident path
 
@@ -224,6 +249,18 @@ def debug_digits_dev(n, d_ws, d_dig, d_top, stream=0):
     rc = lib().fd_ed25519_amd_debug_digits_dev(int(n), d_ws, d_dig, d_top, stream)
     if rc:
         raise EngineError("fd_ed25519_amd_debug_digits_dev rc=%d" % rc)
+
+
+FD_TXN_AMD_ERR_PARSE = -4
+FD_TXN_MAX_SZ = 3570
+
+
+def txn_parse_dev(txn_cnt, d_payload, d_toff, d_tsz, d_fp, d_out=None, out_stride=0, stream=0):
+    """Device batch parse (fd_txn_amd_parse_dev): footprints (and optionally
+    fd_txn_t descriptors, out_stride apart) of txn_cnt wire transactions."""
+    rc = lib().fd_txn_amd_parse_dev(int(txn_cnt), d_payload, d_toff, d_tsz, d_fp, d_out, int(out_stride), stream)
+    if rc:
+        raise EngineError("fd_txn_amd_parse_dev rc=%d" % rc)
 
 
 def version():

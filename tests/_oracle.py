@@ -40,6 +40,12 @@ def oracle():
         L.oracle_stream_gen.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                         ctypes.c_int, vp, vp, vp, vp, vp, vp]
         L.oracle_stream_gen.restype = ctypes.c_uint64
+        L.oracle_txn_parse.argtypes = [vp, ctypes.c_ulong, vp, vp]
+        L.oracle_txn_parse.restype = ctypes.c_ulong
+        L.oracle_txn_parse_fail_line.argtypes = [vp, ctypes.c_ulong]
+        L.oracle_txn_parse_fail_line.restype = ctypes.c_ulong
+        L.oracle_txn_verify_batch.argtypes = [ctypes.c_ulong, vp, vp, vp, vp, vp, vp, ctypes.c_int]
+        L.oracle_txn_verify_batch.restype = ctypes.c_int
         _o = L
     return _o
 
@@ -115,3 +121,28 @@ def stream_inputs(seed, count, szlo, szhi, mixed):
     used = oracle().oracle_stream_gen(seed, count, szlo, szhi, int(mixed), _p(prv), _p(blob), _p(off), _p(sz),
                                       _p(fk), _p(fp))
     return prv, blob[:used + 1], off, sz, fk, fp
+
+
+def txn_parse(payload):
+    """oracle fd_txn_parse: (footprint, descriptor bytes[:footprint], fail line)."""
+    p = bytes(payload)
+    buf = ctypes.create_string_buffer(3570 + 16)
+    fp = oracle().oracle_txn_parse(p if p else None, len(p), buf, None)
+    line = 0 if fp else oracle().oracle_txn_parse_fail_line(p if p else None, len(p))
+    return int(fp), buf.raw[:fp], int(line)
+
+
+def txn_verify_batch(payload, txn_off, txn_sz, nthread=None):
+    """Multi-signer verdicts: (txn_err, sig_base, sig_err) -- the rule of
+    fd_ed25519_amd_verify_txns on the CPU oracle."""
+    payload = np.ascontiguousarray(payload, np.uint8)
+    off = np.ascontiguousarray(txn_off, np.uint32)
+    sz = np.ascontiguousarray(txn_sz, np.uint32)
+    n = off.size
+    terr = np.zeros(max(n, 1), np.int8)
+    base = np.zeros(n + 1, np.uint32)
+    serr = np.zeros(max(payload.size // 65 + 1, 1), np.int8)
+    if nthread is None:
+        nthread = min(16, os.cpu_count() or 1)
+    oracle().oracle_txn_verify_batch(n, _p(payload), _p(off), _p(sz), _p(terr), _p(base), _p(serr), nthread)
+    return terr[:n], base, serr[:int(base[-1])]

@@ -10,14 +10,21 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "fd_ed25519_amd.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in sorted(os.listdir(os.path.join(ROOT, "include")))
+           if h.endswith(".h")]
 
 
 def declared_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    names = re.findall(r"\b(fd_ed25519_\w+)\s*\(", src)
-    return sorted(set(names))
+    """Every extern function declared by include/*.h (static inline helpers
+    and macros excluded)."""
+    names = set()
+    for h in HEADERS:
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"^#.*$", "", src, flags=re.M)
+        src = re.sub(r"static inline[^{]*\{[^}]*\}", "", src)
+        names.update(re.findall(r"\b(fd_\w+)\s*\(", src))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():
@@ -25,6 +32,8 @@ def test_library_exports_every_declared_symbol():
     L = ed25519.lib()
     names = declared_functions()
     assert "fd_ed25519_verify" in names and "fd_ed25519_amd_verify_dev" in names
+    assert "fd_ed25519_amd_verify_txns" in names and "fd_txn_amd_parse_dev" in names
+    assert "fd_txn_footprint" not in names
     for n in names:
         assert hasattr(L, n), n
     # and as real dynamic symbols (a C / Rust / Go caller links by name)
@@ -44,7 +53,7 @@ def test_reference_codes_and_strerror():
     assert ed25519.strerror(-2) == "bad public key"
     assert ed25519.strerror(-3) == "bad message"
     assert ed25519.strerror(7) == "unknown"
-    hdr = open(HEADER).read()
+    hdr = open(os.path.join(ROOT, "include", "fd_ed25519_amd.h")).read()
     for name, val in (("FD_ED25519_SUCCESS", 0), ("FD_ED25519_ERR_SIG", -1), ("FD_ED25519_ERR_PUBKEY", -2),
                       ("FD_ED25519_ERR_MSG", -3)):
         assert re.search(r"#define %s\s+\(\s*%d\)" % (name, val), hdr), name
@@ -74,8 +83,11 @@ def test_c_caller_compiles_against_header(tmp_path):
     c = tmp_path / "caller.c"
     c.write_text('''
 #include "fd_ed25519_amd.h"
+#include "fd_txn_amd.h"
 #include <stdio.h>
 int main( void ) {
+  if( sizeof(fd_txn_t)!=20UL || sizeof(fd_txn_instr_t)!=10UL || sizeof(fd_txn_acct_addr_lut_t)!=8UL ) return 1;
+  if( fd_txn_footprint( 355UL, 0UL )!=FD_TXN_MAX_SZ ) return 1;   /* fd_txn.h:95 worst case */
   printf( "%s\\n", fd_ed25519_strerror( FD_ED25519_ERR_MSG ) );
   printf( "%lu\\n", fd_ed25519_amd_workspace_footprint( 64UL ) );
   return 0;
