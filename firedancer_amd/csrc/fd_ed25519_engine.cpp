@@ -26,41 +26,7 @@
              __FILE__, __LINE__ );                                                              \
     return FD_ED25519_AMD_ERR_DEVICE; } } while(0)
 
-namespace {
-
-struct slot_t {
-  /* device */
-  uint8_t  * d_pub;  uint8_t * d_sig; uint8_t * d_blob;
-  uint32_t * d_off;  uint32_t * d_sz; int8_t * d_err; void * d_ws;
-  /* pinned host staging */
-  uint8_t  * h_pub;  uint8_t * h_sig; uint8_t * h_blob;
-  uint32_t * h_off;  uint32_t * h_sz; int8_t * h_err;
-  hipStream_t stream;
-  hipEvent_t  done;
-  /* the chunk in flight: where its verdicts go */
-  schar *    out;
-  ulong      n;
-  int        busy;
-  /* transaction front end (allocated on first use): per-transaction
-     payload offset/size, footprint, signature-slot base, verdict; per-slot
-     skip plane */
-  uint32_t * d_toff; uint32_t * d_tsz; uint32_t * d_fp; uint32_t * d_tbase; int8_t * d_terr; int8_t * d_skip;
-  uint32_t * h_toff; uint32_t * h_tsz; uint32_t * h_tbase; int8_t * h_terr;
-  /* transaction chunk in flight */
-  schar *    t_out;      /* per-transaction verdicts */
-  ulong      t_n;
-  schar *    s_out;      /* per-signature verdicts (optional) */
-  ulong      s_n;
-};
-
-} /* namespace */
-
-struct fd_ed25519_amd {
-  int    device;
-  ulong  cap;        /* signatures per chunk */
-  ulong  blob_cap;   /* message bytes per chunk */
-  slot_t slot[2];
-};
+#include "fd_ed25519_engine.h"
 
 static void
 slot_free( slot_t * s ) {
@@ -87,6 +53,7 @@ slot_free( slot_t * s ) {
   if( s->h_tsz  ) (void)hipHostFree( s->h_tsz );
   if( s->h_tbase) (void)hipHostFree( s->h_tbase );
   if( s->h_terr ) (void)hipHostFree( s->h_terr );
+  if( s->h_tag  ) (void)hipHostFree( s->h_tag );
   if( s->stream ) (void)hipStreamDestroy( s->stream );
   if( s->done   ) (void)hipEventDestroy( s->done );
   memset( s, 0, sizeof(*s) );
@@ -143,8 +110,8 @@ fd_ed25519_amd_delete( fd_ed25519_amd_t * e ) {
   free( e );
 }
 
-static int
-slot_alloc_txn( slot_t * s, ulong cap ) {
+int
+fd_amd_slot_alloc_aux( slot_t * s, ulong cap ) {
   if( s->d_toff ) return FD_ED25519_AMD_OK;
   HIPCHK( hipMalloc( (void **)&s->d_toff,  4UL*cap ) );
   HIPCHK( hipMalloc( (void **)&s->d_tsz,   4UL*cap ) );
@@ -156,12 +123,13 @@ slot_alloc_txn( slot_t * s, ulong cap ) {
   HIPCHK( hipHostMalloc( (void **)&s->h_tsz,   4UL*cap, hipHostMallocDefault ) );
   HIPCHK( hipHostMalloc( (void **)&s->h_tbase, 4UL*(cap+1UL), hipHostMallocDefault ) );
   HIPCHK( hipHostMalloc( (void **)&s->h_terr,  cap, hipHostMallocDefault ) );
+  HIPCHK( hipHostMalloc( (void **)&s->h_tag,   8UL*cap, hipHostMallocDefault ) );
   return FD_ED25519_AMD_OK;
 }
 
 /* Wait for a slot's chunk and deliver its verdicts. */
-static int
-slot_drain( slot_t * s ) {
+int
+fd_amd_slot_drain( slot_t * s ) {
   if( !s->busy ) return FD_ED25519_AMD_OK;
   HIPCHK( hipEventSynchronize( s->done ) );
   if( s->out   ) memcpy( s->out,   s->h_err,  s->n );
@@ -173,8 +141,8 @@ slot_drain( slot_t * s ) {
 }
 
 /* Launch the staged chunk of slot s (inputs already in pinned memory). */
-static int
-slot_launch( slot_t * s, ulong n, ulong blob_sz, schar * out ) {
+int
+fd_amd_slot_launch( slot_t * s, ulong n, ulong blob_sz, schar * out, int want_tag ) {
   HIPCHK( hipMemcpyAsync( s->d_pub,  s->h_pub,  32UL*n, hipMemcpyHostToDevice, s->stream ) );
   HIPCHK( hipMemcpyAsync( s->d_sig,  s->h_sig,  64UL*n, hipMemcpyHostToDevice, s->stream ) );
   HIPCHK( hipMemcpyAsync( s->d_off,  s->h_off,  4UL*n,  hipMemcpyHostToDevice, s->stream ) );
@@ -183,9 +151,23 @@ slot_launch( slot_t * s, ulong n, ulong blob_sz, schar * out ) {
   if( fd_amd_launch_verify( (uint32_t)n, s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_blob, s->d_err, s->d_ws, s->stream, 1, NULL ) )
     return FD_ED25519_AMD_ERR_DEVICE;
   HIPCHK( hipMemcpyAsync( s->h_err, s->d_err, n, hipMemcpyDeviceToHost, s->stream ) );
+  if( want_tag ) {
+    ws_layout_t L = fd_amd_ws_layout( n );
+    HIPCHK( hipMemcpyAsync( s->h_tag, (uint8_t *)s->d_ws + L.tag, 8UL*n, hipMemcpyDeviceToHost, s->stream ) );
+  }
   HIPCHK( hipEventRecord( s->done, s->stream ) );
-  s->out = out; s->n = n; s->busy = 1;
+  s->out = out; s->n = n; s->busy = 1; s->want_tag = want_tag;
   return FD_ED25519_AMD_OK;
+}
+
+int
+fd_amd_slot_ready( slot_t * s ) {
+  if( !s->busy ) return 1;
+  hipError_t e = hipEventQuery( s->done );
+  if( e == hipSuccess ) return 1;
+  if( e == hipErrorNotReady ) return 0;
+  fprintf( stderr, "fd_ed25519_amd: hipEventQuery failed: %s\n", hipGetErrorString( e ) );
+  return FD_ED25519_AMD_ERR_DEVICE;
 }
 
 /* Launch a staged transaction chunk: c transactions (payload bytes in
@@ -223,7 +205,7 @@ run_chunked( fd_ed25519_amd_t * e, ulong n, schar * err, GET get ) {
   ulong i = 0; int k = 0; int rc = FD_ED25519_AMD_OK;
   while( i < n ) {
     slot_t * s = &e->slot[k];
-    if( (rc = slot_drain( s )) ) return rc;
+    if( (rc = fd_amd_slot_drain( s )) ) return rc;
     ulong c = 0, bsz = 0;
     while( i + c < n && c < e->cap ) {
       uint8_t const * msg; ulong sz; uint8_t const * sig; uint8_t const * pub;
@@ -236,10 +218,10 @@ run_chunked( fd_ed25519_amd_t * e, ulong n, schar * err, GET get ) {
       s->h_off[c] = (uint32_t)bsz; s->h_sz[c] = (uint32_t)sz;
       bsz += sz; c++;
     }
-    if( (rc = slot_launch( s, c, bsz, err + i )) ) return rc;
+    if( (rc = fd_amd_slot_launch( s, c, bsz, err + i, 0 )) ) return rc;
     i += c; k ^= 1;
   }
-  for( int j=0; j<2; j++ ) if( (rc = slot_drain( &e->slot[j] )) ) return rc;
+  for( int j=0; j<2; j++ ) if( (rc = fd_amd_slot_drain( &e->slot[j] )) ) return rc;
   return FD_ED25519_AMD_OK;
 }
 
@@ -283,7 +265,7 @@ fd_ed25519_amd_verify_txns( fd_ed25519_amd_t * e, ulong txn_cnt, uchar const * p
     if( txn_sz[t] > FD_TXN_AMD_MTU || (ulong)txn_off[t] + txn_sz[t] > payload_sz ) return FD_ED25519_AMD_ERR_INVAL;
   if( hipSetDevice( e->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
   int rc;
-  for( int k=0; k<2; k++ ) if( (rc = slot_alloc_txn( &e->slot[k], e->cap )) ) return rc;
+  for( int k=0; k<2; k++ ) if( (rc = fd_amd_slot_alloc_aux( &e->slot[k], e->cap )) ) return rc;
   /* global signature numbering (the caller-visible sig_base) */
   uint acc = 0U;
   if( sig_base ) {
@@ -293,7 +275,7 @@ fd_ed25519_amd_verify_txns( fd_ed25519_amd_t * e, ulong txn_cnt, uchar const * p
   ulong t = 0, gsig = 0; int k = 0;
   while( t < txn_cnt ) {
     slot_t * s = &e->slot[k];
-    if( (rc = slot_drain( s )) ) return rc;
+    if( (rc = fd_amd_slot_drain( s )) ) return rc;
     ulong c = 0, bsz = 0, ns = 0;
     while( t + c < txn_cnt && c < e->cap ) {
       uchar const * p = payload + txn_off[t+c];
@@ -307,7 +289,7 @@ fd_ed25519_amd_verify_txns( fd_ed25519_amd_t * e, ulong txn_cnt, uchar const * p
     if( (rc = slot_launch_txn( s, c, ns, bsz, txn_err + t, sig_err ? sig_err + gsig : NULL )) ) return rc;
     t += c; gsig += ns; k ^= 1;
   }
-  for( int j=0; j<2; j++ ) if( (rc = slot_drain( &e->slot[j] )) ) return rc;
+  for( int j=0; j<2; j++ ) if( (rc = fd_amd_slot_drain( &e->slot[j] )) ) return rc;
   return FD_ED25519_AMD_OK;
 }
 

@@ -1,0 +1,58 @@
+/* firedancer_amd/csrc/fd_ed25519_engine.h -- internal: the batch engine's
+   double-buffered slots, shared by the C-ABI (fd_ed25519_engine.cpp) and
+   the streaming verify tile (fd_verify_tile.cpp). */
+#ifndef FD_ED25519_ENGINE_H
+#define FD_ED25519_ENGINE_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/fd_ed25519_amd.h"
+
+struct slot_t {
+  /* device */
+  uint8_t  * d_pub;  uint8_t * d_sig; uint8_t * d_blob;
+  uint32_t * d_off;  uint32_t * d_sz; int8_t * d_err; void * d_ws;
+  /* pinned host staging */
+  uint8_t  * h_pub;  uint8_t * h_sig; uint8_t * h_blob;
+  uint32_t * h_off;  uint32_t * h_sz; int8_t * h_err;
+  hipStream_t stream;
+  hipEvent_t  done;
+  uint64_t * h_tag;      /* dedup tags (pinned, allocated with the txn buffers) */
+  int        want_tag;
+  /* the chunk in flight: where its verdicts go */
+  schar *    out;
+  ulong      n;
+  int        busy;
+  /* transaction front end (allocated on first use): per-transaction
+     payload offset/size, footprint, signature-slot base, verdict; per-slot
+     skip plane */
+  uint32_t * d_toff; uint32_t * d_tsz; uint32_t * d_fp; uint32_t * d_tbase; int8_t * d_terr; int8_t * d_skip;
+  uint32_t * h_toff; uint32_t * h_tsz; uint32_t * h_tbase; int8_t * h_terr;
+  /* transaction chunk in flight */
+  schar *    t_out;      /* per-transaction verdicts */
+  ulong      t_n;
+  schar *    s_out;      /* per-signature verdicts (optional) */
+  ulong      s_n;
+};
+
+struct fd_ed25519_amd {
+  int    device;
+  ulong  cap;        /* signatures per chunk */
+  ulong  blob_cap;   /* message bytes per chunk */
+  slot_t slot[2];
+};
+
+
+/* Stage-free launch of slot s: inputs already in its pinned buffers (n
+   signatures, blob_sz message bytes).  Verdicts land in s->h_err (and the
+   dedup tags in s->h_tag when want_tag) once s->done has fired; `out`
+   (may be NULL) is where slot_drain copies the verdicts. */
+int  fd_amd_slot_launch( slot_t * s, ulong n, ulong blob_sz, schar * out, int want_tag );
+/* 1 if the slot's chunk finished (or nothing is in flight), 0 if still
+   running, negative on a HIP error.  Non-blocking. */
+int  fd_amd_slot_ready( slot_t * s );
+/* Block until the slot's chunk finished; deliver verdicts to `out`. */
+int  fd_amd_slot_drain( slot_t * s );
+int  fd_amd_slot_alloc_aux( slot_t * s, ulong cap );
+
+#endif

@@ -29,6 +29,10 @@
  *                              10 limbs padded to 12: per-lane contiguous (one ADD gathers
  *                              192 contiguous bytes instead of 40 scattered dwords)
  *   st   : uint32 [3][N]       work statistics (iterations, nnz h, nnz s)
+ *   tag  : uint64 [N]          dedup tag: the first 8 bytes (little endian) of
+ *                              SHA-512(R||A||M), 0 when the s check rejected
+ *                              (app/frank/README.md:107-110: verify yields a
+ *                              secure hash for dedup at no extra cost)
  */
 
 #include "fd_ed25519_dev.h"
@@ -54,6 +58,7 @@ fd_amd_ws_layout( size_t n ) {
   L.R   = o; o = ws_al( o + 4UL*20UL*N );
   L.Ai  = o; o = ws_al( o + 4UL*384UL*N );
   L.st  = o; o = ws_al( o + 4UL*3UL*N );
+  L.tag = o; o = ws_al( o + 8UL*N );
   L.total = o;
   return L;
 }
@@ -138,6 +143,7 @@ k_prep( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
   if( i >= n ) return;
   if( skip && skip[i] ) {   /* slot of a transaction that failed to parse (fd_txn_kernels.hip) */
     ((int *)(ws + L.top))[i] = -1;
+    ((u64 *)(ws + L.tag))[i] = 0UL;
     err[i] = (i8)skip[i];
     return;
   }
@@ -169,11 +175,12 @@ k_prep( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
 
   u16 * dig = (u16 *)(ws + L.dig) + (size_t)i*256u;
   int top = -1;
-  if( code == 1 ) {
+  u64 tag = 0UL;
+  u64 st[8] = FD_AMD_SHA512_H0;
+  if( code >= 0 ) {   /* pending, or accepted by the s window (the tag is still the hash) */
     u32 sz = msg_sz[i];
     u8 const * M = blob + msg_off[i];
     u32 nblk = (64u + sz + 17u + 127u) / 128u;
-    u64 st[8] = FD_AMD_SHA512_H0;
     u64 const ra[8] = { ((u64)r0.y << 32) | r0.x, ((u64)r0.w << 32) | r0.z, ((u64)r1.y << 32) | r1.x, ((u64)r1.w << 32) | r1.z,
                         ((u64)a0.y << 32) | a0.x, ((u64)a0.w << 32) | a0.z, ((u64)a1.y << 32) | a1.x, ((u64)a1.w << 32) | a1.z };
     u64 bitlen = (u64)(64u + sz) << 3;
@@ -190,6 +197,9 @@ k_prep( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
       }
       sha512_compress( st, w );
     }
+    tag = bswap64( st[0] );
+  }
+  if( code == 1 ) {
     u32 hd[16];
     _Pragma("unroll") for( int a=0; a<8; a++ ) {
       hd[2*a]   = __builtin_bswap32( (u32)(st[a] >> 32) );
@@ -206,6 +216,7 @@ k_prep( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
     slide_reg( sw, [&]( int pos, int r ) { db8[2*pos + 1] = (u8)(i8)r; top = max( top, pos ); } );
   }
   ((int *)(ws + L.top))[i] = top;
+  ((u64 *)(ws + L.tag))[i] = tag;
   err[i] = (i8)code;
 }
 

@@ -1,0 +1,301 @@
+/* firedancer_amd/csrc/fd_verify_tile.cpp
+ *
+ * Tango-compatible streaming verify tile on the MI355X engine
+ * (include/fd_tango_amd.h).
+ *
+ * The reference verify tile (src/app/frank/load/fd_frank_verify_synth_load.c:
+ * 300-425) verifies one frag per fd_ed25519_verify call.  Here the run loop
+ * is split into a host side that never blocks on the GPU and a GPU side that
+ * verifies whole batches:
+ *
+ *   poll   -- read the next input frag metadata (seq-checked, overrun-aware)
+ *   dedup  -- HA tag cache (tag = first 8 signature bytes), FD_TCACHE_INSERT
+ *             semantics (src/tango/tcache/fd_tcache.h:372-403): a tag is a
+ *             duplicate iff it is one of the last `depth` distinct tags
+ *   stage  -- copy pub/sig/msg into the pinned staging of the free engine slot
+ *   launch -- adaptive batching: launch when the batch is full, or when the
+ *             GPU is idle (no batch in flight), or when the oldest staged
+ *             frag waited batch_wait_ns; two slots, so one batch stages
+ *             while the other verifies
+ *   publish-- when the oldest batch completes, publish its passing frags in
+ *             arrival order (fd_mcache_publish protocol) with the GPU's
+ *             SHA-512-derived dedup tag as meta.sig; failures count SV_FILT
+ */
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <thread>
+#include <vector>
+#include <atomic>
+#include <algorithm>
+
+#include "../../include/fd_ed25519_amd.h"
+#include "../../include/fd_tango_amd.h"
+#include "fd_ed25519_engine.h"
+#include "fd_ed25519_kernels.h"
+
+/* ------------------------------------------------------------------ */
+/* HA tag cache: ring of the last `depth` distinct tags + open-addressed
+   set (linear probing, backward-shift delete), map_cnt a power of 2 >=
+   2*depth+2 so probes stay short. */
+
+namespace {
+
+struct tcache_t {
+  ulong depth, map_cnt, oldest; int sh;
+  std::vector<ulong> ring, map;
+  void init( ulong d ) {
+    depth = d; oldest = 0;
+    map_cnt = 4; sh = 62; while( map_cnt < 2UL*d + 2UL ) { map_cnt <<= 1; sh--; }
+    ring.assign( d ? d : 1, 0UL ); map.assign( map_cnt, 0UL );
+  }
+  ulong slot( ulong tag ) const { return (tag * 0x9E3779B97F4A7C15UL) >> sh; }   /* Fibonacci hashing */
+  bool find( ulong tag, ulong * at ) const {
+    ulong i = slot( tag );
+    for( ;; ) {
+      ulong v = map[i];
+      if( v == tag ) { *at = i; return true; }
+      if( !v ) { *at = i; return false; }
+      i = (i + 1UL) & (map_cnt - 1UL);
+    }
+  }
+  void remove( ulong tag ) {
+    ulong i;
+    if( !tag || !find( tag, &i ) ) return;
+    /* backward-shift deletion keeps every probe chain contiguous */
+    ulong j = i;
+    for( ;; ) {
+      j = (j + 1UL) & (map_cnt - 1UL);
+      ulong v = map[j];
+      if( !v ) break;
+      ulong h = slot( v );
+      /* can v move to the hole at i?  yes iff h is not cyclically in (i, j] */
+      bool in = (i <= j) ? (h > i && h <= j) : (h > i || h <= j);
+      if( !in ) { map[i] = v; i = j; }
+    }
+    map[i] = 0UL;
+  }
+  /* FD_TCACHE_INSERT: returns 1 if tag is a duplicate, else inserts it
+     (evicting the oldest tag once the window is full) and returns 0 */
+  int insert( ulong tag ) {
+    if( !depth || !tag ) return 0;          /* FD_TCACHE_TAG_NULL is never inserted */
+    ulong at;
+    if( find( tag, &at ) ) return 1;
+    map[at] = tag;
+    ulong old = ring[oldest];
+    ring[oldest] = tag;
+    if( ++oldest >= depth ) oldest = 0;
+    remove( old );
+    return 0;
+  }
+};
+
+struct pending_t {            /* one staged / in-flight frag */
+  uint   chunk;
+  ushort sz, ctl;
+  uint   tsorig;
+};
+
+inline ulong now_ns( void ) {
+  struct timespec ts; clock_gettime( CLOCK_MONOTONIC, &ts );
+  return (ulong)ts.tv_sec * 1000000000UL + (ulong)ts.tv_nsec;
+}
+
+} /* namespace */
+
+struct fd_verify_amd_tile {
+  fd_ed25519_amd_t * eng;
+  ulong              batch_max;
+  ulong              wait_ns;
+  tcache_t           tc;
+  std::vector<pending_t> meta[2];
+};
+
+extern "C" uint
+fd_verify_amd_tickcount( void ) {
+  return (uint)now_ns();
+}
+
+extern "C" fd_verify_amd_tile_t *
+fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong tcache_depth ) {
+  if( !batch_max ) return NULL;
+  fd_ed25519_amd_t * eng = fd_ed25519_amd_new( device, batch_max, batch_max * FD_ED25519_AMD_MSG_MAX );
+  if( !eng ) return NULL;
+  for( int k=0; k<2; k++ ) if( fd_amd_slot_alloc_aux( &eng->slot[k], batch_max ) ) { fd_ed25519_amd_delete( eng ); return NULL; }
+  fd_verify_amd_tile_t * t = new fd_verify_amd_tile_t();
+  t->eng = eng; t->batch_max = batch_max; t->wait_ns = batch_wait_ns;
+  t->tc.init( tcache_depth );
+  for( int k=0; k<2; k++ ) t->meta[k].resize( batch_max );
+  return t;
+}
+
+extern "C" void
+fd_verify_amd_tile_delete( fd_verify_amd_tile_t * t ) {
+  if( !t ) return;
+  fd_ed25519_amd_delete( t->eng );
+  delete t;
+}
+
+extern "C" int
+fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ulong in_depth,
+                        void const * in_chunk0, ulong in_seq0, fd_frag_meta_t * out_mcache, ulong out_depth,
+                        ulong out_seq0, ulong const * out_fseq, ulong frag_cnt, int const * stop,
+                        fd_verify_amd_diag_t * diag, uint * lat, ulong lat_max ) {
+  if( !t || !in_mcache || !in_depth || (in_depth & (in_depth-1UL)) || !out_mcache || !out_depth ||
+      (out_depth & (out_depth-1UL)) || !diag || (!frag_cnt && !stop) ) return FD_ED25519_AMD_ERR_INVAL;
+  fd_ed25519_amd_t * e = t->eng;
+  if( hipSetDevice( e->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+
+  ulong in_seq = in_seq0, out_seq = out_seq0, lat_n = 0;
+  int   stage = 0;                 /* slot being filled */
+  ulong staged = 0, blob_at = 0, stage_t0 = 0;
+  int   fifo[2], nfly = 0;         /* in-flight slots, oldest first */
+  int   rc;
+
+  auto publish = [&]( int k ) -> int {
+    slot_t * s = &e->slot[k];
+    if( (rc = fd_amd_slot_drain( s )) ) return rc;
+    for( ulong i=0; i<s->n; i++ ) {
+      pending_t const & m = t->meta[k][i];
+      if( s->h_err[i] ) { diag->sv_filt_cnt++; diag->sv_filt_sz += m.sz; continue; }
+      if( out_fseq && out_seq - __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) >= out_depth ) {
+        diag->backp_cnt++;         /* credit check against the slowest consumer */
+        while( out_seq - __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) >= out_depth ) { /* spin */ }
+      }
+      uint tspub = fd_verify_amd_tickcount();
+      fd_mcache_publish( out_mcache, out_depth, out_seq, s->h_tag[i], m.chunk, m.sz, m.ctl, m.tsorig, tspub );
+      if( lat && lat_n < lat_max ) lat[lat_n++] = tspub - m.tsorig;
+      out_seq++; diag->out_cnt++; diag->out_sz += m.sz;
+    }
+    return FD_ED25519_AMD_OK;
+  };
+
+  for( ;; ) {
+    /* 1. retire the oldest batch if it is done (publication stays in
+          arrival order: batches retire in launch order) */
+    if( nfly ) {
+      int r = fd_amd_slot_ready( &e->slot[fifo[0]] );
+      if( r < 0 ) return r;
+      if( r ) {
+        if( (rc = publish( fifo[0] )) ) return rc;
+        fifo[0] = fifo[1]; nfly--;
+      }
+    }
+    bool done_in = frag_cnt ? (diag->in_cnt >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
+    if( done_in && !staged && !nfly ) break;
+    bool free_slot = !(nfly == 2 || (nfly == 1 && fifo[0] == stage));
+    if( !free_slot ) continue;
+
+    /* 2. stage input frags into the free slot */
+    slot_t * s = &e->slot[stage];
+    while( !done_in && staged < t->batch_max ) {
+      if( frag_cnt && diag->in_cnt >= frag_cnt ) break;
+      fd_frag_meta_t const * m = in_mcache + (in_seq & (in_depth-1UL));
+      ulong seq_found = __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE );
+      long  d = (long)(seq_found - in_seq);
+      if( d < 0 ) break;                                                 /* not yet published */
+      if( d > 0 ) { diag->ovrn_cnt += (ulong)d; in_seq = seq_found; continue; }   /* overrun: resync */
+      ulong chunk = m->chunk, sz = m->sz, ctl = m->ctl, tsorig = m->tsorig;
+      __atomic_thread_fence( __ATOMIC_ACQUIRE );
+      if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != in_seq ) { diag->ovrn_cnt++; in_seq++; continue; }
+      uchar const * p = (uchar const *)fd_chunk_to_laddr_const( in_chunk0, chunk );
+      in_seq++;
+      __atomic_store_n( &diag->in_cnt, diag->in_cnt + 1UL, __ATOMIC_RELEASE );
+      if( sz < 96UL || sz - 96UL > FD_ED25519_AMD_MSG_MAX ) { diag->bad_frag_cnt++; continue; }
+      ulong ha_tag; memcpy( &ha_tag, p + 32, 8 );                        /* first 8 signature bytes */
+      if( t->tc.insert( ha_tag ) ) { diag->ha_filt_cnt++; diag->ha_filt_sz += sz; continue; }
+      ulong msz = sz - 96UL;                                             /* blob_cap = batch_max*MSG_MAX: fits */
+      memcpy( s->h_pub + 32UL*staged, p,      32 );
+      memcpy( s->h_sig + 64UL*staged, p + 32, 64 );
+      memcpy( s->h_blob + blob_at,    p + 96, msz );
+      s->h_off[staged] = (uint32_t)blob_at; s->h_sz[staged] = (uint32_t)msz;
+      t->meta[stage][staged] = pending_t{ (uint)chunk, (ushort)sz, (ushort)ctl, (uint)tsorig };
+      if( !staged ) stage_t0 = now_ns();
+      blob_at += msz; staged++;
+    }
+    done_in = frag_cnt ? (diag->in_cnt >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
+
+    /* 3. adaptive launch: full batch, idle GPU, end of input, or the
+          oldest staged frag waited long enough */
+    if( staged && ( staged == t->batch_max || !nfly || done_in ||
+                    (t->wait_ns && now_ns() - stage_t0 >= t->wait_ns) ) ) {
+      if( (rc = fd_amd_slot_launch( s, staged, blob_at, NULL, 1 )) ) return rc;
+      diag->batch_cnt++; diag->batch_sig_cnt += staged;
+      fifo[nfly++] = stage;
+      stage ^= 1; staged = 0; blob_at = 0;
+    }
+  }
+  return FD_ED25519_AMD_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* streaming benchmark: producer -> tile -> consumer                    */
+
+extern "C" int
+fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, ulong pool_n, uchar const * pub,
+                            uchar const * sig, uint const * msg_off, uint const * msg_sz, uchar const * blob,
+                            ulong frag_cnt, double * out ) {
+  if( !pool_n || !frag_cnt || !out ) return FD_ED25519_AMD_ERR_INVAL;
+  ulong depth = 1UL; while( depth < 4UL*batch_max + 1024UL ) depth <<= 1;
+  ulong mtu = 96UL + FD_ED25519_AMD_MSG_MAX;
+  ulong chunk_mtu = ((mtu + 2UL*FD_CHUNK_SZ - 1UL) >> (1 + FD_CHUNK_LG_SZ)) << 1;
+  ulong data_chunks = chunk_mtu * (depth + 2UL);
+  std::vector<fd_frag_meta_t> in_mc( depth ), out_mc( depth );
+  for( ulong i=0; i<depth; i++ ) { in_mc[i].seq = i - depth; out_mc[i].seq = i - depth; }   /* "never published" */
+  uchar * dcache = (uchar *)aligned_alloc( 64, data_chunks * FD_CHUNK_SZ );
+  if( !dcache ) return FD_ED25519_AMD_ERR_INVAL;
+  ulong wmark = data_chunks - chunk_mtu;
+
+  fd_verify_amd_tile_t * tile = fd_verify_amd_tile_new( device, batch_max, batch_wait_ns, 0UL );
+  if( !tile ) { free( dcache ); return FD_ED25519_AMD_ERR_DEVICE; }
+
+  std::atomic<ulong> in_fseq( 0UL ), out_fseq( 0UL );   /* consumer progress (credits) */
+  std::vector<uint> lat( frag_cnt );
+  fd_verify_amd_diag_t diag; memset( &diag, 0, sizeof diag );
+  int tile_rc = 0;
+  ulong t0 = now_ns();
+
+  std::thread prod( [&]() {
+    ulong chunk = 0;
+    for( ulong seq=0; seq<frag_cnt; seq++ ) {
+      /* credit: do not lap the tile's consumption of the input mcache */
+      while( seq - __atomic_load_n( &diag.in_cnt, __ATOMIC_ACQUIRE ) >= depth - 16UL ) { /* spin */ }
+      ulong k = seq % pool_n, msz = msg_sz[k], sz = 96UL + msz;
+      uchar * p = dcache + chunk * FD_CHUNK_SZ;
+      memcpy( p, pub + 32UL*k, 32 ); memcpy( p + 32, sig + 64UL*k, 64 ); memcpy( p + 96, blob + msg_off[k], msz );
+      fd_mcache_publish( in_mc.data(), depth, seq, 0UL, chunk, sz, 3UL, fd_verify_amd_tickcount(), 0UL );
+      chunk = fd_dcache_compact_next( chunk, sz, 0UL, wmark );
+    }
+  } );
+  std::thread cons( [&]() {
+    ulong seq = 0;
+    for( ;; ) {
+      if( __atomic_load_n( &tile_rc, __ATOMIC_ACQUIRE ) == 1 ) {   /* tile finished: drain what is there */
+        fd_frag_meta_t const * m = &out_mc[ seq & (depth-1UL) ];
+        if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != seq ) break;
+      }
+      fd_frag_meta_t const * m = &out_mc[ seq & (depth-1UL) ];
+      if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) == seq ) { seq++; out_fseq.store( seq, std::memory_order_release ); }
+    }
+  } );
+  ulong const * ofs = (ulong const *)&out_fseq;
+  int rc = fd_verify_amd_tile_run( tile, in_mc.data(), depth, dcache, 0UL, out_mc.data(), depth, 0UL, ofs,
+                                   frag_cnt, NULL, &diag, lat.data(), frag_cnt );
+  ulong t1 = now_ns();
+  __atomic_store_n( &tile_rc, 1, __ATOMIC_RELEASE );
+  prod.join(); cons.join();
+  fd_verify_amd_tile_delete( tile );
+  free( dcache );
+  if( rc ) return rc;
+  ulong n = std::min( (ulong)diag.out_cnt, frag_cnt );
+  std::sort( lat.begin(), lat.begin() + (long)n );
+  auto pct = [&]( double q ) -> double { return n ? (double)lat[ std::min( n-1UL, (ulong)(q * (double)n) ) ] : 0.0; };
+  out[0] = (double)diag.in_cnt / ((double)(t1 - t0) * 1e-9);
+  out[1] = pct( 0.50 ); out[2] = pct( 0.99 ); out[3] = pct( 0.999 );
+  out[4] = diag.batch_cnt ? (double)diag.batch_sig_cnt / (double)diag.batch_cnt : 0.0;
+  out[5] = (double)diag.out_cnt; out[6] = (double)diag.sv_filt_cnt;
+  (void)in_fseq;
+  return FD_ED25519_AMD_OK;
+}

@@ -74,6 +74,16 @@ def lib():
     L.fd_ed25519_amd_verify_txns.restype = i
     L.fd_txn_amd_parse_dev.argtypes = [ul, vp, vp, vp, vp, vp, ul, vp]
     L.fd_txn_amd_parse_dev.restype = i
+    L.fd_verify_amd_tile_new.argtypes = [i, ul, ul, ul]
+    L.fd_verify_amd_tile_new.restype = vp
+    L.fd_verify_amd_tile_delete.argtypes = [vp]
+    L.fd_verify_amd_tile_delete.restype = None
+    L.fd_verify_amd_tile_run.argtypes = [vp, vp, ul, vp, ul, vp, ul, ul, vp, ul, vp, vp, vp, ul]
+    L.fd_verify_amd_tile_run.restype = i
+    L.fd_verify_amd_tickcount.argtypes = []
+    L.fd_verify_amd_tickcount.restype = ui
+    L.fd_verify_amd_bench_stream.argtypes = [i, ul, ul, ul, vp, vp, vp, vp, vp, ul, vp]
+    L.fd_verify_amd_bench_stream.restype = i
     _lib = L
     return L
 

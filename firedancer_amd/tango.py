@@ -1,0 +1,102 @@
+"""Python mirror of the tango pieces the streaming verify tile speaks
+(include/fd_tango_amd.h; reference src/tango/fd_tango_base.h:146-203,
+src/tango/mcache/fd_mcache.h:299-322, src/tango/dcache/fd_dcache.h:211-269)
+and a handle on the tile itself (fd_verify_amd_tile_*).  The tile's run
+loop is native (firedancer_amd/csrc/fd_verify_tile.cpp); this module only
+lays out memory and calls it."""
+import ctypes
+
+import numpy as np
+
+from . import ed25519
+
+FRAG_META = np.dtype([("seq", "<u8"), ("sig", "<u8"), ("chunk", "<u4"), ("sz", "<u2"), ("ctl", "<u2"),
+                      ("tsorig", "<u4"), ("tspub", "<u4")])
+assert FRAG_META.itemsize == 32
+CHUNK_LG_SZ = 6
+CHUNK_SZ = 64
+DIAG_FIELDS = ("in_cnt", "ha_filt_cnt", "ha_filt_sz", "sv_filt_cnt", "sv_filt_sz", "out_cnt", "out_sz",
+               "ovrn_cnt", "backp_cnt", "batch_cnt", "batch_sig_cnt", "bad_frag_cnt")
+
+
+def _aligned(nbytes, align=64):
+    raw = np.zeros(nbytes + align, np.uint8)
+    off = (-raw.ctypes.data) % align
+    return raw[off:off + nbytes]
+
+
+def mcache_new(depth):
+    """An mcache ring of `depth` (power of 2) frag metadata, every line
+    marked "not yet published" for the first lap (seq = line - depth)."""
+    assert depth and not depth & (depth - 1)
+    m = _aligned(32 * depth).view(FRAG_META)
+    m["seq"] = (np.arange(depth, dtype=np.int64) - depth).astype(np.uint64)
+    return m
+
+
+def publish(mcache, seq, sig, chunk, sz, ctl, tsorig, tspub):
+    """fd_mcache_publish (fd_mcache.h:299-322) from Python (single-threaded use)."""
+    line = mcache[seq & (mcache.size - 1)]
+    line["seq"] = (seq - 1) & 0xFFFFFFFFFFFFFFFF
+    line["sig"], line["chunk"], line["sz"], line["ctl"] = sig, chunk, sz, ctl
+    line["tsorig"], line["tspub"] = tsorig, tspub
+    line["seq"] = seq
+
+
+def dcache_compact_next(chunk, sz, chunk0, wmark):
+    """fd_dcache_compact_next (fd_dcache.h:263-269)."""
+    chunk += ((sz + (2 * CHUNK_SZ - 1)) >> (1 + CHUNK_LG_SZ)) << 1
+    return chunk0 if chunk > wmark else chunk
+
+
+def tickcount():
+    return int(ed25519.lib().fd_verify_amd_tickcount())
+
+
+class VerifyTile:
+    """fd_verify_amd_tile_t: adaptive-batching GPU verify tile."""
+
+    def __init__(self, device=0, batch_max=4096, batch_wait_ns=0, tcache_depth=1 << 16):
+        self._h = ed25519.lib().fd_verify_amd_tile_new(int(device), int(batch_max), int(batch_wait_ns),
+                                                      int(tcache_depth))
+        if not self._h:
+            raise ed25519.EngineError("fd_verify_amd_tile_new failed (no HIP device?)")
+
+    def close(self):
+        if self._h:
+            ed25519.lib().fd_verify_amd_tile_delete(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run(self, in_mcache, in_chunk0, in_seq0, out_mcache, out_seq0, frag_cnt, lat_max=0):
+        """Consume frag_cnt input frags; returns (diag dict, latency samples)."""
+        diag = (ctypes.c_ulong * len(DIAG_FIELDS))()
+        lat = np.zeros(max(lat_max, 1), np.uint32)
+        vp = ctypes.c_void_p
+        rc = ed25519.lib().fd_verify_amd_tile_run(
+            self._h, vp(in_mcache.ctypes.data), in_mcache.size, vp(in_chunk0.ctypes.data), int(in_seq0),
+            vp(out_mcache.ctypes.data), out_mcache.size, int(out_seq0), None, int(frag_cnt), None,
+            ctypes.byref(diag), vp(lat.ctypes.data) if lat_max else None, int(lat_max))
+        if rc:
+            raise ed25519.EngineError("fd_verify_amd_tile_run rc=%d" % rc)
+        d = dict(zip(DIAG_FIELDS, list(diag)))
+        return d, lat[:min(lat_max, d["out_cnt"])]
+
+
+def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, blob, frag_cnt):
+    """fd_verify_amd_bench_stream: producer -> tile -> consumer; returns
+    dict(frags_per_s, p50_ns, p99_ns, p999_ns, mean_batch, published, sv_filt)."""
+    out = (ctypes.c_double * 7)()
+    p = [np.ascontiguousarray(a) for a in (pub, sig, msg_off, msg_sz, blob)]
+    vp = ctypes.c_void_p
+    rc = ed25519.lib().fd_verify_amd_bench_stream(int(device), int(batch_max), int(batch_wait_ns), p[0].shape[0],
+                                                  *[vp(a.ctypes.data) for a in p], int(frag_cnt), out)
+    if rc:
+        raise ed25519.EngineError("fd_verify_amd_bench_stream rc=%d" % rc)
+    keys = ("frags_per_s", "p50_ns", "p99_ns", "p999_ns", "mean_batch", "published", "sv_filt")
+    return dict(zip(keys, list(out)))

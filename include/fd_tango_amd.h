@@ -1,0 +1,174 @@
+#ifndef HEADER_fd_tango_amd_h
+#define HEADER_fd_tango_amd_h
+
+/* Tango-compatible streaming verify tile on the MI355X engine (SURVEY.md
+ * s8 f2, config 5).
+ *
+ * Part 1 reproduces the tango ABI the tile speaks: the 32-byte fragment
+ * metadata (src/tango/fd_tango_base.h:146-203), 64-byte chunk addressing
+ * (:123-126, :239-263), the mcache publish protocol
+ * (src/tango/mcache/fd_mcache.h:299-322: seq-1 first, fields, then seq)
+ * and the compact dcache chunk advance (src/tango/dcache/fd_dcache.h:
+ * 211-269).  When the reference's own tango headers were included first
+ * their definitions are used.
+ *
+ * Part 2 is the tile: it consumes frags public_key(32) | signature(64) |
+ * message from an input mcache/dcache (the framing of the reference verify
+ * tile, src/app/frank/load/fd_frank_verify_synth_load.c:340-347), drops HA
+ * duplicates with a tag cache before verification (:351-370; tag = the
+ * first 8 signature bytes), verifies in adaptive GPU batches, and publishes
+ * the passing frags in arrival order to an output mcache (:404-411) with
+ * the metadata `sig` field set to the dedup tag produced by the verify
+ * itself (the first 8 bytes of SHA-512(R||A||M), app/frank/README.md:
+ * 107-110; consumed by the dedup tile, disco/dedup/fd_dedup.h:247).
+ * Drops are counted like the reference's cnc diagnostics
+ * (app/frank/fd_frank.h:23-28: HA_FILT_{CNT,SZ}, SV_FILT_{CNT,SZ}).
+ */
+
+#include "fd_ed25519_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ===== Part 1: tango ABI ===== */
+
+#ifndef HEADER_fd_src_tango_fd_tango_base_h
+
+typedef unsigned short ushort;
+
+#define FD_CHUNK_LG_SZ      (6)
+#define FD_CHUNK_SZ         (64UL)
+#define FD_FRAG_META_ALIGN  (32UL)
+
+struct __attribute__((aligned(32))) fd_frag_meta {
+  ulong  seq;     /* frag sequence number, written last by the publisher */
+  ulong  sig;     /* application signature: here the dedup tag */
+  uint   chunk;   /* compressed location of the frag in the data region */
+  ushort sz;      /* frag size in bytes */
+  ushort ctl;     /* SOM/EOM/ERR + origin */
+  uint   tsorig;  /* compressed timestamps */
+  uint   tspub;
+};
+typedef struct fd_frag_meta fd_frag_meta_t;
+
+static inline void *
+fd_chunk_to_laddr( void * chunk0, ulong chunk ) { return (void *)((ulong)chunk0 + (chunk << FD_CHUNK_LG_SZ)); }
+
+static inline void const *
+fd_chunk_to_laddr_const( void const * chunk0, ulong chunk ) { return (void const *)((ulong)chunk0 + (chunk << FD_CHUNK_LG_SZ)); }
+
+#endif /* HEADER_fd_src_tango_fd_tango_base_h */
+
+#ifndef HEADER_fd_src_tango_mcache_fd_mcache_h
+/* fd_mcache.h:299-322 semantics: a consumer polling line seq&(depth-1)
+   never sees a torn record it would accept as frag seq. */
+static inline void
+fd_mcache_publish( fd_frag_meta_t * mcache, ulong depth, ulong seq, ulong sig, ulong chunk, ulong sz, ulong ctl,
+                   ulong tsorig, ulong tspub ) {
+  fd_frag_meta_t * m = mcache + (seq & (depth-1UL));
+  __atomic_store_n( &m->seq, seq - 1UL, __ATOMIC_RELEASE );
+  __atomic_thread_fence( __ATOMIC_RELEASE );
+  m->sig = sig; m->chunk = (uint)chunk; m->sz = (ushort)sz; m->ctl = (ushort)ctl;
+  m->tsorig = (uint)tsorig; m->tspub = (uint)tspub;
+  __atomic_store_n( &m->seq, seq, __ATOMIC_RELEASE );
+}
+#endif
+
+#ifndef HEADER_fd_src_tango_dcache_fd_dcache_h
+/* fd_dcache.h:263-269: advance to the next chunk pair, wrap at wmark */
+static inline ulong
+fd_dcache_compact_next( ulong chunk, ulong sz, ulong chunk0, ulong wmark ) {
+  chunk += ((sz + (2UL*FD_CHUNK_SZ - 1UL)) >> (1 + FD_CHUNK_LG_SZ)) << 1;
+  return chunk > wmark ? chunk0 : chunk;
+}
+#endif
+
+/* ===== Part 2: the verify tile ===== */
+
+/* diagnostics (fd_frank.h:23-28 names, plus engine-side counts) */
+typedef struct {
+  ulong in_cnt;        /* input frags consumed */
+  ulong ha_filt_cnt;   /* dropped as HA duplicates before verify */
+  ulong ha_filt_sz;
+  ulong sv_filt_cnt;   /* dropped by signature verification */
+  ulong sv_filt_sz;
+  ulong out_cnt;       /* frags published */
+  ulong out_sz;
+  ulong ovrn_cnt;      /* input frags lost to producer overrun */
+  ulong backp_cnt;     /* times the output was backpressured */
+  ulong batch_cnt;     /* GPU batches launched */
+  ulong batch_sig_cnt; /* signatures in those batches */
+  ulong bad_frag_cnt;  /* frags too short / too long to carry a signature */
+} fd_verify_amd_diag_t;
+
+typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
+
+/* A tile bound to HIP device `device`.  batch_max: largest GPU batch;
+   batch_wait_ns: how long a non-empty partial batch may wait for more
+   frags while the GPU is busy (0 = only the adaptive rule: launch whenever
+   the GPU is idle or the batch is full); tcache_depth: HA dedup window
+   (tags remembered, 0 disables).  NULL on failure. */
+fd_verify_amd_tile_t *
+fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong tcache_depth );
+
+void
+fd_verify_amd_tile_delete( fd_verify_amd_tile_t * tile );
+
+/* Run the tile until `frag_cnt` input frags were consumed (0: until
+   *stop != 0) and every accepted frag is published.  Input: in_mcache
+   (depth in_depth, power of 2), in_chunk0 = local address of chunk 0 of
+   the data region (fd_chunk_to_laddr), first sequence number in_seq0.
+   Output: out_mcache (depth out_depth), first sequence out_seq0; out_fseq
+   (NULL = no flow control) is the slowest consumer's next expected
+   sequence number.  Latency samples (tspub - tsorig, in the caller's
+   timestamp units) of up to lat_max published frags go to lat (NULL to
+   skip).  Returns FD_ED25519_AMD_OK or a negative FD_ED25519_AMD_ERR_*. */
+int
+fd_verify_amd_tile_run( fd_verify_amd_tile_t *  tile,
+                        fd_frag_meta_t const *  in_mcache,
+                        ulong                   in_depth,
+                        void const *            in_chunk0,
+                        ulong                   in_seq0,
+                        fd_frag_meta_t *        out_mcache,
+                        ulong                   out_depth,
+                        ulong                   out_seq0,
+                        ulong const *           out_fseq,
+                        ulong                   frag_cnt,
+                        int const *             stop,
+                        fd_verify_amd_diag_t *  diag,
+                        uint *                  lat,
+                        ulong                   lat_max );
+
+/* The tile's timestamp clock (tsorig/tspub units): nanoseconds of
+   CLOCK_MONOTONIC, low 32 bits (fd_frag_meta_ts_comp-style compression). */
+uint
+fd_verify_amd_tickcount( void );
+
+/* Streaming benchmark (config 5): a producer thread publishes frags
+   public_key | signature | message cyclically from the given pool (SoA
+   layout of fd_ed25519_amd_verify_soa) into a private mcache/dcache at
+   the highest rate the tile sustains (credit-based flow control), the tile
+   runs on `device`, and a consumer drains the output.  Runs until
+   frag_cnt frags were published.  out[0] = frags/s through the tile,
+   out[1..3] = p50 / p99 / p999 latency in ns (producer publish -> tile
+   publish), out[4] = mean GPU batch size, out[5] = frags published,
+   out[6] = frags dropped by verification.  Returns 0 or an error code. */
+int
+fd_verify_amd_bench_stream( int           device,
+                            ulong         batch_max,
+                            ulong         batch_wait_ns,
+                            ulong         pool_n,
+                            uchar const * pub,
+                            uchar const * sig,
+                            uint const *  msg_off,
+                            uint const *  msg_sz,
+                            uchar const * blob,
+                            ulong         frag_cnt,
+                            double *      out );
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HEADER_fd_tango_amd_h */
