@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--no-stream", action="store_true", help="skip the streaming-tile sweep (config 5)")
+    ap.add_argument("--stream-frags", type=int, default=1 << 18, help="frags per streaming-tile run")
     return ap.parse_args()
 
 
@@ -212,6 +214,26 @@ def main():
         lat = np.array(lat[3:])
         out["latency_ms_4096"] = {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
                                   "path": "host SoA -> pinned staging -> H2D -> 3 kernels -> D2H"}
+    if world == 1 and not args.no_stream:
+        # config 5: tango mcache/dcache feed -> verify tile -> consumer, per batch cap
+        from firedancer_amd import tango
+        m = min(n, 1 << 16)
+        rows = []
+        for bmax in (256, 1024, 4096, 16384):
+            sat = tango.bench_stream(local, bmax, 0, pub[:m], sig[:m], off[:m], sz[:m], blob, args.stream_frags)
+            row = {"batch_max": bmax, "saturated_frags_per_s": sat["frags_per_s"],
+                   "saturated_mean_batch": sat["mean_batch"]}
+            for load in (0.5, 0.8):
+                rate = load * sat["frags_per_s"]
+                nf = int(min(args.stream_frags, max(20000, rate * 1.0)))
+                r = tango.bench_stream(local, bmax, 0, pub[:m], sig[:m], off[:m], sz[:m], blob, nf, rate=rate)
+                row["at_%d%%" % int(load * 100)] = {"offered_frags_per_s": rate, "frags_per_s": r["frags_per_s"],
+                                                     "p50_us": r["p50_ns"] / 1e3, "p99_us": r["p99_ns"] / 1e3,
+                                                     "mean_batch": r["mean_batch"]}
+            rows.append(row)
+        out["stream_tile"] = {"path": "producer -> in mcache/dcache -> verify tile (adaptive GPU batches, 4 in "
+                                      "flight) -> out mcache -> consumer; latency = scheduled send to tile publish",
+                              "frags_per_run": args.stream_frags, "rows": rows}
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(pub, sig, off, sz, blob, args.cpu_sample, args.cpu_threads, err,
                                            args.cpu_seconds)

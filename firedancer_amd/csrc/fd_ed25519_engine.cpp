@@ -83,6 +83,12 @@ slot_alloc( slot_t * s, ulong cap, ulong blob_cap ) {
 
 extern "C" fd_ed25519_amd_t *
 fd_ed25519_amd_new( int device, ulong batch_max, ulong blob_max ) {
+  return fd_amd_engine_new( device, batch_max, blob_max, 2 );
+}
+
+fd_ed25519_amd_t *
+fd_amd_engine_new( int device, ulong batch_max, ulong blob_max, int nslot ) {
+  if( nslot < 2 || nslot > FD_AMD_SLOT_MAX ) return NULL;
   if( !batch_max ) batch_max = 1;
   if( batch_max > (1UL<<26) ) return NULL;
   if( blob_max < FD_ED25519_AMD_MSG_MAX ) blob_max = FD_ED25519_AMD_MSG_MAX;
@@ -95,8 +101,8 @@ fd_ed25519_amd_new( int device, ulong batch_max, ulong blob_max ) {
   if( hipSetDevice( device ) != hipSuccess ) return NULL;
   fd_ed25519_amd_t * e = (fd_ed25519_amd_t *)calloc( 1, sizeof(fd_ed25519_amd_t) );
   if( !e ) return NULL;
-  e->device = device; e->cap = batch_max; e->blob_cap = blob_max;
-  for( int k=0; k<2; k++ ) {
+  e->device = device; e->cap = batch_max; e->blob_cap = blob_max; e->nslot = nslot;
+  for( int k=0; k<nslot; k++ ) {
     if( slot_alloc( &e->slot[k], batch_max, blob_max ) ) { fd_ed25519_amd_delete( e ); return NULL; }
   }
   return e;
@@ -106,7 +112,7 @@ extern "C" void
 fd_ed25519_amd_delete( fd_ed25519_amd_t * e ) {
   if( !e ) return;
   (void)hipSetDevice( e->device );
-  for( int k=0; k<2; k++ ) { if( e->slot[k].stream ) (void)hipStreamSynchronize( e->slot[k].stream ); slot_free( &e->slot[k] ); }
+  for( int k=0; k<FD_AMD_SLOT_MAX; k++ ) { if( e->slot[k].stream ) (void)hipStreamSynchronize( e->slot[k].stream ); slot_free( &e->slot[k] ); }
   free( e );
 }
 

@@ -35,12 +35,18 @@ struct slot_t {
   ulong      s_n;
 };
 
+#define FD_AMD_SLOT_MAX (6)
+
 struct fd_ed25519_amd {
   int    device;
   ulong  cap;        /* signatures per chunk */
   ulong  blob_cap;   /* message bytes per chunk */
-  slot_t slot[2];
+  int    nslot;      /* 2 for the batch API (double buffering); the tile uses more */
+  slot_t slot[FD_AMD_SLOT_MAX];
 };
+
+/* An engine with `nslot` in-flight slots (2..FD_AMD_SLOT_MAX). */
+fd_ed25519_amd_t * fd_amd_engine_new( int device, ulong batch_max, ulong blob_max, int nslot );
 
 
 /* Stage-free launch of slot s: inputs already in its pinned buffers (n

@@ -598,7 +598,251 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
 }
 
 /* ------------------------------------------------------------------ */
+/* k_dsm4: the same op stream with FOUR lanes per signature (16 signatures
+ * per wave), for latency: a small batch leaves most SIMDs idle and the
+ * verify time is one lane's sequential op stream.  Every step of the op
+ * stream is 4 independent field muls (p1p1->p3) followed by 4 independent
+ * muls (the op body); lane q of a quad does the q-th mul of each group and
+ * the quad exchanges results with DPP quad_perm broadcasts (the AVX build's
+ * 4-lane split of fd_ed25519_ge.c:408-527, mapped to a lane quad instead of
+ * a ymm register).  The linear mixes are recomputed by all four lanes, so
+ * every lane holds the full point between the two mul groups.  Same field
+ * ops in the same order as k_dsm: identical limbs.
+ *
+ *   p1p1->p3 : q0 Z*T -> u.Z   q1 Z*Y -> u.Y   q2 X*T -> u.X   q3 X*Y -> u.T
+ *   DBL body : q0 (X+Y)^2      q1 Y^2          q2 X^2          q3 Z*2Z
+ *   ADD body : q0 (Y+X)*qP     q1 (Y-X)*qM     q2 Z*qZ         q3 T*qT
+ *   FIN      : q0 Z*RX         q1 Z*RY  (then the limb compare, quad AND)
+ * Each lane loads only the table row its mul needs (qP/qM/qZ/qT).
+ */
+template<int K>
+__device__ __forceinline__ i32 qb( i32 v ) {   /* broadcast lane K of each quad: DPP quad_perm(K,K,K,K) */
+  return __builtin_amdgcn_mov_dpp( v, K * 0x55, 0xf, 0xf, false );
+}
+__device__ __forceinline__ void qgather( fe const & mine, fe & f0, fe & f1, fe & f2, fe & f3 ) {
+  _Pragma("unroll") for( int k=0; k<10; k++ ) {
+    f0.v[k] = qb<0>( mine.v[k] ); f1.v[k] = qb<1>( mine.v[k] );
+    f2.v[k] = qb<2>( mine.v[k] ); f3.v[k] = qb<3>( mine.v[k] );
+  }
+}
+/* per-lane choice among four values by quad position (lane masks m1,m2:
+   bit 0 / bit 1 of q) */
+__device__ __forceinline__ i32 q4( u64 m1, u64 m2, i32 a0, i32 a1, i32 a2, i32 a3 ) {
+  return vsel( m2, vsel( m1, a3, a2 ), vsel( m1, a1, a0 ) );
+}
+
+/* p1p1 -> p3 on a quad: every lane ends with the full u */
+__device__ __forceinline__ void
+quad_p3( p3 & u, p1p1 const & t, u64 m1, u64 m2 ) {
+  fe a, b;
+  _Pragma("unroll") for( int k=0; k<10; k++ ) {
+    a.v[k] = vsel( m2, t.X.v[k], t.Z.v[k] );                               /* Z Z X X */
+    b.v[k] = vsel( m1, t.Y.v[k], t.T.v[k] );                               /* T Y T Y */
+  }
+  fe pm = fe_mul( a, b );
+  qgather( pm, u.Z, u.Y, u.X, u.T );
+}
+
+/* op body + mix on a quad.  qrow: this lane's table row (ADD); isD/neg per
+   lane (uniform within the quad). */
+__device__ __forceinline__ void
+quad_body( p1p1 & t, p3 const & u, fe const & qrow, u64 mD, u64 mN, u64 m1, u64 m2 ) {
+  fe a, b;
+  _Pragma("unroll") for( int k=0; k<10; k++ ) {
+    i32 X = u.X.v[k], Y = u.Y.v[k], Z = u.Z.v[k], T = u.T.v[k];
+    i32 xy = X + Y;
+    i32 aD = q4( m1, m2, xy, Y, X, Z );
+    i32 bD = q4( m1, m2, xy, Y, X, Z + Z );
+    i32 aA = q4( m1, m2, xy, Y - X, Z, T );
+    a.v[k] = vsel( mD, aD, aA );
+    b.v[k] = vsel( mD, bD, qrow.v[k] );
+  }
+  fe m = fe_mul( a, b );
+  fe M0, M1, M2, M3;
+  qgather( m, M0, M1, M2, M3 );
+  _Pragma("unroll") for( int k=0; k<10; k++ ) {
+    i32 A0 = M0.v[k], A1 = M1.v[k], A2 = M2.v[k], A3 = M3.v[k];
+    i32 z2 = A2 + A2;
+    i32 dX = A0 - A1 - A2, dY = A1 + A2, dZ = A1 - A2, dT = A3 - A1 + A2;
+    i32 aX = A0 - A1,      aY = A0 + A1;
+    i32 zp = z2 + A3, zm = z2 - A3;
+    i32 aZ = vsel( mN, zm, zp ), aT = vsel( mN, zp, zm );
+    t.X.v[k] = vsel( mD, dX, aX );
+    t.Y.v[k] = vsel( mD, dY, aY );
+    t.Z.v[k] = vsel( mD, dZ, aZ );
+    t.T.v[k] = vsel( mD, dT, aT );
+  }
+}
+
+/* p3 -> this lane's cached row (q0 Z*1, q1 Y1-X1, q2 Y1+X1, q3 T*2d) */
+__device__ __forceinline__ fe
+quad_cached_row( p3 const & u, u64 m1, u64 m2 ) {
+  fe const D2 = {FD_AMD_FE_D2};
+  fe Z1 = fe_mul_one( u.Z ), Y1 = fe_mul_one( u.Y ), X1 = fe_mul_one( u.X );
+  fe T2 = fe_mul( u.T, D2 );
+  fe r;
+  _Pragma("unroll") for( int k=0; k<10; k++ ) r.v[k] = q4( m1, m2, Z1.v[k], Y1.v[k] - X1.v[k], Y1.v[k] + X1.v[k], T2.v[k] );
+  return r;
+}
+
+__global__ void __launch_bounds__(64)
+k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats ) {
+  __shared__ i32 bi[8][40];
+  for( int k=threadIdx.x; k<8*40; k+=64 ) {
+    int e = k / 40, c = (k % 40) / 10, l = k % 10;
+    i32 v;
+    if( c == 0 ) v = (l == 0);
+    else if( c == 1 ) v = BI_TABLE[e][1][l];
+    else if( c == 2 ) v = BI_TABLE[e][0][l];
+    else v = BI_TABLE[e][2][l];
+    bi[e][c*10 + l] = v;
+  }
+  __syncthreads();
+
+  u32 gt = blockIdx.x * 64u + threadIdx.x;
+  u32 i = gt >> 2;
+  int qd = (int)(threadIdx.x & 3u);
+  bool act = (i < n) && (err[i] == 1);
+  size_t N = L.N;
+  u32 ii = (i < n) ? i : 0u;
+  i32 * Ail = (i32 *)(ws + L.Ai) + (size_t)ii*384u;
+  u64 const m1 = __builtin_amdgcn_ballot_w64( qd & 1 ), m2 = __builtin_amdgcn_ballot_w64( qd & 2 );
+
+  /* -A and its odd multiples (cached rows; lane q writes row q) */
+  {
+    p3 A;
+    i32 const * Aw = (i32 const *)(ws + L.A);
+    _Pragma("unroll") for( int k=0; k<10; k++ ) {
+      A.X.v[k] = act ? Aw[(size_t)(k   )*N + ii] : 0;
+      A.Y.v[k] = act ? Aw[(size_t)(10+k)*N + ii] : (k==0);
+      A.T.v[k] = act ? Aw[(size_t)(20+k)*N + ii] : 0;
+      A.Z.v[k] = (k==0);
+    }
+    fe row = quad_cached_row( A, m1, m2 );
+#   define AI_ROW4( e ) do {                                                        \
+      int4 * d_ = (int4 *)(Ail + (e)*48 + qd*12);                                   \
+      d_[0] = make_int4( row.v[0], row.v[1], row.v[2], row.v[3] );                 \
+      d_[1] = make_int4( row.v[4], row.v[5], row.v[6], row.v[7] );                 \
+      d_[2] = make_int4( row.v[8], row.v[9], 0, 0 );                               \
+    } while(0)
+    if( act ) AI_ROW4( 0 );
+    u64 const all = ~0UL, none = 0UL;
+    p1p1 t; fe z0 = fe_zero();
+    quad_body( t, A, z0, all, none, m1, m2 );            /* DBL(A) */
+    p3 A2; quad_p3( A2, t, m1, m2 );
+    for( int e=0; e<7; e++ ) {
+      fe R0, R1, R2, R3;
+      qgather( row, R0, R1, R2, R3 );                    /* rows Z, Y-X, Y+X, 2dT of entry e */
+      fe br;
+      _Pragma("unroll") for( int k=0; k<10; k++ ) br.v[k] = q4( m1, m2, R2.v[k], R1.v[k], R0.v[k], R3.v[k] );
+      quad_body( t, A2, br, none, none, m1, m2 );        /* A2 + Ai[e] */
+      p3 u; quad_p3( u, t, m1, m2 );
+      row = quad_cached_row( u, m1, m2 );
+      if( act ) AI_ROW4( e+1 );
+    }
+#   undef AI_ROW4
+  }
+
+  u64 const * dg = (u64 const *)((u16 const *)(ws + L.dig) + (size_t)ii*256u);
+  int p   = act ? ((int const *)(ws + L.top))[ii] : -1;
+  int ph  = act ? (p >= 0 ? PH_DBL : PH_FIN) : PH_DONE;
+  u64 dc  = (p >= 0) ? dg[p >> 2] : 0UL;
+  u64 dn  = (p >= 4) ? dg[(p >> 2) - 1] : 0UL;
+  int cur = (int)((dc >> (16 * (p & 3))) & 0xffffu);
+  i32 const * Rw = (i32 const *)(ws + L.R);
+  u32 nha = 0, nhb = 0;
+  u32 nit = (u32)(p + 1);
+  bool qneg = false;
+  fe qrow = fe_zero();
+  /* lanes 0/1 hold R.X / R.Y for the final compare */
+  if( ph == PH_FIN ) {
+    _Pragma("unroll") for( int k=0; k<10; k++ ) qrow.v[k] = Rw[(size_t)((qd & 1)*10 + k)*N + ii];
+  }
+  p1p1 t;
+  t.X = fe_zero(); t.Y = fe_one(); t.Z = fe_one(); t.T = fe_one();
+
+  for( ;; ) {
+    p3 u; quad_p3( u, t, m1, m2 );
+
+    bool fin = (ph == PH_FIN);
+    if( __any( fin ) ) {
+      /* q0: Z*RX, q1: Z*RY; lanes 2,3 compute a don't-care product */
+      fe xz = fe_mul( u.Z, qrow );
+      bool eq = true;
+      _Pragma("unroll") for( int k=0; k<8; k++ ) {
+        i32 ref = vsel( m1, u.Y.v[k], u.X.v[k] );
+        eq = eq && (xz.v[k] == ref);
+      }
+      int e01 = (int)eq;
+      int both = qb<0>( e01 ) & qb<1>( e01 );
+      if( fin ) {
+        if( qd == 0 ) err[i] = (i8)(both ? 0 : -3);
+        ph = PH_DONE;
+      }
+    }
+    if( __all( ph == PH_DONE ) ) break;
+
+    bool isD = (ph == PH_DBL);
+    u64 mD = __builtin_amdgcn_ballot_w64( isD ), mN = __builtin_amdgcn_ballot_w64( qneg );
+    quad_body( t, u, qrow, mD, mN, m1, m2 );
+
+    int da = (int)(i8)(cur & 0xff), db = (int)(i8)(cur >> 8);
+    int nph;
+    if( ph == PH_DBL )       nph = da ? PH_ADDA : (db ? PH_ADDB : -1);
+    else if( ph == PH_ADDA ) nph = db ? PH_ADDB : -1;
+    else if( ph == PH_ADDB ) nph = -1;
+    else                     nph = PH_DONE;
+    if( nph == -1 ) {
+      p--;
+      if( p < 0 ) nph = PH_FIN;
+      else {
+        if( (p & 3) == 3 ) { dc = dn; dn = (p >= 4) ? dg[(p >> 2) - 1] : 0UL; }
+        cur = (int)((dc >> (16 * (p & 3))) & 0xffffu);
+        nph = PH_DBL;
+      }
+    }
+    ph = nph;
+
+    /* this lane's row of the next op's operand: q0 qP, q1 qM, q2 qZ, q3 qT;
+       rows of an entry are [Z, Y-X, Y+X, 2dT], a negative digit swaps Y-X/Y+X */
+    if( ph == PH_ADDA || ph == PH_ADDB ) {
+      int d = (ph == PH_ADDA) ? da : db;
+      int e = (d < 0 ? -d : d) >> 1;
+      qneg = d < 0;
+      int row = (qd == 0) ? (qneg ? 1 : 2) : (qd == 1) ? (qneg ? 2 : 1) : (qd == 2) ? 0 : 3;
+      if( ph == PH_ADDA ) {
+        nha++;
+        int4 const * src = (int4 const *)(Ail + e*48 + row*12);
+        int4 x0 = src[0], x1 = src[1], x2 = src[2];
+        qrow.v[0] = x0.x; qrow.v[1] = x0.y; qrow.v[2] = x0.z; qrow.v[3] = x0.w;
+        qrow.v[4] = x1.x; qrow.v[5] = x1.y; qrow.v[6] = x1.z; qrow.v[7] = x1.w;
+        qrow.v[8] = x2.x; qrow.v[9] = x2.y;
+      } else {
+        nhb++;
+        _Pragma("unroll") for( int k=0; k<10; k++ ) qrow.v[k] = bi[e][row*10 + k];
+      }
+    } else if( ph == PH_FIN ) {
+      _Pragma("unroll") for( int k=0; k<10; k++ ) qrow.v[k] = Rw[(size_t)((qd & 1)*10 + k)*N + ii];
+    }
+  }
+
+  if( want_stats && i < n && qd == 0 ) {
+    u32 * st = (u32 *)(ws + L.st);
+    st[i] = act ? nit : 0u; st[N + i] = act ? nha : 0u; st[2*N + i] = act ? nhb : 0u;
+  }
+}
+
+/* ------------------------------------------------------------------ */
 /* launch                                                               */
+
+/* Batches up to this size use k_dsm4 (fd_ed25519_amd_set_small_batch_max). */
+static volatile u32 g_dsm4_max = 16384u;
+static u32 fd_amd_dsm4_max( void ) { return g_dsm4_max; }
+
+extern "C" void
+fd_ed25519_amd_set_small_batch_max( unsigned long n ) {
+  g_dsm4_max = n > 0xFFFFFFFFUL ? 0xFFFFFFFFu : (u32)n;
+}
 
 int
 fd_amd_launch_verify( u32 n, u8 const * d_pub, u8 const * d_sig, u32 const * d_off, u32 const * d_sz,
@@ -613,7 +857,10 @@ fd_amd_launch_verify( u32 n, u8 const * d_pub, u8 const * d_sig, u32 const * d_o
   if( ev ) (void)hipEventRecord( ev[1], stream );
   hipLaunchKernelGGL( k_decomp, dim3(2u*nb),   dim3(64), 0, stream, n, d_pub, d_sig, d_err, ws, L );
   if( ev ) (void)hipEventRecord( ev[2], stream );
-  hipLaunchKernelGGL( k_dsm,    dim3(nb),      dim3(64), 0, stream, n, d_err, ws, L, want_stats );
+  if( n <= fd_amd_dsm4_max() )   /* small batch: 4 lanes per signature, lower latency */
+    hipLaunchKernelGGL( k_dsm4, dim3((n + 15u)/16u), dim3(64), 0, stream, n, d_err, ws, L, want_stats );
+  else
+    hipLaunchKernelGGL( k_dsm,  dim3(nb),            dim3(64), 0, stream, n, d_err, ws, L, want_stats );
   if( ev ) (void)hipEventRecord( ev[3], stream );
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

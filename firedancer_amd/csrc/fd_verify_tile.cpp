@@ -110,8 +110,12 @@ struct fd_verify_amd_tile {
   ulong              batch_max;
   ulong              wait_ns;
   tcache_t           tc;
-  std::vector<pending_t> meta[2];
+  int                nslot;
+  std::vector<pending_t> meta[FD_AMD_SLOT_MAX];
 };
+
+#define TILE_NSLOT (4)   /* batches in flight: one wave's verify takes ~0.7 ms, so small
+                            batches need several in flight to keep the GPU busy */
 
 extern "C" uint
 fd_verify_amd_tickcount( void ) {
@@ -121,13 +125,14 @@ fd_verify_amd_tickcount( void ) {
 extern "C" fd_verify_amd_tile_t *
 fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong tcache_depth ) {
   if( !batch_max ) return NULL;
-  fd_ed25519_amd_t * eng = fd_ed25519_amd_new( device, batch_max, batch_max * FD_ED25519_AMD_MSG_MAX );
+  fd_ed25519_amd_t * eng = fd_amd_engine_new( device, batch_max, batch_max * FD_ED25519_AMD_MSG_MAX, TILE_NSLOT );
   if( !eng ) return NULL;
-  for( int k=0; k<2; k++ ) if( fd_amd_slot_alloc_aux( &eng->slot[k], batch_max ) ) { fd_ed25519_amd_delete( eng ); return NULL; }
+  for( int k=0; k<TILE_NSLOT; k++ )
+    if( fd_amd_slot_alloc_aux( &eng->slot[k], batch_max ) ) { fd_ed25519_amd_delete( eng ); return NULL; }
   fd_verify_amd_tile_t * t = new fd_verify_amd_tile_t();
-  t->eng = eng; t->batch_max = batch_max; t->wait_ns = batch_wait_ns;
+  t->eng = eng; t->batch_max = batch_max; t->wait_ns = batch_wait_ns; t->nslot = TILE_NSLOT;
   t->tc.init( tcache_depth );
-  for( int k=0; k<2; k++ ) t->meta[k].resize( batch_max );
+  for( int k=0; k<TILE_NSLOT; k++ ) t->meta[k].resize( batch_max );
   return t;
 }
 
@@ -149,9 +154,10 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
   if( hipSetDevice( e->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
 
   ulong in_seq = in_seq0, out_seq = out_seq0, lat_n = 0;
-  int   stage = 0;                 /* slot being filled */
+  int   K = t->nslot;
+  int   stage = 0;                 /* slot being filled; slots are used round robin, so the */
+  int   oldest = 0, nfly = 0;      /* in-flight ones are oldest, oldest+1, ... (mod K)      */
   ulong staged = 0, blob_at = 0, stage_t0 = 0;
-  int   fifo[2], nfly = 0;         /* in-flight slots, oldest first */
   int   rc;
 
   auto publish = [&]( int k ) -> int {
@@ -175,27 +181,26 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
   for( ;; ) {
     /* 1. retire the oldest batch if it is done (publication stays in
           arrival order: batches retire in launch order) */
-    if( nfly ) {
-      int r = fd_amd_slot_ready( &e->slot[fifo[0]] );
+    while( nfly ) {
+      int r = fd_amd_slot_ready( &e->slot[oldest] );
       if( r < 0 ) return r;
-      if( r ) {
-        if( (rc = publish( fifo[0] )) ) return rc;
-        fifo[0] = fifo[1]; nfly--;
-      }
+      if( !r ) break;
+      if( (rc = publish( oldest )) ) return rc;
+      oldest = (oldest + 1) % K; nfly--;
     }
     bool done_in = frag_cnt ? (diag->in_cnt >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
     if( done_in && !staged && !nfly ) break;
-    bool free_slot = !(nfly == 2 || (nfly == 1 && fifo[0] == stage));
-    if( !free_slot ) continue;
+    if( nfly == K ) continue;      /* every slot in flight: the staging slot is busy */
 
     /* 2. stage input frags into the free slot */
     slot_t * s = &e->slot[stage];
+    bool idle_in = false;
     while( !done_in && staged < t->batch_max ) {
       if( frag_cnt && diag->in_cnt >= frag_cnt ) break;
       fd_frag_meta_t const * m = in_mcache + (in_seq & (in_depth-1UL));
       ulong seq_found = __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE );
       long  d = (long)(seq_found - in_seq);
-      if( d < 0 ) break;                                                 /* not yet published */
+      if( d < 0 ) { idle_in = true; break; }                             /* not yet published */
       if( d > 0 ) { diag->ovrn_cnt += (ulong)d; in_seq = seq_found; continue; }   /* overrun: resync */
       ulong chunk = m->chunk, sz = m->sz, ctl = m->ctl, tsorig = m->tsorig;
       __atomic_thread_fence( __ATOMIC_ACQUIRE );
@@ -217,14 +222,19 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
     }
     done_in = frag_cnt ? (diag->in_cnt >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
 
-    /* 3. adaptive launch: full batch, idle GPU, end of input, or the
-          oldest staged frag waited long enough */
-    if( staged && ( staged == t->batch_max || !nfly || done_in ||
+    /* 3. adaptive launch (a free slot exists here): full batch, input
+          momentarily drained (greedy: under light load batches stay small
+          and latency low; under load every slot is busy and batches grow
+          toward batch_max), end of input, or the oldest staged frag waited
+          batch_wait_ns.  A nonzero batch_wait_ns turns the greedy rule off
+          while another batch is in flight. */
+    bool greedy = idle_in && (!t->wait_ns || !nfly);
+    if( staged && ( staged == t->batch_max || greedy || done_in ||
                     (t->wait_ns && now_ns() - stage_t0 >= t->wait_ns) ) ) {
       if( (rc = fd_amd_slot_launch( s, staged, blob_at, NULL, 1 )) ) return rc;
       diag->batch_cnt++; diag->batch_sig_cnt += staged;
-      fifo[nfly++] = stage;
-      stage ^= 1; staged = 0; blob_at = 0;
+      nfly++;
+      stage = (stage + 1) % K; staged = 0; blob_at = 0;
     }
   }
   return FD_ED25519_AMD_OK;
@@ -234,11 +244,11 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
 /* streaming benchmark: producer -> tile -> consumer                    */
 
 extern "C" int
-fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, ulong pool_n, uchar const * pub,
-                            uchar const * sig, uint const * msg_off, uint const * msg_sz, uchar const * blob,
-                            ulong frag_cnt, double * out ) {
+fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, double rate, ulong pool_n,
+                            uchar const * pub, uchar const * sig, uint const * msg_off, uint const * msg_sz,
+                            uchar const * blob, ulong frag_cnt, double * out ) {
   if( !pool_n || !frag_cnt || !out ) return FD_ED25519_AMD_ERR_INVAL;
-  ulong depth = 1UL; while( depth < 4UL*batch_max + 1024UL ) depth <<= 1;
+  ulong depth = 1UL; while( depth < 8UL*batch_max + 1024UL ) depth <<= 1;   /* > batches in flight + staging */
   ulong mtu = 96UL + FD_ED25519_AMD_MSG_MAX;
   ulong chunk_mtu = ((mtu + 2UL*FD_CHUNK_SZ - 1UL) >> (1 + FD_CHUNK_LG_SZ)) << 1;
   ulong data_chunks = chunk_mtu * (depth + 2UL);
@@ -259,13 +269,18 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, ul
 
   std::thread prod( [&]() {
     ulong chunk = 0;
+    ulong p0 = now_ns();
     for( ulong seq=0; seq<frag_cnt; seq++ ) {
+      ulong due = rate > 0.0 ? p0 + (ulong)((double)seq * 1e9 / rate) : 0UL;   /* paced: open loop */
+      if( due ) while( now_ns() < due ) { /* spin */ }
       /* credit: do not lap the tile's consumption of the input mcache */
       while( seq - __atomic_load_n( &diag.in_cnt, __ATOMIC_ACQUIRE ) >= depth - 16UL ) { /* spin */ }
       ulong k = seq % pool_n, msz = msg_sz[k], sz = 96UL + msz;
       uchar * p = dcache + chunk * FD_CHUNK_SZ;
       memcpy( p, pub + 32UL*k, 32 ); memcpy( p + 32, sig + 64UL*k, 64 ); memcpy( p + 96, blob + msg_off[k], msz );
-      fd_mcache_publish( in_mc.data(), depth, seq, 0UL, chunk, sz, 3UL, fd_verify_amd_tickcount(), 0UL );
+      /* tsorig = the scheduled send time when paced, so producer stalls count as latency */
+      uint tso = due ? (uint)due : fd_verify_amd_tickcount();
+      fd_mcache_publish( in_mc.data(), depth, seq, 0UL, chunk, sz, 3UL, tso, 0UL );
       chunk = fd_dcache_compact_next( chunk, sz, 0UL, wmark );
     }
   } );

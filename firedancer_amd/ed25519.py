@@ -74,6 +74,8 @@ def lib():
     L.fd_ed25519_amd_verify_txns.restype = i
     L.fd_txn_amd_parse_dev.argtypes = [ul, vp, vp, vp, vp, vp, ul, vp]
     L.fd_txn_amd_parse_dev.restype = i
+    L.fd_ed25519_amd_set_small_batch_max.argtypes = [ul]
+    L.fd_ed25519_amd_set_small_batch_max.restype = None
     L.fd_verify_amd_tile_new.argtypes = [i, ul, ul, ul]
     L.fd_verify_amd_tile_new.restype = vp
     L.fd_verify_amd_tile_delete.argtypes = [vp]
@@ -82,7 +84,7 @@ def lib():
     L.fd_verify_amd_tile_run.restype = i
     L.fd_verify_amd_tickcount.argtypes = []
     L.fd_verify_amd_tickcount.restype = ui
-    L.fd_verify_amd_bench_stream.argtypes = [i, ul, ul, ul, vp, vp, vp, vp, vp, ul, vp]
+    L.fd_verify_amd_bench_stream.argtypes = [i, ul, ul, ctypes.c_double, ul, vp, vp, vp, vp, vp, ul, vp]
     L.fd_verify_amd_bench_stream.restype = i
     _lib = L
     return L
@@ -261,6 +263,12 @@ def debug_digits_dev(n, d_ws, d_dig, d_top, stream=0):
         raise EngineError("fd_ed25519_amd_debug_digits_dev rc=%d" % rc)
 
 
+def set_small_batch_max(n):
+    """Batches of at most n signatures use the 4-lane latency kernel (k_dsm4)."""
+    lib().fd_ed25519_amd_set_small_batch_max(int(n))
+
+
+SMALL_BATCH_MAX_DEFAULT = 16384
 FD_TXN_AMD_ERR_PARSE = -4
 FD_TXN_MAX_SZ = 3570
 

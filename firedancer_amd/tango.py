@@ -88,13 +88,14 @@ class VerifyTile:
         return d, lat[:min(lat_max, d["out_cnt"])]
 
 
-def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, blob, frag_cnt):
-    """fd_verify_amd_bench_stream: producer -> tile -> consumer; returns
+def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, blob, frag_cnt, rate=0.0):
+    """fd_verify_amd_bench_stream: producer (rate frags/s, 0 = saturate) -> tile -> consumer; returns
     dict(frags_per_s, p50_ns, p99_ns, p999_ns, mean_batch, published, sv_filt)."""
     out = (ctypes.c_double * 7)()
     p = [np.ascontiguousarray(a) for a in (pub, sig, msg_off, msg_sz, blob)]
     vp = ctypes.c_void_p
-    rc = ed25519.lib().fd_verify_amd_bench_stream(int(device), int(batch_max), int(batch_wait_ns), p[0].shape[0],
+    rc = ed25519.lib().fd_verify_amd_bench_stream(int(device), int(batch_max), int(batch_wait_ns), float(rate),
+                                                  p[0].shape[0],
                                                   *[vp(a.ctypes.data) for a in p], int(frag_cnt), out)
     if rc:
         raise ed25519.EngineError("fd_verify_amd_bench_stream rc=%d" % rc)

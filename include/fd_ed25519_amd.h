@@ -203,6 +203,14 @@ fd_ed25519_amd_sign_batch( ulong         n,
                            uchar *       sig,
                            int           nthread );
 
+/* Kernel choice for the double-scalar multiply.  Batches of at most n
+   signatures (default 16384) run the latency kernel (four lanes per
+   signature, k_dsm4); larger ones the throughput kernel (one lane per
+   signature, k_dsm).  Both give identical verdicts; 0 disables the
+   latency kernel.  Process-wide. */
+void
+fd_ed25519_amd_set_small_batch_max( ulong n );
+
 /* Library version / build string. */
 char const *
 fd_ed25519_amd_version( void );

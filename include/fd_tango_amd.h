@@ -104,11 +104,14 @@ typedef struct {
 
 typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
 
-/* A tile bound to HIP device `device`.  batch_max: largest GPU batch;
-   batch_wait_ns: how long a non-empty partial batch may wait for more
-   frags while the GPU is busy (0 = only the adaptive rule: launch whenever
-   the GPU is idle or the batch is full); tcache_depth: HA dedup window
-   (tags remembered, 0 disables).  NULL on failure. */
+/* A tile bound to HIP device `device`, with up to 4 GPU batches in
+   flight.  batch_max: largest GPU batch.  Launch rule (adaptive): a batch
+   goes as soon as a slot is free and the input is momentarily drained
+   (light load: small batches, low latency; heavy load: every slot busy, so
+   batches grow toward batch_max).  batch_wait_ns != 0 replaces "drained"
+   by "the oldest staged frag waited batch_wait_ns" while another batch is
+   in flight (fewer, larger batches).  tcache_depth: HA dedup window (tags
+   remembered, 0 disables).  NULL on failure. */
 fd_verify_amd_tile_t *
 fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong tcache_depth );
 
@@ -147,10 +150,11 @@ fd_verify_amd_tickcount( void );
 
 /* Streaming benchmark (config 5): a producer thread publishes frags
    public_key | signature | message cyclically from the given pool (SoA
-   layout of fd_ed25519_amd_verify_soa) into a private mcache/dcache at
-   the highest rate the tile sustains (credit-based flow control), the tile
-   runs on `device`, and a consumer drains the output.  Runs until
-   frag_cnt frags were published.  out[0] = frags/s through the tile,
+   layout of fd_ed25519_amd_verify_soa) into a private mcache/dcache --
+   at `rate` frags/s (open loop; tsorig = scheduled send time) or, with
+   rate 0, as fast as the tile accepts (credit-based flow control) -- the
+   tile runs on `device` with 4 batches in flight, and a consumer drains
+   the output.  Runs until frag_cnt frags were published.  out[0] = frags/s through the tile,
    out[1..3] = p50 / p99 / p999 latency in ns (producer publish -> tile
    publish), out[4] = mean GPU batch size, out[5] = frags published,
    out[6] = frags dropped by verification.  Returns 0 or an error code. */
@@ -158,6 +162,7 @@ int
 fd_verify_amd_bench_stream( int           device,
                             ulong         batch_max,
                             ulong         batch_wait_ns,
+                            double        rate,
                             ulong         pool_n,
                             uchar const * pub,
                             uchar const * sig,

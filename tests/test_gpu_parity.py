@@ -191,3 +191,42 @@ def test_prep_digits_vs_python(golden):
         assert ga == ea, ("h digits", j, "gpu digits encode %x, want %x" % (hv, h))
         nz = [p for p in range(256) if ea[p] or eb[p]]
         assert tp[j] == (max(nz) if nz else -1)
+
+
+@pytest.fixture(params=["k_dsm", "k_dsm4"])
+def dsm_kernel(request):
+    """Run a test once per double-scalar-mult kernel (throughput / latency)."""
+    from firedancer_amd import ed25519
+    ed25519.set_small_batch_max(0 if request.param == "k_dsm" else 1 << 20)
+    yield request.param
+    ed25519.set_small_batch_max(ed25519.SMALL_BATCH_MAX_DEFAULT)
+
+
+def test_both_kernels_golden_and_mixed(engine, golden, dsm_kernel):
+    """Golden fixtures and 2^15 fresh mixed signatures through each kernel."""
+    err = engine.verify_soa(golden.pub, golden.sig, golden.msg_off, golden.msg_sz, golden.blob)
+    assert np.array_equal(err, golden.expect), dsm_kernel
+    b = _sign_stream(4321, 1 << 15, 0, 1232, True)
+    err = engine.verify_soa(b.pub, b.sig, b.msg_off, b.msg_sz, b.blob)
+    assert np.array_equal(err, _oracle.verify_batch(b)), dsm_kernel
+
+
+def test_both_kernels_stats_and_false_rejects(dsm_kernel):
+    """Work statistics (device path) and the limb-compare false rejects of
+    the golden set through each kernel."""
+    from firedancer_amd import ed25519, hip
+    b = _sign_stream(98, 2048, 200, 200, True)
+    n = len(b)
+    d = {k: hip.DeviceBuffer.from_array(v) for k, v in
+         dict(pub=b.pub, sig=b.sig, off=b.msg_off, sz=b.msg_sz, blob=b.blob).items()}
+    err = hip.DeviceBuffer(n)
+    ws = hip.DeviceBuffer(ed25519.workspace_footprint(n))
+    stats = hip.DeviceBuffer(4 * 3 * n)
+    stream = hip.Stream()
+    ed25519.verify_dev(n, d["pub"].ptr, d["sig"].ptr, d["off"].ptr, d["sz"].ptr, d["blob"].ptr, err.ptr, ws.ptr,
+                       stream.handle)
+    ed25519.work_stats_dev(n, ws.ptr, stats.ptr, stream.handle)
+    stream.synchronize()
+    exp, st = _oracle.verify_batch(b, stats=True)
+    assert np.array_equal(err.to_array(np.int8, n), exp)
+    assert np.array_equal(stats.to_array(np.uint32, 3 * n).reshape(3, n).T, st)

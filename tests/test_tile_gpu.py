@@ -131,3 +131,5 @@ def test_stream_bench_smoke():
     r = tango.bench_stream(0, 256, 0, pub, sig, off, sz, blob, 20000)
     assert r["published"] == 20000 and r["sv_filt"] == 0
     assert r["frags_per_s"] > 0 and 0 < r["p50_ns"] <= r["p99_ns"]
+    r = tango.bench_stream(0, 256, 0, pub, sig, off, sz, blob, 5000, rate=50000.0)
+    assert r["published"] == 5000 and r["p50_ns"] > 0

@@ -14,7 +14,7 @@ for i, l in enumerate(s):
     m = re.match(r"^_Z(\d+)(\w+):", l)
     if m:
         starts[m.group(2)[:int(m.group(1))]] = i
-for k in ("k_prep", "k_decomp", "k_dsm"):
+for k in ("k_prep", "k_decomp", "k_dsm", "k_dsm4"):
     i = starts[k]
     j = next(n for n in range(i, len(s)) if "s_endpgm" in s[n])
     body = s[i:j]
@@ -24,7 +24,7 @@ for k in ("k_prep", "k_decomp", "k_dsm"):
     occ += " scratch " + re.search(r"; ScratchSize: (\d+)", meta).group(1)
     ins = [l.split()[0] for l in body if l.startswith("\t") and not l.strip().startswith(";") and not l.strip().startswith(".")]
     print("%-9s vgpr %s occ %s  static instrs %d" % (k, vg, occ, len(ins)))
-    if k == "k_dsm":
+    if k in ("k_dsm", "k_dsm4"):
         # largest loop: header with "Inner Loop Header" whose back-edge is farthest
         hdrs = [(n, re.match(r"^(\.LBB\d+_\d+):", body[n]).group(1)) for n in range(len(body)) if "Loop Header" in body[n]]
         best = None
@@ -36,7 +36,7 @@ for k in ("k_prep", "k_decomp", "k_dsm"):
         c = collections.Counter(loop)
         heavy = sum(v for k2, v in c.items() if k2.startswith(("v_mad_i64", "v_mad_u64", "v_mul_lo", "v_lshl_add_u64", "v_ashrrev_i64", "v_lshrrev_b64", "v_lshlrev_b64", "v_mul_hi")))
         valu = sum(v for k2, v in c.items() if k2.startswith("v_"))
-        print("k_dsm main loop: %d instrs, %d VALU (%d 64-bit/mul class), %d v_mad_i64_i32" % (len(loop), valu, heavy, c["v_mad_i64_i32"]))
+        print(k + " main loop: %d instrs, %d VALU (%d 64-bit/mul class), %d v_mad_i64_i32" % (len(loop), valu, heavy, c["v_mad_i64_i32"]))
         print("  " + ", ".join("%s %d" % kv for kv in c.most_common(16)))
 PY
 rm -rf $D
