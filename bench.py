@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1 << 20, help="signatures per GPU per step")
+    ap.add_argument("--sigs", "--n", dest="n", type=int, default=1 << 20, help="signatures per GPU per step")
     ap.add_argument("--msg-sz", type=int, default=200)
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -120,7 +120,10 @@ def main():
 
     from firedancer_amd import ed25519, hip
 
-    if hip.device_count() <= local:
+    ndev = hip.device_count()
+    if os.environ.get("FD_AMD_DEVICE_MAP") == "mod" and ndev:   # rehearsal: more ranks than GPUs
+        local = local % ndev
+    if ndev <= local:
         raise SystemExit("bench.py: no HIP device %d visible" % local)
     hip.set_device(local)
     nthread = max(1, min(16, (os.cpu_count() or 1) // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", world)))))
