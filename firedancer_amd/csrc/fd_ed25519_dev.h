@@ -292,6 +292,30 @@ FD_DEV void sha512_compress( u64 st[8], u64 w[16] ) {
   st[0]+=a; st[1]+=b; st[2]+=c; st[3]+=d; st[4]+=e; st[5]+=f; st[6]+=g; st[7]+=h;
 }
 
+/* 8 bytes of the padded message starting at message offset o (multiple of
+   8), little-endian: message bytes, the 0x80 terminator at offset sz, zeros
+   after.  Only dwords that intersect [0, sz) are loaded. */
+FD_DEV u64
+msg_word( u8 const * __restrict__ m, u32 sz, u32 o ) {
+  uintptr_t a  = (uintptr_t)(m + o);
+  u32 sh = (u32)(a & 3u);
+  u32 const * p = (u32 const *)(a - sh);   /* dword j covers message bytes [o-sh+4j, o-sh+4j+4) */
+  u32 d0 = (o       < sz + sh)         ? p[0] : 0u;
+  u32 d1 = (o + 4u  < sz + sh)         ? p[1] : 0u;
+  u32 d2 = (sh && o + 8u < sz + sh)    ? p[2] : 0u;
+  u32 lo = __builtin_amdgcn_alignbyte( d1, d0, sh );
+  u32 hi = __builtin_amdgcn_alignbyte( d2, d1, sh );
+  u64 w = ((u64)hi << 32) | lo;
+  if( sz >= o + 8u ) return w;                                /* 8 message bytes */
+  if( sz <  o      ) return 0UL;                              /* past the terminator */
+  u32 nv = sz - o;                                            /* 0..7 message bytes, then 0x80 */
+  return (w & ((1UL << (8u*nv)) - 1UL)) | (0x80UL << (8u*nv));
+}
+
+FD_DEV u64 bswap64( u64 x ) {
+  return ((u64)__builtin_bswap32( (u32)x ) << 32) | (u64)__builtin_bswap32( (u32)(x >> 32) );
+}
+
 /* ------------------------------------------------------------------ */
 /* x mod L for a 512-bit x (fd_ed25519_sc_reduce, fd_ed25519_user.c:3-110:
    canonical result, so any exact reduction is bit-identical). 32-bit word

@@ -312,6 +312,17 @@ fd_txn_amd_parse_dev( ulong txn_cnt, uchar const * d_payload, uint const * d_txn
   return FD_ED25519_AMD_OK;
 }
 
+extern "C" int
+fd_ed25519_amd_sign_dev( ulong n, uchar const * d_prv, uint const * d_msg_off, uint const * d_msg_sz,
+                         uchar const * d_blob, uchar * d_pub, uchar * d_sig, void * stream ) {
+  if( n > 0xFFFFFFFFUL ) return FD_ED25519_AMD_ERR_INVAL;
+  if( !n ) return FD_ED25519_AMD_OK;
+  if( !d_prv || !d_msg_off || !d_msg_sz || !d_blob || !d_pub || !d_sig ) return FD_ED25519_AMD_ERR_INVAL;
+  if( fd_amd_launch_sign( (uint32_t)n, d_prv, d_msg_off, d_msg_sz, d_blob, d_pub, d_sig, (hipStream_t)stream ) )
+    return FD_ED25519_AMD_ERR_DEVICE;
+  return FD_ED25519_AMD_OK;
+}
+
 extern "C" ulong
 fd_ed25519_amd_workspace_footprint( ulong n ) {
   return fd_amd_ws_layout( n ).total;

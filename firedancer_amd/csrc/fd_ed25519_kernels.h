@@ -41,4 +41,9 @@ int fd_amd_launch_txn_parse( uint32_t txn_cnt, uint8_t const * d_payload, uint32
 int fd_amd_launch_txn_reduce( uint32_t txn_cnt, uint32_t const * d_fp, uint32_t const * d_tbase,
                               int8_t const * d_err, int8_t * d_terr, hipStream_t stream );
 
+/* GPU keygen + sign (fd_ed25519_sign.hip): prv[n][32] seeds, messages
+   blob[off[i] .. +sz[i]) -> pub[n][32], sig[n][64].  0 on success. */
+int fd_amd_launch_sign( uint32_t n, uint8_t const * d_prv, uint32_t const * d_off, uint32_t const * d_sz,
+                        uint8_t const * d_blob, uint8_t * d_pub, uint8_t * d_sig, hipStream_t stream );
+
 #endif

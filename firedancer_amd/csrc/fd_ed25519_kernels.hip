@@ -66,30 +66,6 @@ fd_amd_ws_layout( size_t n ) {
 /* ------------------------------------------------------------------ */
 /* k_prep                                                               */
 
-/* 8 bytes of the padded message starting at message offset o (multiple of
-   8), little-endian: message bytes, the 0x80 terminator at offset sz, zeros
-   after.  Only dwords that intersect [0, sz) are loaded. */
-__device__ __forceinline__ u64
-msg_word( u8 const * __restrict__ m, u32 sz, u32 o ) {
-  uintptr_t a  = (uintptr_t)(m + o);
-  u32 sh = (u32)(a & 3u);
-  u32 const * p = (u32 const *)(a - sh);   /* dword j covers message bytes [o-sh+4j, o-sh+4j+4) */
-  u32 d0 = (o       < sz + sh)         ? p[0] : 0u;
-  u32 d1 = (o + 4u  < sz + sh)         ? p[1] : 0u;
-  u32 d2 = (sh && o + 8u < sz + sh)    ? p[2] : 0u;
-  u32 lo = __builtin_amdgcn_alignbyte( d1, d0, sh );
-  u32 hi = __builtin_amdgcn_alignbyte( d2, d1, sh );
-  u64 w = ((u64)hi << 32) | lo;
-  if( sz >= o + 8u ) return w;                                /* 8 message bytes */
-  if( sz <  o      ) return 0UL;                              /* past the terminator */
-  u32 nv = sz - o;                                            /* 0..7 message bytes, then 0x80 */
-  return (w & ((1UL << (8u*nv)) - 1UL)) | (0x80UL << (8u*nv));
-}
-
-__device__ __forceinline__ u64 bswap64( u64 x ) {
-  return ((u64)__builtin_bswap32( (u32)x ) << 32) | (u64)__builtin_bswap32( (u32)(x >> 32) );
-}
-
 /* fd_ed25519_ge_slide (avx/fd_ed25519_ge.c:378-400) on a 256-bit register
    shift window: bit 0 of w0 is always position `pos`, so every look-ahead
    index is static.  The reference's carry loop "for k>=i+b: if !r[k] set,

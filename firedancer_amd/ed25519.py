@@ -74,6 +74,8 @@ def lib():
     L.fd_ed25519_amd_verify_txns.restype = i
     L.fd_txn_amd_parse_dev.argtypes = [ul, vp, vp, vp, vp, vp, ul, vp]
     L.fd_txn_amd_parse_dev.restype = i
+    L.fd_ed25519_amd_sign_dev.argtypes = [ul, vp, vp, vp, vp, vp, vp, vp]
+    L.fd_ed25519_amd_sign_dev.restype = i
     L.fd_ed25519_amd_set_small_batch_max.argtypes = [ul]
     L.fd_ed25519_amd_set_small_batch_max.restype = None
     L.fd_verify_amd_tile_new.argtypes = [i, ul, ul, ul]
@@ -261,6 +263,29 @@ def debug_digits_dev(n, d_ws, d_dig, d_top, stream=0):
     rc = lib().fd_ed25519_amd_debug_digits_dev(int(n), d_ws, d_dig, d_top, stream)
     if rc:
         raise EngineError("fd_ed25519_amd_debug_digits_dev rc=%d" % rc)
+
+
+def sign_dev(n, d_prv, d_off, d_sz, d_blob, d_pub, d_sig, stream=0):
+    """GPU keygen + sign on device buffers (fd_ed25519_amd_sign_dev)."""
+    rc = lib().fd_ed25519_amd_sign_dev(int(n), d_prv, d_off, d_sz, d_blob, d_pub, d_sig, stream)
+    if rc:
+        raise EngineError("fd_ed25519_amd_sign_dev rc=%d" % rc)
+
+
+def sign_batch_gpu(prv, blob, msg_off, msg_sz):
+    """Host arrays in, (pub, sig) out, signed on the GPU (k_sign)."""
+    from . import hip
+    prv = np.ascontiguousarray(prv, np.uint8)
+    n = prv.shape[0]
+    if not n:
+        return np.zeros((0, 32), np.uint8), np.zeros((0, 64), np.uint8)
+    d = [hip.DeviceBuffer.from_array(np.ascontiguousarray(a)) for a in
+         (prv, np.asarray(msg_off, np.uint32), np.asarray(msg_sz, np.uint32), np.asarray(blob, np.uint8))]
+    d_pub, d_sig = hip.DeviceBuffer(32 * n), hip.DeviceBuffer(64 * n)
+    st = hip.Stream()
+    sign_dev(n, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr, d_pub.ptr, d_sig.ptr, st.handle)
+    st.synchronize()
+    return d_pub.to_array(np.uint8, 32 * n).reshape(n, 32), d_sig.to_array(np.uint8, 64 * n).reshape(n, 64)
 
 
 def set_small_batch_max(n):

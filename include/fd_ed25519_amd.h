@@ -203,6 +203,21 @@ fd_ed25519_amd_sign_batch( ulong         n,
                            uchar *       sig,
                            int           nthread );
 
+/* GPU batch keygen + sign (workload synthesis): device
+   buffers prv[n][32] (32-aligned records), messages d_blob[d_msg_off[i] ..
+   +d_msg_sz[i]) -> d_pub[n][32], d_sig[n][64]; the bytes equal
+   fd_ed25519_public_from_private / fd_ed25519_sign (deterministic RFC 8032).
+   Not constant time: never for real keys.  Enqueued on `stream`. */
+int
+fd_ed25519_amd_sign_dev( ulong         n,
+                         uchar const * d_prv,
+                         uint const *  d_msg_off,
+                         uint const *  d_msg_sz,
+                         uchar const * d_blob,
+                         uchar *       d_pub,
+                         uchar *       d_sig,
+                         void *        stream );
+
 /* Kernel choice for the double-scalar multiply.  Batches of at most n
    signatures (default 16384) run the latency kernel (four lanes per
    signature, k_dsm4); larger ones the throughput kernel (one lane per
