@@ -299,6 +299,64 @@ fd_ed25519_amd_verify_txns( fd_ed25519_amd_t * e, ulong txn_cnt, uchar const * p
   return FD_ED25519_AMD_OK;
 }
 
+/* Device-resident transaction batch: workspace = verify workspace for
+   slot_cnt signatures + the signature layout planes + footprints. */
+namespace {
+struct txn_ws_t { size_t vws, pub, sig, off, sz, skip, err, fp, total; };
+inline size_t al256( size_t x ) { return (x + 255UL) & ~(size_t)255UL; }
+txn_ws_t txn_ws_layout( ulong txn_cnt, ulong slot_cnt ) {
+  txn_ws_t L; size_t o = 0; ulong S = slot_cnt ? slot_cnt : 1UL;
+  L.vws  = o; o = al256( o + fd_amd_ws_layout( S ).total );
+  L.pub  = o; o = al256( o + 32UL*S );
+  L.sig  = o; o = al256( o + 64UL*S );
+  L.off  = o; o = al256( o + 4UL*S );
+  L.sz   = o; o = al256( o + 4UL*S );
+  L.skip = o; o = al256( o + S );
+  L.err  = o; o = al256( o + S );
+  L.fp   = o; o = al256( o + 4UL*(txn_cnt ? txn_cnt : 1UL) );
+  L.total = o;
+  return L;
+}
+}
+
+extern "C" ulong
+fd_ed25519_amd_txn_workspace_footprint( ulong txn_cnt, ulong slot_cnt ) {
+  return txn_ws_layout( txn_cnt, slot_cnt ).total;
+}
+
+extern "C" ulong
+fd_ed25519_amd_txn_slots( ulong txn_cnt, uchar const * payload, uint const * txn_off, uint const * txn_sz,
+                          uint * tbase ) {
+  ulong acc = 0;
+  for( ulong t=0; t<txn_cnt; t++ ) { tbase[t] = (uint)acc; acc += txn_slots( payload + txn_off[t], txn_sz[t] ); }
+  tbase[txn_cnt] = (uint)acc;
+  return acc;
+}
+
+extern "C" int
+fd_ed25519_amd_verify_txns_dev( ulong txn_cnt, ulong slot_cnt, uchar const * d_payload, uint const * d_txn_off,
+                                uint const * d_txn_sz, uint const * d_tbase, schar * d_txn_err, schar * d_sig_err,
+                                void * d_ws, void * stream ) {
+  if( txn_cnt > 0xFFFFFFFFUL || slot_cnt > 0xFFFFFFFFUL ) return FD_ED25519_AMD_ERR_INVAL;
+  if( !txn_cnt ) return FD_ED25519_AMD_OK;
+  if( !d_payload || !d_txn_off || !d_txn_sz || !d_tbase || !d_txn_err || !d_ws ) return FD_ED25519_AMD_ERR_INVAL;
+  txn_ws_t L = txn_ws_layout( txn_cnt, slot_cnt );
+  uint8_t * w = (uint8_t *)d_ws;
+  hipStream_t st = (hipStream_t)stream;
+  int8_t * err = d_sig_err ? (int8_t *)d_sig_err : (int8_t *)(w + L.err);
+  if( fd_amd_launch_txn_parse( (uint32_t)txn_cnt, d_payload, d_txn_off, d_txn_sz, (uint32_t *)(w + L.fp), NULL, 0,
+                               d_tbase, w + L.pub, w + L.sig, (uint32_t *)(w + L.off), (uint32_t *)(w + L.sz),
+                               (int8_t *)(w + L.skip), st ) )
+    return FD_ED25519_AMD_ERR_DEVICE;
+  if( slot_cnt && fd_amd_launch_verify( (uint32_t)slot_cnt, w + L.pub, w + L.sig, (uint32_t *)(w + L.off),
+                                        (uint32_t *)(w + L.sz), d_payload, err, w + L.vws, st, 0, NULL,
+                                        (int8_t *)(w + L.skip) ) )
+    return FD_ED25519_AMD_ERR_DEVICE;
+  if( fd_amd_launch_txn_reduce( (uint32_t)txn_cnt, (uint32_t *)(w + L.fp), d_tbase, err, (int8_t *)d_txn_err, st ) )
+    return FD_ED25519_AMD_ERR_DEVICE;
+  return FD_ED25519_AMD_OK;
+}
+
 extern "C" int
 fd_txn_amd_parse_dev( ulong txn_cnt, uchar const * d_payload, uint const * d_txn_off, uint const * d_txn_sz,
                       uint * d_footprint, uchar * d_out, ulong out_stride, void * stream ) {

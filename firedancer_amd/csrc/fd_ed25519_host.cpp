@@ -358,4 +358,65 @@ fd_ed25519_amd_sign_batch( unsigned long n, uint8_t const * prv, uint8_t const *
   return 0;
 }
 
+/* Workload synthesis for the transaction front end (config 4): txn_cnt
+   well-formed wire transactions (fd_txn.h layout), legacy and v0 by turns,
+   with nsig in [nsig_lo, nsig_hi] signers whose account addresses are the
+   next public keys of pub[] (consumed in order) and a message of about
+   [msg_lo, msg_hi] bytes, capped so a payload fits the 1232-byte MTU.
+   Signature fields are left zero; per signature s the caller gets where
+   its message starts/ends (sig_msg_off / sig_msg_sz, offsets in payload)
+   and where its 64 bytes go (sig_at).  Returns the number of signatures
+   (0 if payload_cap or pub_cnt is too small). */
+unsigned long
+fd_ed25519_amd_synth_txns( unsigned long seed, unsigned long txn_cnt, uint32_t nsig_lo, uint32_t nsig_hi,
+                           uint32_t msg_lo, uint32_t msg_hi, uint8_t const * pub, unsigned long pub_cnt,
+                           uint8_t * payload, unsigned long payload_cap, uint32_t * txn_off, uint32_t * txn_sz,
+                           uint32_t * sig_msg_off, uint32_t * sig_msg_sz, uint32_t * sig_at ) {
+  uint64_t s = seed * 0x9E3779B97F4A7C15UL + 0x1234567UL;
+  auto rnd = [&]() -> uint64_t {
+    uint64_t z = (s += 0x9e3779b97f4a7c15UL);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9UL; z = (z ^ (z >> 27)) * 0x94d049bb133111ebUL; return z ^ (z >> 31);
+  };
+  auto cu16 = [&]( uint8_t * p, uint32_t v ) -> uint32_t {
+    if( v < 0x80u ) { p[0] = (uint8_t)v; return 1u; }
+    if( v < 0x4000u ) { p[0] = (uint8_t)(0x80u | (v & 0x7fu)); p[1] = (uint8_t)(v >> 7); return 2u; }
+    p[0] = (uint8_t)(0x80u | (v & 0x7fu)); p[1] = (uint8_t)(0x80u | ((v >> 7) & 0x7fu)); p[2] = (uint8_t)(v >> 14); return 3u;
+  };
+  unsigned long at = 0, ns = 0;
+  if( nsig_lo < 1 ) nsig_lo = 1;
+  if( nsig_hi < nsig_lo ) nsig_hi = nsig_lo;
+  for( unsigned long t=0; t<txn_cnt; t++ ) {
+    uint32_t nsig = nsig_lo + (uint32_t)(rnd() % (nsig_hi - nsig_lo + 1u));
+    if( ns + nsig > pub_cnt || at + 1232UL > payload_cap ) return 0UL;
+    int v0 = (int)(t & 1u);
+    uint32_t nx = nsig >= 10u ? 1u : 1u + (uint32_t)(rnd() % 3u), nacct = nsig + nx;
+    uint32_t fixed = 1u + 64u*nsig + (v0 ? 1u : 0u) + 3u + 1u + 32u*nacct + 32u + 1u + 1u + 1u + 2u + 2u + (v0 ? 1u : 0u);
+    uint32_t want = msg_lo + (uint32_t)(rnd() % (msg_hi - msg_lo + 1u));
+    uint32_t total = fixed + (want > fixed - 1u - 64u*nsig ? want - (fixed - 1u - 64u*nsig) : 0u);
+    if( total > 1232u ) total = 1232u;
+    uint32_t dlen = total - fixed;
+    if( fixed > 1232u ) return 0UL;
+    uint8_t * p = payload + at;
+    uint32_t o = 0;
+    p[o++] = (uint8_t)nsig;
+    for( uint32_t j=0; j<nsig; j++ ) { sig_at[ns + j] = (uint32_t)(at + o); memset( p + o, 0, 64 ); o += 64u; }
+    uint32_t moff = o;
+    if( v0 ) p[o++] = 0x80u;
+    p[o++] = (uint8_t)nsig; p[o++] = (uint8_t)(rnd() % nsig); p[o++] = (uint8_t)(rnd() % (nx + 1u));
+    o += cu16( p + o, nacct );
+    for( uint32_t j=0; j<nsig; j++ ) { memcpy( p + o, pub + 32UL*(ns + j), 32 ); o += 32u; }
+    for( uint32_t j=0; j<32u*nx + 32u; j++ ) p[o++] = (uint8_t)rnd();          /* other accounts + blockhash */
+    p[o++] = 1u;                                                               /* one instruction */
+    p[o++] = (uint8_t)(1u + rnd() % (nacct - 1u));
+    p[o++] = 2u; p[o++] = 0u; p[o++] = (uint8_t)(nacct - 1u);
+    o += cu16( p + o, dlen );
+    for( uint32_t j=0; j<dlen; j++ ) p[o++] = (uint8_t)rnd();
+    if( v0 ) p[o++] = 0u;                                                      /* no lookup tables */
+    txn_off[t] = (uint32_t)at; txn_sz[t] = o;
+    for( uint32_t j=0; j<nsig; j++ ) { sig_msg_off[ns + j] = (uint32_t)(at + moff); sig_msg_sz[ns + j] = o - moff; }
+    at += o; ns += nsig;
+  }
+  return ns;
+}
+
 } /* extern "C" */

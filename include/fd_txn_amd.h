@@ -147,6 +147,58 @@ fd_ed25519_amd_verify_txns( fd_ed25519_amd_t * eng,
                             uint *             sig_base,
                             schar *            sig_err );
 
+/* Device-resident form (inputs already in HBM, caller's stream, no sync).
+   Signature slots follow the same rule as fd_ed25519_amd_verify_txns:
+   d_tbase[t] (txn_cnt+1 entries, slot_cnt = d_tbase[txn_cnt]) is what
+   fd_ed25519_amd_txn_slots computes on the host.  d_sig_err (optional,
+   slot_cnt entries) receives the per-signature codes.  d_ws: at least
+   fd_ed25519_amd_txn_workspace_footprint(txn_cnt, slot_cnt) bytes,
+   256-aligned. */
+ulong
+fd_ed25519_amd_txn_workspace_footprint( ulong txn_cnt, ulong slot_cnt );
+
+ulong
+fd_ed25519_amd_txn_slots( ulong         txn_cnt,
+                          uchar const * payload,
+                          uint const *  txn_off,
+                          uint const *  txn_sz,
+                          uint *        tbase );
+
+int
+fd_ed25519_amd_verify_txns_dev( ulong         txn_cnt,
+                                ulong         slot_cnt,
+                                uchar const * d_payload,
+                                uint const *  d_txn_off,
+                                uint const *  d_txn_sz,
+                                uint const *  d_tbase,
+                                schar *       d_txn_err,
+                                schar *       d_sig_err,
+                                void *        d_ws,
+                                void *        stream );
+
+/* Workload synthesis (config 4): txn_cnt well-formed legacy / v0
+   transactions with nsig_lo..nsig_hi signers (account addresses = the
+   next public keys of pub[]) and ~msg_lo..msg_hi-byte messages, capped at
+   the MTU; signature fields zero.  Per signature: its message range in
+   payload (sig_msg_off, sig_msg_sz) and where its 64 bytes go (sig_at).
+   Returns the signature count, 0 if payload_cap / pub_cnt is too small. */
+ulong
+fd_ed25519_amd_synth_txns( ulong         seed,
+                           ulong         txn_cnt,
+                           uint          nsig_lo,
+                           uint          nsig_hi,
+                           uint          msg_lo,
+                           uint          msg_hi,
+                           uchar const * pub,
+                           ulong         pub_cnt,
+                           uchar *       payload,
+                           ulong         payload_cap,
+                           uint *        txn_off,
+                           uint *        txn_sz,
+                           uint *        sig_msg_off,
+                           uint *        sig_msg_sz,
+                           uint *        sig_at );
+
 #ifdef __cplusplus
 }
 #endif

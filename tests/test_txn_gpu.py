@@ -136,3 +136,31 @@ def test_verify_txns_empty_and_limits(engine):
     assert t.shape == (0,)
     with pytest.raises(ed25519.EngineError):
         engine.verify_txns(np.zeros(1300, np.uint8), np.zeros(1, np.uint32), np.full(1, 1233, np.uint32))
+
+
+def test_synth_txn_workload_and_device_path(engine):
+    """Config-4 workload (GPU-signed multi-signer transactions, 64..1232-B
+    messages): every transaction parses and verifies; the device-resident
+    entry point agrees with the host-staged one and with the oracle, also
+    after corruptions."""
+    from firedancer_amd import hip, workload
+    payload, toff, tsz, tbase = workload.txn_batch(3000, 77)
+    assert (tsz <= 1232).all() and int(tbase[-1]) > 2500
+    rng = np.random.default_rng(1)
+    bad = rng.choice(toff.size, 40, replace=False)
+    for t in bad[:20]:
+        payload[toff[t] + 1 + int(rng.integers(0, 64))] ^= 0x20         # a signature byte
+    for t in bad[20:]:
+        payload[toff[t] + tsz[t] - 1] ^= 0x01                           # last byte (data or LUT count)
+    dev = workload.TxnDevice(payload, toff, tsz, tbase)
+    st = hip.Stream()
+    dev.run(st.handle)
+    st.synchronize()
+    terr, serr = dev.verdicts()
+    eterr, ebase, eserr = _oracle.txn_verify_batch(payload, toff, tsz)
+    assert np.array_equal(ebase, tbase)
+    assert np.array_equal(terr, eterr) and np.array_equal(serr, eserr)
+    h_terr, h_base, h_serr = engine.verify_txns(payload, toff, tsz, want_sigs=True)
+    assert np.array_equal(h_terr, terr) and np.array_equal(h_serr, serr)
+    ok = np.setdiff1d(np.arange(toff.size), bad)
+    assert (terr[ok] == 0).all() and (terr[bad] != 0).all()
