@@ -26,6 +26,14 @@ import time
 
 import numpy as np
 
+# The streaming tile keeps 4 GPU batches in flight on 4 HIP streams; with
+# HIP's default of 4 hardware queues per process only 2 of them run
+# concurrently (measured, tools/dbg/dbg_conc.py), so give the process 8
+# (read at HIP runtime init, before any device call; well under the pool's
+# limit of 32).
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -61,6 +69,19 @@ def parse():
                     help="sigs: configs[1] (default bench line); txn: configs[3] multi-signer transactions")
     ap.add_argument("--stream-frags", type=int, default=1 << 18, help="frags per streaming-tile run")
     return ap.parse_args()
+
+
+def pmc_traffic(kernel, n):
+    """HBM bytes per launch of `kernel` at batch n, from the PMC summary
+    committed under profiles/ (tools/prof_pmc.sh + tools/pmc_summary.py on
+    the same build), scaled linearly from the profiled batch size."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_latest.json")
+    try:
+        d = json.load(open(path))
+        b = d[kernel]["derived"]["hbm_bytes_per_launch"]
+        return b * n / d.get("_sigs_per_launch", 262144)
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def make_workload(n, msg_sz, seed):
@@ -227,6 +248,7 @@ def main():
     live = float((st[0] > 0).sum())
     dsm_mac = MAC_MUL * (68 * live + 3 * I + 8 * nh + 7 * ns + 2 * live) + MAC_SQ * (4 * live + 4 * I)
     achieved = dsm_mac / (stage_ms[2] * 1e-3) / 1e12
+    traffic = pmc_traffic("k_dsm", n)
 
     if rank != 0:
         return
@@ -249,7 +271,9 @@ def main():
         "stage_ms": {"k_prep": stage_ms[0], "k_decomp": stage_ms[1], "k_dsm": stage_ms[2]},
         "verdicts": {"ok": int((err == 0).sum()), "rejected": int((err != 0).sum())},
         "roofline": {"bound": "valu-imad64", "kernel": "k_dsm", "achieved": achieved, "peak": PEAK_TMAC,
-                     "unit": "TMAC/s", "frac": achieved / PEAK_TMAC, "traffic": None,
+                     "unit": "TMAC/s", "frac": achieved / PEAK_TMAC, "traffic": traffic,
+                     "traffic_note": "HBM bytes per launch from the committed PMC pass (profiles/r01_pmc_latest.json: "
+                                     "2*FETCH_SIZE+WRITE_SIZE KB, gfx950 correction), scaled to this batch",
                      "mac_per_sig": dsm_mac / max(live, 1.0)},
         "workload_gen_s": gen_s,
     }

@@ -10,6 +10,7 @@ import os
 import sys
 
 d = sys.argv[1]
+n_sigs = int(sys.argv[2]) if len(sys.argv) > 2 else 262144   # the --sigs of the profiled bench run
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(os.path.join(d, "*", "p_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
@@ -31,5 +32,6 @@ for k, cs in agg.items():
     if "SQ_INSTS_VALU" in m and "SQ_WAVES" in m and m["SQ_WAVES"]:
         der["valu_insts_per_wave"] = m["SQ_INSTS_VALU"] / m["SQ_WAVES"]
     out[k] = {"counters": m, "derived": der}
+out["_sigs_per_launch"] = n_sigs
 json.dump(out, sys.stdout, indent=1, sort_keys=True)
 print()
