@@ -619,6 +619,63 @@ quad_p3( p3 & u, p1p1 const & t, u64 m1, u64 m2 ) {
   qgather( pm, u.Z, u.Y, u.X, u.T );
 }
 
+/* p1p1 -> p3 on a quad, keeping only this lane's product:
+   q0 u.Z, q1 u.Y, q2 u.X, q3 u.T */
+__device__ __forceinline__ fe
+quad_p3_own( p1p1 const & t, u64 m1, u64 m2 ) {
+  fe a, b;
+  _Pragma("unroll") for( int k=0; k<10; k++ ) {
+    a.v[k] = vsel( m2, t.X.v[k], t.Z.v[k] );
+    b.v[k] = vsel( m1, t.Y.v[k], t.T.v[k] );
+  }
+  return fe_mul( a, b );
+}
+
+/* DPP quad_perm with a per-destination source lane: lane q reads lane s_q */
+template<int S0, int S1, int S2, int S3>
+__device__ __forceinline__ i32 qp( i32 v ) {
+  return __builtin_amdgcn_mov_dpp( v, S0 | (S1 << 2) | (S2 << 4) | (S3 << 6), 0xf, 0xf, false );
+}
+
+/* op body + mix on a quad from the lanes' own p3 products (q0 Z, q1 Y,
+   q2 X, q3 T).  Two DPP reads give every lane the two coordinates its
+   operand needs:  P1 = quad_perm(2,2,2,0) -> X X X Z,
+                   P2 = quad_perm(1,1,0,3) -> Y Y Z T,
+   then   a = [X+Y, Y | Y-X, X | Z, Z | T]  (DBL | ADD)
+          b = DBL ? [X+Y, Y, X, 2Z] : qrow.
+   Per lane 32-bit masks (constant per step): k1 keeps P1, k2 keeps P2,
+   n1 negates P1 (q1 ADD), k3 doubles (q3 DBL). */
+__device__ __forceinline__ void
+quad_body_own( p1p1 & t, fe const & pm, fe const & qrow, bool isD, u64 mD, u64 mN, int qd ) {
+  i32 const ones = -1;
+  i32 k1 = (qd == 0 || (qd == 1 && !isD) || (qd >= 2 && isD)) ? ones : 0;
+  i32 k2 = (qd <= 1 || !isD) ? ones : 0;
+  i32 n1 = (qd == 1 && !isD) ? ones : 0;
+  i32 k3 = (qd == 3) ? ones : 0;
+  fe a, b;
+  _Pragma("unroll") for( int k=0; k<10; k++ ) {
+    i32 P1 = qp<2,2,2,0>( pm.v[k] ), P2 = qp<1,1,0,3>( pm.v[k] );
+    i32 av = (P2 & k2) + (((P1 & k1) ^ n1) - n1);
+    a.v[k] = av;
+    b.v[k] = vsel( mD, av + (av & k3), qrow.v[k] );
+  }
+  fe m = fe_mul( a, b );
+  fe M0, M1, M2, M3;
+  qgather( m, M0, M1, M2, M3 );
+  _Pragma("unroll") for( int k=0; k<10; k++ ) {
+    i32 A0 = M0.v[k], A1 = M1.v[k], A2 = M2.v[k], A3 = M3.v[k];
+    i32 z2 = A2 + A2;
+    i32 dY = A1 + A2, dZ = A1 - A2, dX = A0 - dY, dT = A3 - dZ;
+    i32 aX = A0 - A1,      aY = A0 + A1;
+    i32 zp = z2 + A3, zm = z2 - A3;
+    i32 aZ = vsel( mN, zm, zp ), aT = vsel( mN, zp, zm );
+    t.X.v[k] = vsel( mD, dX, aX );
+    t.Y.v[k] = vsel( mD, dY, aY );
+    t.Z.v[k] = vsel( mD, dZ, aZ );
+    t.T.v[k] = vsel( mD, dT, aT );
+  }
+}
+
 /* op body + mix on a quad.  qrow: this lane's table row (ADD); isD/neg per
    lane (uniform within the quad). */
 __device__ __forceinline__ void
@@ -738,17 +795,19 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
   t.X = fe_zero(); t.Y = fe_one(); t.Z = fe_one(); t.T = fe_one();
 
   for( ;; ) {
-    p3 u; quad_p3( u, t, m1, m2 );
+    fe pm = quad_p3_own( t, m1, m2 );       /* q0 u.Z, q1 u.Y, q2 u.X, q3 u.T */
 
     bool fin = (ph == PH_FIN);
     if( __any( fin ) ) {
-      /* q0: Z*RX, q1: Z*RY; lanes 2,3 compute a don't-care product */
-      fe xz = fe_mul( u.Z, qrow );
-      bool eq = true;
-      _Pragma("unroll") for( int k=0; k<8; k++ ) {
-        i32 ref = vsel( m1, u.Y.v[k], u.X.v[k] );
-        eq = eq && (xz.v[k] == ref);
+      /* q0: Z*RX vs X, q1: Z*RY vs Y; lanes 2,3 compute don't-care values */
+      fe Z, ref;
+      _Pragma("unroll") for( int k=0; k<10; k++ ) {
+        Z.v[k] = qb<0>( pm.v[k] );
+        ref.v[k] = qp<2,1,2,1>( pm.v[k] );  /* q0 <- X (lane 2), q1 <- Y (own) */
       }
+      fe xz = fe_mul( Z, qrow );
+      bool eq = true;
+      _Pragma("unroll") for( int k=0; k<8; k++ ) eq = eq && (xz.v[k] == ref.v[k]);
       int e01 = (int)eq;
       int both = qb<0>( e01 ) & qb<1>( e01 );
       if( fin ) {
@@ -760,7 +819,7 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
 
     bool isD = (ph == PH_DBL);
     u64 mD = __builtin_amdgcn_ballot_w64( isD ), mN = __builtin_amdgcn_ballot_w64( qneg );
-    quad_body( t, u, qrow, mD, mN, m1, m2 );
+    quad_body_own( t, pm, qrow, isD, mD, mN, qd );
 
     int da = (int)(i8)(cur & 0xff), db = (int)(i8)(cur >> 8);
     int nph;
