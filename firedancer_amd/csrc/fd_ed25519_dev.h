@@ -34,6 +34,13 @@ FD_DEV fe fe_one () { fe r = fe_zero(); r.v[0] = 1; return r; }
 FD_DEV i32 wmul( i32 a, i32 k ) { return (i32)((u32)a * (u32)k); }   /* int32 wrap: the low 32 bits the AVX mul sees */
 FD_DEV i64 mll ( i32 a, i32 b ) { return (i64)a * (i64)b; }            /* v_mad_i64_i32 */
 
+/* Column sums as explicit v_mad_i64_i32 chains.  fd_pin is an empty asm
+   (no instruction) that only makes its value opaque: LLVM can then neither
+   reassociate a chain nor move its accumulator input (a column bias, or a
+   carry) to a trailing 64-bit add. */
+FD_DEV i64 fd_pin( i64 x ) { asm( "" : "+v"(x) ); return x; }
+FD_DEV i64 mac( i32 a, i32 b, i64 c ) { return fd_pin( (i64)a * (i64)b + c ); }
+
 FD_DEV fe fe_add( fe const & f, fe const & g ) { fe h; _Pragma("unroll") for( int i=0; i<10; i++ ) h.v[i] = (i32)((u32)f.v[i] + (u32)g.v[i]); return h; }
 FD_DEV fe fe_sub( fe const & f, fe const & g ) { fe h; _Pragma("unroll") for( int i=0; i<10; i++ ) h.v[i] = (i32)((u32)f.v[i] - (u32)g.v[i]); return h; }
 FD_DEV fe fe_neg( fe const & f )               { fe h; _Pragma("unroll") for( int i=0; i<10; i++ ) h.v[i] = (i32)(0u - (u32)f.v[i]); return h; }
@@ -120,26 +127,16 @@ FD_DEV fe fe_mul( fe const & F, fe const & G ) {
   i32 g7_19 = wmul( g[7], 19 ), g8_19 = wmul( g[8], 19 ), g9_19 = wmul( g[9], 19 );
   i32 f1_2 = wmul( f[1], 2 ), f3_2 = wmul( f[3], 2 ), f5_2 = wmul( f[5], 2 );
   i32 f7_2 = wmul( f[7], 2 ), f9_2 = wmul( f[9], 2 );
-  i64 h0 = FD_B26 + mll(f[0],g[0]) + mll(f1_2,g9_19) + mll(f[2],g8_19) + mll(f3_2,g7_19) + mll(f[4],g6_19)
-         + mll(f5_2,g5_19) + mll(f[6],g4_19) + mll(f7_2,g3_19) + mll(f[8],g2_19) + mll(f9_2,g1_19);
-  i64 h1 = FD_B25 + mll(f[0],g[1]) + mll(f[1],g[0]) + mll(f[2],g9_19) + mll(f[3],g8_19) + mll(f[4],g7_19)
-         + mll(f[5],g6_19) + mll(f[6],g5_19) + mll(f[7],g4_19) + mll(f[8],g3_19) + mll(f[9],g2_19);
-  i64 h2 = FD_B26 + mll(f[0],g[2]) + mll(f1_2,g[1]) + mll(f[2],g[0]) + mll(f3_2,g9_19) + mll(f[4],g8_19)
-         + mll(f5_2,g7_19) + mll(f[6],g6_19) + mll(f7_2,g5_19) + mll(f[8],g4_19) + mll(f9_2,g3_19);
-  i64 h3 = FD_B25 + mll(f[0],g[3]) + mll(f[1],g[2]) + mll(f[2],g[1]) + mll(f[3],g[0]) + mll(f[4],g9_19)
-         + mll(f[5],g8_19) + mll(f[6],g7_19) + mll(f[7],g6_19) + mll(f[8],g5_19) + mll(f[9],g4_19);
-  i64 h4 = FD_B26 + mll(f[0],g[4]) + mll(f1_2,g[3]) + mll(f[2],g[2]) + mll(f3_2,g[1]) + mll(f[4],g[0])
-         + mll(f5_2,g9_19) + mll(f[6],g8_19) + mll(f7_2,g7_19) + mll(f[8],g6_19) + mll(f9_2,g5_19);
-  i64 h5 = FD_B25 + mll(f[0],g[5]) + mll(f[1],g[4]) + mll(f[2],g[3]) + mll(f[3],g[2]) + mll(f[4],g[1])
-         + mll(f[5],g[0]) + mll(f[6],g9_19) + mll(f[7],g8_19) + mll(f[8],g7_19) + mll(f[9],g6_19);
-  i64 h6 = FD_B26 + mll(f[0],g[6]) + mll(f1_2,g[5]) + mll(f[2],g[4]) + mll(f3_2,g[3]) + mll(f[4],g[2])
-         + mll(f5_2,g[1]) + mll(f[6],g[0]) + mll(f7_2,g9_19) + mll(f[8],g8_19) + mll(f9_2,g7_19);
-  i64 h7 = FD_B25 + mll(f[0],g[7]) + mll(f[1],g[6]) + mll(f[2],g[5]) + mll(f[3],g[4]) + mll(f[4],g[3])
-         + mll(f[5],g[2]) + mll(f[6],g[1]) + mll(f[7],g[0]) + mll(f[8],g9_19) + mll(f[9],g8_19);
-  i64 h8 = FD_B26 + mll(f[0],g[8]) + mll(f1_2,g[7]) + mll(f[2],g[6]) + mll(f3_2,g[5]) + mll(f[4],g[4])
-         + mll(f5_2,g[3]) + mll(f[6],g[2]) + mll(f7_2,g[1]) + mll(f[8],g[0]) + mll(f9_2,g9_19);
-  i64 h9 = FD_B25 + mll(f[0],g[9]) + mll(f[1],g[8]) + mll(f[2],g[7]) + mll(f[3],g[6]) + mll(f[4],g[5])
-         + mll(f[5],g[4]) + mll(f[6],g[3]) + mll(f[7],g[2]) + mll(f[8],g[1]) + mll(f[9],g[0]);
+  i64 h0 = FD_B26 + mll(f[0],g[0]) + mll(f1_2,g9_19) + mll(f[2],g8_19) + mll(f3_2,g7_19) + mll(f[4],g6_19) + mll(f5_2,g5_19) + mll(f[6],g4_19) + mll(f7_2,g3_19) + mll(f[8],g2_19) + mll(f9_2,g1_19);
+  i64 h1 = FD_B25 + mll(f[0],g[1]) + mll(f[1],g[0]) + mll(f[2],g9_19) + mll(f[3],g8_19) + mll(f[4],g7_19) + mll(f[5],g6_19) + mll(f[6],g5_19) + mll(f[7],g4_19) + mll(f[8],g3_19) + mll(f[9],g2_19);
+  i64 h2 = FD_B26 + mll(f[0],g[2]) + mll(f1_2,g[1]) + mll(f[2],g[0]) + mll(f3_2,g9_19) + mll(f[4],g8_19) + mll(f5_2,g7_19) + mll(f[6],g6_19) + mll(f7_2,g5_19) + mll(f[8],g4_19) + mll(f9_2,g3_19);
+  i64 h3 = FD_B25 + mll(f[0],g[3]) + mll(f[1],g[2]) + mll(f[2],g[1]) + mll(f[3],g[0]) + mll(f[4],g9_19) + mll(f[5],g8_19) + mll(f[6],g7_19) + mll(f[7],g6_19) + mll(f[8],g5_19) + mll(f[9],g4_19);
+  i64 h4 = FD_B26 + mll(f[0],g[4]) + mll(f1_2,g[3]) + mll(f[2],g[2]) + mll(f3_2,g[1]) + mll(f[4],g[0]) + mll(f5_2,g9_19) + mll(f[6],g8_19) + mll(f7_2,g7_19) + mll(f[8],g6_19) + mll(f9_2,g5_19);
+  i64 h5 = FD_B25 + mll(f[0],g[5]) + mll(f[1],g[4]) + mll(f[2],g[3]) + mll(f[3],g[2]) + mll(f[4],g[1]) + mll(f[5],g[0]) + mll(f[6],g9_19) + mll(f[7],g8_19) + mll(f[8],g7_19) + mll(f[9],g6_19);
+  i64 h6 = FD_B26 + mll(f[0],g[6]) + mll(f1_2,g[5]) + mll(f[2],g[4]) + mll(f3_2,g[3]) + mll(f[4],g[2]) + mll(f5_2,g[1]) + mll(f[6],g[0]) + mll(f7_2,g9_19) + mll(f[8],g8_19) + mll(f9_2,g7_19);
+  i64 h7 = FD_B25 + mll(f[0],g[7]) + mll(f[1],g[6]) + mll(f[2],g[5]) + mll(f[3],g[4]) + mll(f[4],g[3]) + mll(f[5],g[2]) + mll(f[6],g[1]) + mll(f[7],g[0]) + mll(f[8],g9_19) + mll(f[9],g8_19);
+  i64 h8 = FD_B26 + mll(f[0],g[8]) + mll(f1_2,g[7]) + mll(f[2],g[6]) + mll(f3_2,g[5]) + mll(f[4],g[4]) + mll(f5_2,g[3]) + mll(f[6],g[2]) + mll(f7_2,g[1]) + mll(f[8],g[0]) + mll(f9_2,g9_19);
+  i64 h9 = FD_B25 + mll(f[0],g[9]) + mll(f[1],g[8]) + mll(f[2],g[7]) + mll(f[3],g[6]) + mll(f[4],g[5]) + mll(f[5],g[4]) + mll(f[6],g[3]) + mll(f[7],g[2]) + mll(f[8],g[1]) + mll(f[9],g[0]);
   return fe_carry_b( h0, h1, h2, h3, h4, h5, h6, h7, h8, h9 );
 }
 
@@ -153,16 +150,16 @@ FD_DEV fe fe_sqn( fe const & F ) {
   i32 f4_2 = wmul( f[4], 2 ), f5_2 = wmul( f[5], 2 ), f6_2 = wmul( f[6], 2 ), f7_2 = wmul( f[7], 2 );
   i32 f5_38 = wmul( f[5], 38 ), f6_19 = wmul( f[6], 19 ), f7_38 = wmul( f[7], 38 );
   i32 f8_19 = wmul( f[8], 19 ), f9_38 = wmul( f[9], 38 );
-  i64 h0 = (N==1 ? FD_B26 : 0L) + mll(f[0],f[0]) + mll(f1_2,f9_38) + mll(f2_2,f8_19) + mll(f3_2,f7_38) + mll(f4_2,f6_19) + mll(f[5],f5_38);
-  i64 h1 = (N==1 ? FD_B25 : 0L) + mll(f0_2,f[1]) + mll(f[2],f9_38) + mll(f3_2,f8_19) + mll(f[4],f7_38) + mll(f5_2,f6_19);
-  i64 h2 = (N==1 ? FD_B26 : 0L) + mll(f0_2,f[2]) + mll(f1_2,f[1]) + mll(f3_2,f9_38) + mll(f4_2,f8_19) + mll(f5_2,f7_38) + mll(f[6],f6_19);
-  i64 h3 = (N==1 ? FD_B25 : 0L) + mll(f0_2,f[3]) + mll(f1_2,f[2]) + mll(f[4],f9_38) + mll(f5_2,f8_19) + mll(f[6],f7_38);
-  i64 h4 = (N==1 ? FD_B26 : 0L) + mll(f0_2,f[4]) + mll(f1_2,f3_2) + mll(f[2],f[2]) + mll(f5_2,f9_38) + mll(f6_2,f8_19) + mll(f[7],f7_38);
-  i64 h5 = (N==1 ? FD_B25 : 0L) + mll(f0_2,f[5]) + mll(f1_2,f[4]) + mll(f2_2,f[3]) + mll(f[6],f9_38) + mll(f7_2,f8_19);
-  i64 h6 = (N==1 ? FD_B26 : 0L) + mll(f0_2,f[6]) + mll(f1_2,f5_2) + mll(f2_2,f[4]) + mll(f3_2,f[3]) + mll(f7_2,f9_38) + mll(f[8],f8_19);
-  i64 h7 = (N==1 ? FD_B25 : 0L) + mll(f0_2,f[7]) + mll(f1_2,f[6]) + mll(f2_2,f[5]) + mll(f3_2,f[4]) + mll(f[8],f9_38);
-  i64 h8 = (N==1 ? FD_B26 : 0L) + mll(f0_2,f[8]) + mll(f1_2,f7_2) + mll(f2_2,f[6]) + mll(f3_2,f5_2) + mll(f[4],f[4]) + mll(f[9],f9_38);
-  i64 h9 = (N==1 ? FD_B25 : 0L) + mll(f0_2,f[9]) + mll(f1_2,f[8]) + mll(f2_2,f[7]) + mll(f3_2,f[6]) + mll(f4_2,f[5]);
+  i64 h0 = mac( f[5], f5_38, mac( f4_2, f6_19, mac( f3_2, f7_38, mac( f2_2, f8_19, mac( f1_2, f9_38, mac( f[0], f[0], (N==1 ? FD_B26 : 0L) ) ) ) ) ) );
+  i64 h1 = mac( f5_2, f6_19, mac( f[4], f7_38, mac( f3_2, f8_19, mac( f[2], f9_38, mac( f0_2, f[1], (N==1 ? FD_B25 : 0L) ) ) ) ) );
+  i64 h2 = mac( f[6], f6_19, mac( f5_2, f7_38, mac( f4_2, f8_19, mac( f3_2, f9_38, mac( f1_2, f[1], mac( f0_2, f[2], (N==1 ? FD_B26 : 0L) ) ) ) ) ) );
+  i64 h3 = mac( f[6], f7_38, mac( f5_2, f8_19, mac( f[4], f9_38, mac( f1_2, f[2], mac( f0_2, f[3], (N==1 ? FD_B25 : 0L) ) ) ) ) );
+  i64 h4 = mac( f[7], f7_38, mac( f6_2, f8_19, mac( f5_2, f9_38, mac( f[2], f[2], mac( f1_2, f3_2, mac( f0_2, f[4], (N==1 ? FD_B26 : 0L) ) ) ) ) ) );
+  i64 h5 = mac( f7_2, f8_19, mac( f[6], f9_38, mac( f2_2, f[3], mac( f1_2, f[4], mac( f0_2, f[5], (N==1 ? FD_B25 : 0L) ) ) ) ) );
+  i64 h6 = mac( f[8], f8_19, mac( f7_2, f9_38, mac( f3_2, f[3], mac( f2_2, f[4], mac( f1_2, f5_2, mac( f0_2, f[6], (N==1 ? FD_B26 : 0L) ) ) ) ) ) );
+  i64 h7 = mac( f[8], f9_38, mac( f3_2, f[4], mac( f2_2, f[5], mac( f1_2, f[6], mac( f0_2, f[7], (N==1 ? FD_B25 : 0L) ) ) ) ) );
+  i64 h8 = mac( f[9], f9_38, mac( f[4], f[4], mac( f3_2, f5_2, mac( f2_2, f[6], mac( f1_2, f7_2, mac( f0_2, f[8], (N==1 ? FD_B26 : 0L) ) ) ) ) ) );
+  i64 h9 = mac( f4_2, f[5], mac( f3_2, f[6], mac( f2_2, f[7], mac( f1_2, f[8], mac( f0_2, f[9], (N==1 ? FD_B25 : 0L) ) ) ) ) );
   if( N==2 ) {
     h0 += h0; h1 += h1; h2 += h2; h3 += h3; h4 += h4; h5 += h5; h6 += h6; h7 += h7; h8 += h8; h9 += h9;
     return fe_carry( h0, h1, h2, h3, h4, h5, h6, h7, h8, h9 );
