@@ -102,6 +102,35 @@ FD_DEV fe fe_carry_b( i64 h0, i64 h1, i64 h2, i64 h3, i64 h4, i64 h5, i64 h6, i6
   return r;
 }
 
+/* Carry-folded chain (used where MAC chains are pinned, fd_pin): the
+   rounding carry out of columns 0,2,4,6,8 is the accumulator INPUT of the
+   chains of columns 1,3,5,7,9, so five 64-bit adds vanish.  Even columns
+   start from K = 2^25 + 2^50: their own rounding bias plus the next odd
+   column's 2^24 pre-shifted by 26 ((h + 2^50) >> 26 == (h >> 26) + 2^24,
+   low 26 bits untouched); odd columns carry no bias of their own.  This
+   finishes the chain once columns 1..9 hold their carries-in.  Same limbs
+   as fe_carry / fe_carry_b. */
+FD_DEV fe fe_carry_fold_out( i64 h0, i64 h1, i64 h2, i64 h3, i64 h4, i64 h5, i64 h6, i64 h7, i64 h8, i64 h9 ) {
+  i64 const M26 = (1L<<26) - 1;
+  i64 t4 = (h4 & M26) + (h3 >> 25);
+  i32 c4b = (i32)(t4 >> 26);
+  i64 t0 = (h0 & M26) + (h9 >> 25) * 19;
+  i32 c0b = (i32)(t0 >> 26);
+  u32 const m26 = (1u<<26) - 1u, m25 = (1u<<25) - 1u;
+  fe r;
+  r.v[0] = (i32)((u32)t0 & m26) - (1<<25);
+  r.v[1] = (i32)((u32)h1 & m25) - (1<<24) + c0b;
+  r.v[2] = (i32)((u32)h2 & m26) - (1<<25);
+  r.v[3] = (i32)((u32)h3 & m25) - (1<<24);
+  r.v[4] = (i32)((u32)t4 & m26) - (1<<25);
+  r.v[5] = (i32)((u32)h5 & m25) - (1<<24) + c4b;
+  r.v[6] = (i32)((u32)h6 & m26) - (1<<25);
+  r.v[7] = (i32)((u32)h7 & m25) - (1<<24);
+  r.v[8] = (i32)((u32)h8 & m26) - (1<<25);
+  r.v[9] = (i32)((u32)h9 & m25) - (1<<24);
+  return r;
+}
+
 /* The column biases as OPAQUE wave-uniform values: LLVM canonicalises an
    integer constant to the end of an add chain, which would cost one extra
    64-bit add per column; an opaque SGPR value stays first and becomes the
@@ -167,7 +196,40 @@ FD_DEV fe fe_sqn( fe const & F ) {
   return fe_carry_b( h0, h1, h2, h3, h4, h5, h6, h7, h8, h9 );
 }
 
-FD_DEV fe fe_sq( fe const & f ) { return fe_sqn<1>( f ); }
+#ifndef FD_SQ_FOLD
+#define FD_SQ_FOLD 1
+#endif
+/* fe_sqn<1> with the carry fold (same limbs) */
+FD_DEV fe fe_sq_fold( fe const & F ) {
+  i32 const * f = F.v;
+  i64 const kb = fd_opaque( (1L<<25) + (1L<<50) );
+  i32 f0_2 = wmul( f[0], 2 ), f1_2 = wmul( f[1], 2 ), f2_2 = wmul( f[2], 2 ), f3_2 = wmul( f[3], 2 );
+  i32 f4_2 = wmul( f[4], 2 ), f5_2 = wmul( f[5], 2 ), f6_2 = wmul( f[6], 2 ), f7_2 = wmul( f[7], 2 );
+  i32 f5_38 = wmul( f[5], 38 ), f6_19 = wmul( f[6], 19 ), f7_38 = wmul( f[7], 38 );
+  i32 f8_19 = wmul( f[8], 19 ), f9_38 = wmul( f[9], 38 );
+  i64 h0 = mac( f[5], f5_38, mac( f4_2, f6_19, mac( f3_2, f7_38, mac( f2_2, f8_19, mac( f1_2, f9_38, mac( f[0], f[0], kb ) ) ) ) ) );
+  i64 h4 = mac( f[7], f7_38, mac( f6_2, f8_19, mac( f5_2, f9_38, mac( f[2], f[2], mac( f1_2, f3_2, mac( f0_2, f[4], kb ) ) ) ) ) );
+  i64 h2 = mac( f[6], f6_19, mac( f5_2, f7_38, mac( f4_2, f8_19, mac( f3_2, f9_38, mac( f1_2, f[1], mac( f0_2, f[2], kb ) ) ) ) ) );
+  i64 h6 = mac( f[8], f8_19, mac( f7_2, f9_38, mac( f3_2, f[3], mac( f2_2, f[4], mac( f1_2, f5_2, mac( f0_2, f[6], kb ) ) ) ) ) );
+  i64 h8 = mac( f[9], f9_38, mac( f[4], f[4], mac( f3_2, f5_2, mac( f2_2, f[6], mac( f1_2, f7_2, mac( f0_2, f[8], kb ) ) ) ) ) );
+  i64 h1 = mac( f5_2, f6_19, mac( f[4], f7_38, mac( f3_2, f8_19, mac( f[2], f9_38, mac( f0_2, f[1], h0 >> 26 ) ) ) ) );
+  i64 h5 = mac( f7_2, f8_19, mac( f[6], f9_38, mac( f2_2, f[3], mac( f1_2, f[4], mac( f0_2, f[5], h4 >> 26 ) ) ) ) );
+  h2 += h1 >> 25;
+  h6 += h5 >> 25;
+  i64 h3 = mac( f[6], f7_38, mac( f5_2, f8_19, mac( f[4], f9_38, mac( f1_2, f[2], mac( f0_2, f[3], h2 >> 26 ) ) ) ) );
+  i64 h7 = mac( f[8], f9_38, mac( f3_2, f[4], mac( f2_2, f[5], mac( f1_2, f[6], mac( f0_2, f[7], h6 >> 26 ) ) ) ) );
+  h8 += h7 >> 25;
+  i64 h9 = mac( f4_2, f[5], mac( f3_2, f[6], mac( f2_2, f[7], mac( f1_2, f[8], mac( f0_2, f[9], h8 >> 26 ) ) ) ) );
+  return fe_carry_fold_out( h0, h1, h2, h3, h4, h5, h6, h7, h8, h9 );
+}
+
+FD_DEV fe fe_sq( fe const & f ) {
+#if FD_SQ_FOLD
+  return fe_sq_fold( f );
+#else
+  return fe_sqn<1>( f );
+#endif
+}
 
 FD_DEV fe fe_sq_iter( fe h, int n ) {
   _Pragma("unroll 1")
