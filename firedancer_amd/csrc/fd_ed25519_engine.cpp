@@ -473,5 +473,5 @@ fd_ed25519_strerror( int err ) {
 
 extern "C" char const *
 fd_ed25519_amd_version( void ) {
-  return "fd_ed25519_amd 0.1 (gfx950; k_prep/k_decomp/k_dsm, one signature per lane)";
+  return "fd_ed25519_amd 0.2 (gfx950; k_prep/k_decomp/k_dsm + k_dsm4, txn front end, verify tile, GPU signer)";
 }

@@ -230,3 +230,28 @@ def test_both_kernels_stats_and_false_rejects(dsm_kernel):
     exp, st = _oracle.verify_batch(b, stats=True)
     assert np.array_equal(err.to_array(np.int8, n), exp)
     assert np.array_equal(stats.to_array(np.uint32, 3 * n).reshape(3, n).T, st)
+
+
+def test_config2_full_size_properties():
+    """configs[1] at full size: 2^20 GPU-signed 200-B signatures through the
+    device path.  Every signature is valid, so every rejection must be an
+    AVX limb-compare false reject (rate ~1.6e-6) confirmed by the oracle;
+    resubmission is idempotent."""
+    from firedancer_amd import ed25519, hip, workload
+    n = 1 << 20
+    pub, sig, off, sz, blob = workload.sig_batch(n, 200, 20240)
+    d = {k: hip.DeviceBuffer.from_array(v) for k, v in dict(pub=pub, sig=sig, off=off, sz=sz, blob=blob).items()}
+    err = hip.DeviceBuffer(n)
+    ws = hip.DeviceBuffer(ed25519.workspace_footprint(n))
+    st = hip.Stream()
+    outs = []
+    for _ in range(2):
+        ed25519.verify_dev(n, d["pub"].ptr, d["sig"].ptr, d["off"].ptr, d["sz"].ptr, d["blob"].ptr, err.ptr,
+                           ws.ptr, st.handle)
+        st.synchronize()
+        outs.append(err.to_array(np.int8, n))
+    assert np.array_equal(outs[0], outs[1])
+    rej = np.nonzero(outs[0])[0]
+    assert rej.size <= 12, rej.size
+    for i in rej:
+        assert _oracle.verify(bytes(blob[off[i]:off[i] + 200]), bytes(sig[i]), bytes(pub[i])) == int(outs[0][i]) == -3
