@@ -43,6 +43,8 @@ slot_free( slot_t * s ) {
   if( s->h_off  ) (void)hipHostFree( s->h_off );
   if( s->h_sz   ) (void)hipHostFree( s->h_sz );
   if( s->h_err  ) (void)hipHostFree( s->h_err );
+  if( s->d_pack ) (void)hipFree( s->d_pack );
+  if( s->h_pack ) (void)hipHostFree( s->h_pack );
   if( s->d_toff ) (void)hipFree( s->d_toff );
   if( s->d_tsz  ) (void)hipFree( s->d_tsz );
   if( s->d_fp   ) (void)hipFree( s->d_fp );
@@ -76,6 +78,8 @@ slot_alloc( slot_t * s, ulong cap, ulong blob_cap ) {
   HIPCHK( hipHostMalloc( (void **)&s->h_off,  4UL*cap, hipHostMallocDefault ) );
   HIPCHK( hipHostMalloc( (void **)&s->h_sz,   4UL*cap, hipHostMallocDefault ) );
   HIPCHK( hipHostMalloc( (void **)&s->h_err,  cap, hipHostMallocDefault ) );
+  HIPCHK( hipMalloc( (void **)&s->d_pack, 104UL*cap + blob_cap + 64UL ) );
+  HIPCHK( hipHostMalloc( (void **)&s->h_pack, 104UL*cap + blob_cap + 64UL, hipHostMallocDefault ) );
   HIPCHK( hipStreamCreateWithFlags( &s->stream, hipStreamNonBlocking ) );
   HIPCHK( hipEventCreateWithFlags( &s->done, hipEventDisableTiming ) );
   return FD_ED25519_AMD_OK;
@@ -167,6 +171,19 @@ fd_amd_slot_launch( slot_t * s, ulong n, ulong blob_sz, schar * out, int want_ta
 }
 
 int
+fd_amd_slot_launch_packed( slot_t * s, ulong n, ulong blob_sz, schar * out ) {
+  uint8_t * d = s->d_pack;
+  HIPCHK( hipMemcpyAsync( d, s->h_pack, 104UL*n + blob_sz, hipMemcpyHostToDevice, s->stream ) );
+  if( fd_amd_launch_verify( (uint32_t)n, d, d + 32UL*n, (uint32_t *)(d + 96UL*n), (uint32_t *)(d + 100UL*n),
+                            d + 104UL*n, s->d_err, s->d_ws, s->stream, 1, NULL ) )
+    return FD_ED25519_AMD_ERR_DEVICE;
+  HIPCHK( hipMemcpyAsync( s->h_err, s->d_err, n, hipMemcpyDeviceToHost, s->stream ) );
+  HIPCHK( hipEventRecord( s->done, s->stream ) );
+  s->out = out; s->n = n; s->busy = 1; s->want_tag = 0;
+  return FD_ED25519_AMD_OK;
+}
+
+int
 fd_amd_slot_ready( slot_t * s ) {
   if( !s->busy ) return 1;
   hipError_t e = hipEventQuery( s->done );
@@ -212,19 +229,29 @@ run_chunked( fd_ed25519_amd_t * e, ulong n, schar * err, GET get ) {
   while( i < n ) {
     slot_t * s = &e->slot[k];
     if( (rc = fd_amd_slot_drain( s )) ) return rc;
+    /* size the chunk first, then stage it packed: [pub|sig|off|sz|blob] */
     ulong c = 0, bsz = 0;
     while( i + c < n && c < e->cap ) {
       uint8_t const * msg; ulong sz; uint8_t const * sig; uint8_t const * pub;
       get( i + c, &msg, &sz, &sig, &pub );
       if( sz > e->blob_cap ) return FD_ED25519_AMD_ERR_INVAL;   /* cannot be staged in one chunk */
       if( bsz + sz > e->blob_cap ) break;
-      memcpy( s->h_pub + 32UL*c, pub, 32 );
-      memcpy( s->h_sig + 64UL*c, sig, 64 );
-      if( sz ) memcpy( s->h_blob + bsz, msg, sz );
-      s->h_off[c] = (uint32_t)bsz; s->h_sz[c] = (uint32_t)sz;
       bsz += sz; c++;
     }
-    if( (rc = fd_amd_slot_launch( s, c, bsz, err + i, 0 )) ) return rc;
+    uint8_t * hp = s->h_pack;
+    uint8_t * h_pub = hp, * h_sig = hp + 32UL*c, * h_blob = hp + 104UL*c;
+    uint32_t * h_off = (uint32_t *)(hp + 96UL*c), * h_sz = (uint32_t *)(hp + 100UL*c);
+    bsz = 0;
+    for( ulong j=0; j<c; j++ ) {
+      uint8_t const * msg; ulong sz; uint8_t const * sig; uint8_t const * pub;
+      get( i + j, &msg, &sz, &sig, &pub );
+      memcpy( h_pub + 32UL*j, pub, 32 );
+      memcpy( h_sig + 64UL*j, sig, 64 );
+      if( sz ) memcpy( h_blob + bsz, msg, sz );
+      h_off[j] = (uint32_t)bsz; h_sz[j] = (uint32_t)sz;
+      bsz += sz;
+    }
+    if( (rc = fd_amd_slot_launch_packed( s, c, bsz, err + i )) ) return rc;
     i += c; k ^= 1;
   }
   for( int j=0; j<2; j++ ) if( (rc = fd_amd_slot_drain( &e->slot[j] )) ) return rc;

@@ -29,6 +29,8 @@
  *                              10 limbs padded to 12: per-lane contiguous (one ADD gathers
  *                              192 contiguous bytes instead of 40 scattered dwords)
  *   st   : uint32 [3][N]       work statistics (iterations, nnz h, nnz s)
+ *   ds   : uint8  [N][2]       decompression status of A / R (0 ok, 1 not on the
+ *                              curve); k_dsm turns a failure into -2
  *   tag  : uint64 [N]          dedup tag: the first 8 bytes (little endian) of
  *                              SHA-512(R||A||M), 0 when the s check rejected
  *                              (app/frank/README.md:107-110: verify yields a
@@ -59,6 +61,7 @@ fd_amd_ws_layout( size_t n ) {
   L.Ai  = o; o = ws_al( o + 4UL*384UL*N );
   L.st  = o; o = ws_al( o + 4UL*3UL*N );
   L.tag = o; o = ws_al( o + 8UL*N );
+  L.ds  = o; o = ws_al( o + 2UL*N );
   L.total = o;
   return L;
 }
@@ -110,12 +113,11 @@ slide_reg( u32 const a[8], EMIT emit ) {
   }
 }
 
-__global__ void __launch_bounds__(64)
-k_prep( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
-        u32 const * __restrict__ msg_off, u32 const * __restrict__ msg_sz,
-        u8 const * __restrict__ blob, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L,
-        i8 const * __restrict__ skip ) {
-  u32 i = blockIdx.x * 64u + threadIdx.x;
+__device__ __forceinline__ void
+prep_body( u32 i, u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
+           u32 const * __restrict__ msg_off, u32 const * __restrict__ msg_sz,
+           u8 const * __restrict__ blob, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L,
+           i8 const * __restrict__ skip ) {
   if( i >= n ) return;
   if( skip && skip[i] ) {   /* slot of a transaction that failed to parse (fd_txn_kernels.hip) */
     ((int *)(ws + L.top))[i] = -1;
@@ -196,19 +198,31 @@ k_prep( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
   err[i] = (i8)code;
 }
 
+__global__ void __launch_bounds__(64)
+k_prep( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
+        u32 const * __restrict__ msg_off, u32 const * __restrict__ msg_sz,
+        u8 const * __restrict__ blob, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L,
+        i8 const * __restrict__ skip ) {
+  prep_body( blockIdx.x * 64u + threadIdx.x, n, pub, sig, msg_off, msg_sz, blob, err, ws, L, skip );
+}
+
 /* ------------------------------------------------------------------ */
 /* k_decomp: lane 2i -> A = pub[i], lane 2i+1 -> R = sig[i][0:32]       */
 
 #ifndef FD_DECOMP_WAVES
 #define FD_DECOMP_WAVES 2
 #endif
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FD_DECOMP_WAVES)))
-k_decomp( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
-          i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L ) {
-  u32 t = blockIdx.x * 64u + threadIdx.x;
+/* one point per lane: t = 2i (A = pub[i]) or 2i+1 (R = sig[i][0:32]).
+   Independent of k_prep (reads no verdict) when `gate` is 0, so the two
+   can run concurrently (k_front); with gate, signatures k_prep already
+   decided are skipped. */
+__device__ __forceinline__ void
+decomp_body( u32 t, u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
+             i8 const * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, bool gate ) {
   u32 i = t >> 1; u32 which = t & 1u;
   if( i >= n ) return;
-  if( err[i] != 1 ) return;
+  if( gate && err[i] != 1 ) return;
+  u8 * ds = ws + L.ds;
   u8 const * src = which ? (sig + 64UL*i) : (pub + 32UL*i);
   u32 w[8];
   _Pragma("unroll") for( int k=0; k<8; k++ )
@@ -230,7 +244,7 @@ k_decomp( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
   fe chk = fe_sub( vxx, u );
   if( fe_isnonzero( chk ) ) {
     chk = fe_add( vxx, u );
-    if( fe_isnonzero( chk ) ) { err[i] = (i8)-2; return; }
+    if( fe_isnonzero( chk ) ) { ds[2u*i + which] = 1u; return; }
     x = fe_mul( x, SQRTM1 );
   }
   if( fe_isnegative( x ) != (int)(w[7] >> 31) ) x = fe_neg( x );
@@ -252,6 +266,26 @@ k_decomp( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
       R[(size_t)(10+k)*N + i] = Y.v[k];
     }
   }
+  ds[2u*i + which] = 0u;
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FD_DECOMP_WAVES)))
+k_decomp( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
+          i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L ) {
+  decomp_body( blockIdx.x * 64u + threadIdx.x, n, pub, sig, err, ws, L, true );
+}
+
+/* k_front: k_prep and k_decomp as ONE launch, blocks [0, nbp) hashing and
+   blocks [nbp, 3 nbp) decompressing, concurrently (latency path: a small
+   batch does not fill the GPU, so the two stages overlap instead of
+   queueing). */
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FD_DECOMP_WAVES)))
+k_front( u32 n, u32 nbp, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
+         u32 const * __restrict__ msg_off, u32 const * __restrict__ msg_sz,
+         u8 const * __restrict__ blob, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L,
+         i8 const * __restrict__ skip ) {
+  if( blockIdx.x < nbp ) prep_body( blockIdx.x * 64u + threadIdx.x, n, pub, sig, msg_off, msg_sz, blob, err, ws, L, skip );
+  else                   decomp_body( (blockIdx.x - nbp) * 64u + threadIdx.x, n, pub, sig, err, ws, L, false );
 }
 
 /* ------------------------------------------------------------------ */
@@ -386,6 +420,7 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
 
   u32 i = blockIdx.x * 64u + threadIdx.x;
   bool act = (i < n) && (err[i] == 1);
+  if( act && (ws[L.ds + 2u*i] | ws[L.ds + 2u*i + 1u]) ) { err[i] = (i8)-2; act = false; }   /* A or R undecodable */
   size_t N = L.N;
   u32 ii = (i < n) ? i : 0u;
   i32 * Ail = (i32 *)(ws + L.Ai) + (size_t)ii*384u;   /* this lane's 8 x 4 x 12 table */
@@ -736,6 +771,10 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
   u32 i = gt >> 2;
   int qd = (int)(threadIdx.x & 3u);
   bool act = (i < n) && (err[i] == 1);
+  if( act && (ws[L.ds + 2u*i] | ws[L.ds + 2u*i + 1u]) ) {            /* A or R undecodable */
+    act = false;
+    if( qd == 0 ) err[i] = (i8)-2;
+  }
   size_t N = L.N;
   u32 ii = (i < n) ? i : 0u;
   i32 * Ail = (i32 *)(ws + L.Ai) + (size_t)ii*384u;
@@ -887,15 +926,19 @@ fd_amd_launch_verify( u32 n, u8 const * d_pub, u8 const * d_sig, u32 const * d_o
   ws_layout_t L = fd_amd_ws_layout( n );
   u8 * ws = (u8 *)d_ws;
   u32 nb = (n + 63u) / 64u;
+  bool small = n <= fd_amd_dsm4_max();
   if( ev ) (void)hipEventRecord( ev[0], stream );
-  hipLaunchKernelGGL( k_prep,   dim3(nb),      dim3(64), 0, stream, n, d_pub, d_sig, d_off, d_sz, d_blob, d_err, ws, L, d_skip );
-  if( ev ) (void)hipEventRecord( ev[1], stream );
-  hipLaunchKernelGGL( k_decomp, dim3(2u*nb),   dim3(64), 0, stream, n, d_pub, d_sig, d_err, ws, L );
-  if( ev ) (void)hipEventRecord( ev[2], stream );
-  if( n <= fd_amd_dsm4_max() )   /* small batch: 4 lanes per signature, lower latency */
+  if( small ) {   /* latency path: one front launch (hash || decompress), then k_dsm4 */
+    hipLaunchKernelGGL( k_front, dim3(3u*nb), dim3(64), 0, stream, n, nb, d_pub, d_sig, d_off, d_sz, d_blob, d_err, ws, L, d_skip );
+    if( ev ) { (void)hipEventRecord( ev[1], stream ); (void)hipEventRecord( ev[2], stream ); }
     hipLaunchKernelGGL( k_dsm4, dim3((n + 15u)/16u), dim3(64), 0, stream, n, d_err, ws, L, want_stats );
-  else
-    hipLaunchKernelGGL( k_dsm,  dim3(nb),            dim3(64), 0, stream, n, d_err, ws, L, want_stats );
+  } else {
+    hipLaunchKernelGGL( k_prep,   dim3(nb),    dim3(64), 0, stream, n, d_pub, d_sig, d_off, d_sz, d_blob, d_err, ws, L, d_skip );
+    if( ev ) (void)hipEventRecord( ev[1], stream );
+    hipLaunchKernelGGL( k_decomp, dim3(2u*nb), dim3(64), 0, stream, n, d_pub, d_sig, d_err, ws, L );
+    if( ev ) (void)hipEventRecord( ev[2], stream );
+    hipLaunchKernelGGL( k_dsm,    dim3(nb),    dim3(64), 0, stream, n, d_err, ws, L, want_stats );
+  }
   if( ev ) (void)hipEventRecord( ev[3], stream );
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
