@@ -196,8 +196,8 @@ fd_amd_slot_ready( slot_t * s ) {
 /* Launch a staged transaction chunk: c transactions (payload bytes in
    h_blob, rebased offsets in h_toff/h_tsz, signature-slot bases in
    h_tbase[0..c]), nslot = h_tbase[c] signature slots. */
-static int
-slot_launch_txn( slot_t * s, ulong c, ulong nslot, ulong blob_sz, schar * t_out, schar * s_out ) {
+int
+fd_amd_slot_launch_txn( slot_t * s, ulong c, ulong nslot, ulong blob_sz, schar * t_out, schar * s_out, int want_tag ) {
   HIPCHK( hipMemcpyAsync( s->d_toff,  s->h_toff,  4UL*c,        hipMemcpyHostToDevice, s->stream ) );
   HIPCHK( hipMemcpyAsync( s->d_tsz,   s->h_tsz,   4UL*c,        hipMemcpyHostToDevice, s->stream ) );
   HIPCHK( hipMemcpyAsync( s->d_tbase, s->h_tbase, 4UL*(c+1UL),  hipMemcpyHostToDevice, s->stream ) );
@@ -212,6 +212,10 @@ slot_launch_txn( slot_t * s, ulong c, ulong nslot, ulong blob_sz, schar * t_out,
     return FD_ED25519_AMD_ERR_DEVICE;
   HIPCHK( hipMemcpyAsync( s->h_terr, s->d_terr, c, hipMemcpyDeviceToHost, s->stream ) );
   if( s_out && nslot ) HIPCHK( hipMemcpyAsync( s->h_err, s->d_err, nslot, hipMemcpyDeviceToHost, s->stream ) );
+  if( want_tag && nslot ) {
+    ws_layout_t L = fd_amd_ws_layout( nslot );
+    HIPCHK( hipMemcpyAsync( s->h_tag, (uint8_t *)s->d_ws + L.tag, 8UL*nslot, hipMemcpyDeviceToHost, s->stream ) );
+  }
   HIPCHK( hipEventRecord( s->done, s->stream ) );
   s->t_out = t_out; s->t_n = c;
   s->s_out = nslot ? s_out : NULL; s->s_n = nslot;
@@ -282,8 +286,8 @@ fd_ed25519_amd_verify_soa( fd_ed25519_amd_t * e, ulong n, uchar const * pub, uch
 /* Signature slots the engine reserves for a payload: its first byte when
    that is a plausible signature count (fd_txn_parse.c:79-82 accept it),
    else 0.  Exact for every payload that parses. */
-static inline ulong
-txn_slots( uchar const * p, ulong sz ) {
+ulong
+fd_amd_txn_slots1( uchar const * p, ulong sz ) {
   if( !sz ) return 0UL;
   ulong k = p[0];
   return ( k >= 1UL && k <= FD_TXN_SIG_MAX && 64UL*k <= sz - 1UL ) ? k : 0UL;
@@ -302,7 +306,7 @@ fd_ed25519_amd_verify_txns( fd_ed25519_amd_t * e, ulong txn_cnt, uchar const * p
   /* global signature numbering (the caller-visible sig_base) */
   uint acc = 0U;
   if( sig_base ) {
-    for( ulong t=0; t<txn_cnt; t++ ) { sig_base[t] = acc; acc += (uint)txn_slots( payload + txn_off[t], txn_sz[t] ); }
+    for( ulong t=0; t<txn_cnt; t++ ) { sig_base[t] = acc; acc += (uint)fd_amd_txn_slots1( payload + txn_off[t], txn_sz[t] ); }
     sig_base[txn_cnt] = acc;
   }
   ulong t = 0, gsig = 0; int k = 0;
@@ -312,14 +316,14 @@ fd_ed25519_amd_verify_txns( fd_ed25519_amd_t * e, ulong txn_cnt, uchar const * p
     ulong c = 0, bsz = 0, ns = 0;
     while( t + c < txn_cnt && c < e->cap ) {
       uchar const * p = payload + txn_off[t+c];
-      ulong sz = txn_sz[t+c], k2 = txn_slots( p, sz );
+      ulong sz = txn_sz[t+c], k2 = fd_amd_txn_slots1( p, sz );
       if( bsz + sz > e->blob_cap || ns + k2 > e->cap ) break;
       if( sz ) memcpy( s->h_blob + bsz, p, sz );
       s->h_toff[c] = (uint32_t)bsz; s->h_tsz[c] = (uint32_t)sz; s->h_tbase[c] = (uint32_t)ns;
       bsz += sz; ns += k2; c++;
     }
     s->h_tbase[c] = (uint32_t)ns;
-    if( (rc = slot_launch_txn( s, c, ns, bsz, txn_err + t, sig_err ? sig_err + gsig : NULL )) ) return rc;
+    if( (rc = fd_amd_slot_launch_txn( s, c, ns, bsz, txn_err + t, sig_err ? sig_err + gsig : NULL, 0 )) ) return rc;
     t += c; gsig += ns; k ^= 1;
   }
   for( int j=0; j<2; j++ ) if( (rc = fd_amd_slot_drain( &e->slot[j] )) ) return rc;
@@ -355,7 +359,7 @@ extern "C" ulong
 fd_ed25519_amd_txn_slots( ulong txn_cnt, uchar const * payload, uint const * txn_off, uint const * txn_sz,
                           uint * tbase ) {
   ulong acc = 0;
-  for( ulong t=0; t<txn_cnt; t++ ) { tbase[t] = (uint)acc; acc += txn_slots( payload + txn_off[t], txn_sz[t] ); }
+  for( ulong t=0; t<txn_cnt; t++ ) { tbase[t] = (uint)acc; acc += fd_amd_txn_slots1( payload + txn_off[t], txn_sz[t] ); }
   tbase[txn_cnt] = (uint)acc;
   return acc;
 }

@@ -111,8 +111,17 @@ struct fd_verify_amd_tile {
   ulong              wait_ns;
   tcache_t           tc;
   int                nslot;
+  int                framing;   /* FD_VERIFY_AMD_FRAMING_* */
   std::vector<pending_t> meta[FD_AMD_SLOT_MAX];
 };
+
+extern "C" int
+fd_verify_amd_tile_set_framing( fd_verify_amd_tile_t * t, int framing ) {
+  if( !t || (framing != FD_VERIFY_AMD_FRAMING_PUB_SIG_MSG && framing != FD_VERIFY_AMD_FRAMING_TXN) )
+    return FD_ED25519_AMD_ERR_INVAL;
+  t->framing = framing;
+  return FD_ED25519_AMD_OK;
+}
 
 #define TILE_NSLOT (4)   /* batches in flight: one wave's verify takes ~0.7 ms, so small
                             batches need several in flight to keep the GPU busy */
@@ -131,6 +140,7 @@ fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong 
     if( fd_amd_slot_alloc_aux( &eng->slot[k], batch_max ) ) { fd_ed25519_amd_delete( eng ); return NULL; }
   fd_verify_amd_tile_t * t = new fd_verify_amd_tile_t();
   t->eng = eng; t->batch_max = batch_max; t->wait_ns = batch_wait_ns; t->nslot = TILE_NSLOT;
+  t->framing = FD_VERIFY_AMD_FRAMING_PUB_SIG_MSG;
   t->tc.init( tcache_depth );
   for( int k=0; k<TILE_NSLOT; k++ ) t->meta[k].resize( batch_max );
   return t;
@@ -157,21 +167,26 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
   int   K = t->nslot;
   int   stage = 0;                 /* slot being filled; slots are used round robin, so the */
   int   oldest = 0, nfly = 0;      /* in-flight ones are oldest, oldest+1, ... (mod K)      */
-  ulong staged = 0, blob_at = 0, stage_t0 = 0;
+  ulong staged = 0, blob_at = 0, stage_t0 = 0, slots = 0;
   int   rc;
 
+  bool txn = t->framing == FD_VERIFY_AMD_FRAMING_TXN;
   auto publish = [&]( int k ) -> int {
     slot_t * s = &e->slot[k];
     if( (rc = fd_amd_slot_drain( s )) ) return rc;
-    for( ulong i=0; i<s->n; i++ ) {
+    ulong cnt = txn ? s->t_n : s->n;
+    for( ulong i=0; i<cnt; i++ ) {
       pending_t const & m = t->meta[k][i];
-      if( s->h_err[i] ) { diag->sv_filt_cnt++; diag->sv_filt_sz += m.sz; continue; }
+      int bad = txn ? s->h_terr[i] : s->h_err[i];
+      if( bad ) { diag->sv_filt_cnt++; diag->sv_filt_sz += m.sz; continue; }
+      /* dedup tag: the verify's SHA-512 tag of the (first) signature */
+      ulong tag = txn ? s->h_tag[ s->h_tbase[i] ] : s->h_tag[i];
       if( out_fseq && out_seq - __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) >= out_depth ) {
         diag->backp_cnt++;         /* credit check against the slowest consumer */
         while( out_seq - __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) >= out_depth ) { /* spin */ }
       }
       uint tspub = fd_verify_amd_tickcount();
-      fd_mcache_publish( out_mcache, out_depth, out_seq, s->h_tag[i], m.chunk, m.sz, m.ctl, m.tsorig, tspub );
+      fd_mcache_publish( out_mcache, out_depth, out_seq, tag, m.chunk, m.sz, m.ctl, m.tsorig, tspub );
       if( lat && lat_n < lat_max ) lat[lat_n++] = tspub - m.tsorig;
       out_seq++; diag->out_cnt++; diag->out_sz += m.sz;
     }
@@ -194,7 +209,7 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
 
     /* 2. stage input frags into the free slot */
     slot_t * s = &e->slot[stage];
-    bool idle_in = false;
+    bool idle_in = false, full = false;
     while( !done_in && staged < t->batch_max ) {
       if( frag_cnt && diag->in_cnt >= frag_cnt ) break;
       fd_frag_meta_t const * m = in_mcache + (in_seq & (in_depth-1UL));
@@ -208,17 +223,36 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
       uchar const * p = (uchar const *)fd_chunk_to_laddr_const( in_chunk0, chunk );
       in_seq++;
       __atomic_store_n( &diag->in_cnt, diag->in_cnt + 1UL, __ATOMIC_RELEASE );
-      if( sz < 96UL || sz - 96UL > FD_ED25519_AMD_MSG_MAX ) { diag->bad_frag_cnt++; continue; }
-      ulong ha_tag; memcpy( &ha_tag, p + 32, 8 );                        /* first 8 signature bytes */
-      if( t->tc.insert( ha_tag ) ) { diag->ha_filt_cnt++; diag->ha_filt_sz += sz; continue; }
-      ulong msz = sz - 96UL;                                             /* blob_cap = batch_max*MSG_MAX: fits */
-      memcpy( s->h_pub + 32UL*staged, p,      32 );
-      memcpy( s->h_sig + 64UL*staged, p + 32, 64 );
-      memcpy( s->h_blob + blob_at,    p + 96, msz );
-      s->h_off[staged] = (uint32_t)blob_at; s->h_sz[staged] = (uint32_t)msz;
+      if( !txn ) {
+        if( sz < 96UL || sz - 96UL > FD_ED25519_AMD_MSG_MAX ) { diag->bad_frag_cnt++; continue; }
+        ulong ha_tag; memcpy( &ha_tag, p + 32, 8 );                      /* first 8 signature bytes */
+        if( t->tc.insert( ha_tag ) ) { diag->ha_filt_cnt++; diag->ha_filt_sz += sz; continue; }
+        ulong msz = sz - 96UL;                                           /* blob_cap = batch_max*MSG_MAX: fits */
+        memcpy( s->h_pub + 32UL*staged, p,      32 );
+        memcpy( s->h_sig + 64UL*staged, p + 32, 64 );
+        memcpy( s->h_blob + blob_at,    p + 96, msz );
+        s->h_off[staged] = (uint32_t)blob_at; s->h_sz[staged] = (uint32_t)msz;
+        blob_at += msz;
+      } else {
+        /* wire transaction (fd_txn.h layout): dedup on its first signature */
+        if( sz > FD_ED25519_AMD_MSG_MAX ) { diag->bad_frag_cnt++; continue; }
+        ulong k2 = fd_amd_txn_slots1( p, sz );
+        if( slots + k2 > t->batch_max ) {                              /* no room for its signatures: next batch */
+          in_seq--; __atomic_store_n( &diag->in_cnt, diag->in_cnt - 1UL, __ATOMIC_RELEASE );
+          full = true;
+          break;
+        }
+        if( k2 ) {
+          ulong ha_tag; memcpy( &ha_tag, p + 1, 8 );
+          if( t->tc.insert( ha_tag ) ) { diag->ha_filt_cnt++; diag->ha_filt_sz += sz; continue; }
+        }
+        memcpy( s->h_blob + blob_at, p, sz );
+        s->h_toff[staged] = (uint32_t)blob_at; s->h_tsz[staged] = (uint32_t)sz; s->h_tbase[staged] = (uint32_t)slots;
+        blob_at += sz; slots += k2;
+      }
       t->meta[stage][staged] = pending_t{ (uint)chunk, (ushort)sz, (ushort)ctl, (uint)tsorig };
       if( !staged ) stage_t0 = now_ns();
-      blob_at += msz; staged++;
+      staged++;
     }
     done_in = frag_cnt ? (diag->in_cnt >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
 
@@ -229,12 +263,19 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
           batch_wait_ns.  A nonzero batch_wait_ns turns the greedy rule off
           while another batch is in flight. */
     bool greedy = idle_in && (!t->wait_ns || !nfly);
-    if( staged && ( staged == t->batch_max || greedy || done_in ||
+    if( staged && ( staged == t->batch_max || full || greedy || done_in ||
                     (t->wait_ns && now_ns() - stage_t0 >= t->wait_ns) ) ) {
-      if( (rc = fd_amd_slot_launch( s, staged, blob_at, NULL, 1 )) ) return rc;
-      diag->batch_cnt++; diag->batch_sig_cnt += staged;
+      if( txn ) {
+        s->h_tbase[staged] = (uint32_t)slots;
+        if( (rc = fd_amd_slot_launch_txn( s, staged, slots, blob_at, NULL, NULL, 1 )) ) return rc;
+        diag->batch_sig_cnt += slots;
+      } else {
+        if( (rc = fd_amd_slot_launch( s, staged, blob_at, NULL, 1 )) ) return rc;
+        diag->batch_sig_cnt += staged;
+      }
+      diag->batch_cnt++;
       nfly++;
-      stage = (stage + 1) % K; staged = 0; blob_at = 0;
+      stage = (stage + 1) % K; staged = 0; blob_at = 0; slots = 0;
     }
   }
   return FD_ED25519_AMD_OK;

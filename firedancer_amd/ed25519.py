@@ -80,6 +80,8 @@ def lib():
     L.fd_ed25519_amd_set_small_batch_max.restype = None
     L.fd_verify_amd_tile_new.argtypes = [i, ul, ul, ul]
     L.fd_verify_amd_tile_new.restype = vp
+    L.fd_verify_amd_tile_set_framing.argtypes = [vp, i]
+    L.fd_verify_amd_tile_set_framing.restype = i
     L.fd_verify_amd_tile_delete.argtypes = [vp]
     L.fd_verify_amd_tile_delete.restype = None
     L.fd_verify_amd_tile_run.argtypes = [vp, vp, ul, vp, ul, vp, ul, ul, vp, ul, vp, vp, vp, ul]

@@ -56,11 +56,16 @@ def tickcount():
 class VerifyTile:
     """fd_verify_amd_tile_t: adaptive-batching GPU verify tile."""
 
-    def __init__(self, device=0, batch_max=4096, batch_wait_ns=0, tcache_depth=1 << 16):
+    FRAMING_PUB_SIG_MSG = 0
+    FRAMING_TXN = 1
+
+    def __init__(self, device=0, batch_max=4096, batch_wait_ns=0, tcache_depth=1 << 16, framing=0):
         self._h = ed25519.lib().fd_verify_amd_tile_new(int(device), int(batch_max), int(batch_wait_ns),
                                                       int(tcache_depth))
         if not self._h:
             raise ed25519.EngineError("fd_verify_amd_tile_new failed (no HIP device?)")
+        if ed25519.lib().fd_verify_amd_tile_set_framing(self._h, int(framing)):
+            raise ed25519.EngineError("bad framing %r" % framing)
 
     def close(self):
         if self._h:

@@ -118,6 +118,19 @@ fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong 
 void
 fd_verify_amd_tile_delete( fd_verify_amd_tile_t * tile );
 
+/* Frag framing.  PUB_SIG_MSG (default): public_key(32) | signature(64) |
+   message, one signature per frag (fd_frank_verify_synth_load.c:340-347).
+   TXN: the frag is a wire-format Solana transaction (fd_txn.h); the tile
+   parses it on the GPU (fd_txn_parse semantics), verifies every signature
+   against its account address (multi-signer) and publishes the transaction
+   iff it parses and all its signatures pass; HA dedup uses its first
+   signature, the published tag is that signature's SHA-512 tag.  A frag
+   that fails to parse counts as SV_FILT. */
+#define FD_VERIFY_AMD_FRAMING_PUB_SIG_MSG (0)
+#define FD_VERIFY_AMD_FRAMING_TXN         (1)
+int
+fd_verify_amd_tile_set_framing( fd_verify_amd_tile_t * tile, int framing );
+
 /* Run the tile until `frag_cnt` input frags were consumed (0: until
    *stop != 0) and every accepted frag is published.  Input: in_mcache
    (depth in_depth, power of 2), in_chunk0 = local address of chunk 0 of

@@ -133,3 +133,63 @@ def test_stream_bench_smoke():
     assert r["frags_per_s"] > 0 and 0 < r["p50_ns"] <= r["p99_ns"]
     r = tango.bench_stream(0, 256, 0, pub, sig, off, sz, blob, 5000, rate=50000.0)
     assert r["published"] == 5000 and r["p50_ns"] > 0
+
+
+def test_tile_txn_framing_vs_oracle():
+    """Frags carrying wire transactions (multi-signer, legacy + v0, some
+    corrupted, some duplicated): the tile publishes exactly the
+    transactions the oracle accepts (fd_txn_parse + every signature), in
+    order, tagged with the first signature's SHA-512 tag; drops count as
+    SV_FILT / HA_FILT."""
+    import hashlib
+    import _txn
+    from firedancer_amd import tango
+    rng = np.random.default_rng(8)
+    pays, nsig = _txn.build_txns(44, 200, nsig_hi=6)
+    pays = [bytearray(p) for p in pays]
+    for t in rng.choice(len(pays), 30, replace=False):
+        pays[t][1 + int(rng.integers(0, 64))] ^= 0x08                      # a signature byte
+    for t in rng.choice(len(pays), 10, replace=False):
+        pays[t][1 + 64 * pays[t][0]] ^= 0x40                              # header -> parse failure
+    pays = [bytes(p) for p in pays]
+    order = list(range(len(pays))) + [3, 7, 11]                            # three HA duplicates
+    depth = 1024
+    mtu_chunks = ((1232 + 127) >> 7) << 1
+    dcache = tango._aligned(64 * mtu_chunks * (len(order) + 2))
+    mc_in, mc_out = tango.mcache_new(depth), tango.mcache_new(depth)
+    chunk = 0
+    chunks = []
+    for seq, k in enumerate(order):
+        p = pays[k]
+        dcache[64 * chunk:64 * chunk + len(p)] = np.frombuffer(p, np.uint8)
+        tango.publish(mc_in, seq, 0, chunk, len(p), 3, seq, 0)
+        chunks.append(chunk)
+        chunk += mtu_chunks
+    blob, off, sz = _txn.pack(pays)
+    eterr, _, _ = _oracle.txn_verify_batch(blob, off, sz)
+    tile = tango.VerifyTile(0, batch_max=64, tcache_depth=4096, framing=tango.VerifyTile.FRAMING_TXN)
+    try:
+        diag, _ = tile.run(mc_in, dcache, 0, mc_out, 0, len(order))
+    finally:
+        tile.close()
+    seen, exp = set(), []
+    ha = sv = 0
+    for seq, k in enumerate(order):
+        p = pays[k]
+        tag = int.from_bytes(p[1:9], "little") if 1 <= p[0] <= 127 and 64 * p[0] <= len(p) - 1 else 0
+        if tag:
+            if tag in seen:
+                ha += 1
+                continue
+            seen.add(tag)
+        if eterr[k]:
+            sv += 1
+            continue
+        m = 1 + 64 * p[0]
+        h = hashlib.sha512(p[1:33] + p[m + (1 if p[m] & 0x80 else 0) + 4: m + (1 if p[m] & 0x80 else 0) + 36] +
+                           p[m:]).digest()
+        exp.append((seq, int.from_bytes(h[:8], "little")))
+    assert diag["ha_filt_cnt"] == ha == 3 and diag["sv_filt_cnt"] == sv and diag["out_cnt"] == len(exp)
+    for o, (seq_in, tag) in enumerate(exp):
+        assert int(mc_out[o]["chunk"]) == chunks[seq_in] and int(mc_out[o]["tsorig"]) == seq_in
+        assert int(mc_out[o]["sig"]) == tag
