@@ -468,21 +468,29 @@ fd_ed25519_amd_debug_digits_dev( ulong n, void const * d_ws, ushort * d_dig, int
 extern "C" int
 fd_ed25519_verify( void const * msg, ulong sz, void const * sig, void const * public_key, fd_sha512_t * sha ) {
   (void)sha;   /* scratch of the reference; hashing happens on the GPU */
+  /* one engine per calling thread (the reference is reentrant with one
+     fd_sha512_t per thread, fd_frank_verify.c:121-123); it grows when a
+     message exceeds its staging (the reference accepts any size) */
   static thread_local fd_ed25519_amd_t * eng = NULL;
-  if( !eng ) {
+  static thread_local ulong eng_blob = 0;
+  if( sz > 0xFFFFFFFFUL - 4096UL ) {
+    fprintf( stderr, "fd_ed25519_verify: message of %lu bytes exceeds the engine's 32-bit offsets\n", sz );
+    abort();
+  }
+  if( !eng || sz > eng_blob ) {
+    ulong want = 64UL*FD_ED25519_AMD_MSG_MAX;
+    while( want < sz ) want <<= 1;
+    if( eng ) fd_ed25519_amd_delete( eng );
     char const * d = getenv( "FD_ED25519_AMD_DEVICE" );
-    eng = fd_ed25519_amd_new( d ? atoi( d ) : 0, 64UL, 64UL*FD_ED25519_AMD_MSG_MAX );
+    eng = fd_ed25519_amd_new( d ? atoi( d ) : 0, 64UL, want );
     if( !eng ) {
       fprintf( stderr, "fd_ed25519_verify: no usable MI355X/HIP device; this library has no CPU path\n" );
       abort();
     }
+    eng_blob = want;
   }
   static uint8_t const zero = 0;
   uint32_t off = 0, s32 = (uint32_t)sz;
-  if( sz > 64UL*FD_ED25519_AMD_MSG_MAX ) {
-    fprintf( stderr, "fd_ed25519_verify: message of %lu bytes exceeds the engine limit\n", sz );
-    abort();
-  }
   schar err = 0;
   int rc = fd_ed25519_amd_verify_soa( eng, 1UL, (uchar const *)public_key, (uchar const *)sig, &off, &s32,
                                       sz ? (uchar const *)msg : &zero, sz, &err );

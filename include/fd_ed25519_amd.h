@@ -94,10 +94,12 @@ fd_ed25519_sign( void *        sig,
 /* ===== Part 2: batch engine (new) ===== */
 
 #define FD_ED25519_AMD_OK          ( 0)
-#define FD_ED25519_AMD_ERR_INVAL   (-10) /* bad argument (NULL, n too large, msg too large) */
+#define FD_ED25519_AMD_ERR_INVAL   (-10) /* bad argument (NULL, n too large, a message larger than the engine's blob_max) */
 #define FD_ED25519_AMD_ERR_DEVICE  (-11) /* HIP error / no device */
 
-/* Largest message accepted per signature (Solana MTU). */
+/* Solana MTU: the message size the staging is dimensioned
+   for.  Longer messages verify too, as long as each fits the engine's
+   blob_max (the drop-in fd_ed25519_verify grows its engine as needed). */
 #define FD_ED25519_AMD_MSG_MAX     (1232UL)
 
 typedef struct fd_ed25519_amd fd_ed25519_amd_t;

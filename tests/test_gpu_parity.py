@@ -255,3 +255,18 @@ def test_config2_full_size_properties():
     assert rej.size <= 12, rej.size
     for i in rej:
         assert _oracle.verify(bytes(blob[off[i]:off[i] + 200]), bytes(sig[i]), bytes(pub[i])) == int(outs[0][i]) == -3
+
+
+def test_dropin_long_messages():
+    """The reference verifies messages of any size; the drop-in entry point
+    grows its staging (64 KB .. 1 MB messages, valid and corrupted)."""
+    from firedancer_amd import ed25519
+    rng = np.random.default_rng(12)
+    for sz in (70000, 200001, 1 << 20):
+        prv = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+        msg = bytes(rng.integers(0, 256, sz, dtype=np.uint8))
+        pub = ed25519.public_from_private(prv)
+        sig = ed25519.sign(msg, pub, prv)
+        assert ed25519.verify(msg, sig, pub) == 0 == _oracle.verify(msg, sig, pub)
+        bad = bytearray(msg); bad[sz // 2] ^= 1
+        assert ed25519.verify(bytes(bad), sig, pub) == _oracle.verify(bytes(bad), sig, pub) == -3
