@@ -298,19 +298,26 @@ def main():
         m = min(n, 1 << 16)
         rows = []
         for bmax in (256, 1024, 4096, 16384):
-            sat = tango.bench_stream(local, bmax, 0, pub[:m], sig[:m], off[:m], sz[:m], blob, args.stream_frags)
-            row = {"batch_max": bmax, "saturated_frags_per_s": sat["frags_per_s"],
-                   "saturated_mean_batch": sat["mean_batch"]}
-            for load in (0.5, 0.8):
-                rate = load * sat["frags_per_s"]
-                nf = int(min(args.stream_frags, max(20000, rate * 1.0)))
-                r = tango.bench_stream(local, bmax, 0, pub[:m], sig[:m], off[:m], sz[:m], blob, nf, rate=rate)
-                row["at_%d%%" % int(load * 100)] = {"offered_frags_per_s": rate, "frags_per_s": r["frags_per_s"],
-                                                     "p50_us": r["p50_ns"] / 1e3, "p99_us": r["p99_ns"] / 1e3,
-                                                     "mean_batch": r["mean_batch"]}
+            row = {"batch_max": bmax}
+            for zc in (False, True):
+                key = "zero_copy" if zc else "copy"
+                sat = tango.bench_stream(local, bmax, 0, pub[:m], sig[:m], off[:m], sz[:m], blob, args.stream_frags,
+                                         zero_copy=zc)
+                rr = {"saturated_frags_per_s": sat["frags_per_s"], "saturated_mean_batch": sat["mean_batch"]}
+                for load in (0.5, 0.8):
+                    rate = load * sat["frags_per_s"]
+                    nf = int(min(args.stream_frags, max(20000, rate * 1.0)))
+                    r = tango.bench_stream(local, bmax, 0, pub[:m], sig[:m], off[:m], sz[:m], blob, nf, rate=rate,
+                                           zero_copy=zc)
+                    rr["at_%d%%" % int(load * 100)] = {"offered_frags_per_s": rate, "frags_per_s": r["frags_per_s"],
+                                                        "p50_us": r["p50_ns"] / 1e3, "p99_us": r["p99_ns"] / 1e3,
+                                                        "mean_batch": r["mean_batch"]}
+                row[key] = rr
             rows.append(row)
-        out["stream_tile"] = {"path": "producer -> in mcache/dcache -> verify tile (adaptive GPU batches, 4 in "
-                                      "flight) -> out mcache -> consumer; latency = scheduled send to tile publish",
+        out["stream_tile"] = {"path": "producer (metadata only; frames pre-placed in the data region as a NIC would) "
+                                      "-> in mcache/dcache -> verify tile (adaptive GPU batches, 4 in flight; copy: "
+                                      "host staging, zero_copy: GPU-mapped data region) -> out mcache -> consumer; "
+                                      "latency = scheduled send to tile publish",
                               "frags_per_run": args.stream_frags, "rows": rows}
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(pub, sig, off, sz, blob, args.cpu_sample, args.cpu_threads, err,

@@ -158,7 +158,8 @@ fd_amd_slot_launch( slot_t * s, ulong n, ulong blob_sz, schar * out, int want_ta
   HIPCHK( hipMemcpyAsync( s->d_off,  s->h_off,  4UL*n,  hipMemcpyHostToDevice, s->stream ) );
   HIPCHK( hipMemcpyAsync( s->d_sz,   s->h_sz,   4UL*n,  hipMemcpyHostToDevice, s->stream ) );
   if( blob_sz ) HIPCHK( hipMemcpyAsync( s->d_blob, s->h_blob, blob_sz, hipMemcpyHostToDevice, s->stream ) );
-  if( fd_amd_launch_verify( (uint32_t)n, s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_blob, s->d_err, s->d_ws, s->stream, 1, NULL ) )
+  if( fd_amd_launch_verify( (uint32_t)n, s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_blob, s->d_err, s->d_ws, s->stream, 1, NULL,
+                            NULL, s->dsm_mode ) )
     return FD_ED25519_AMD_ERR_DEVICE;
   HIPCHK( hipMemcpyAsync( s->h_err, s->d_err, n, hipMemcpyDeviceToHost, s->stream ) );
   if( want_tag ) {
@@ -167,6 +168,24 @@ fd_amd_slot_launch( slot_t * s, ulong n, ulong blob_sz, schar * out, int want_ta
   }
   HIPCHK( hipEventRecord( s->done, s->stream ) );
   s->out = out; s->n = n; s->busy = 1; s->want_tag = want_tag;
+  return FD_ED25519_AMD_OK;
+}
+
+int
+fd_amd_slot_launch_zc( slot_t * s, ulong n, uint8_t const * d_dc ) {
+  /* h_off / h_sz hold chunk / frag size; the SoA planes are built on the GPU */
+  HIPCHK( hipMemcpyAsync( s->d_toff, s->h_off, 4UL*n, hipMemcpyHostToDevice, s->stream ) );
+  HIPCHK( hipMemcpyAsync( s->d_tsz,  s->h_sz,  4UL*n, hipMemcpyHostToDevice, s->stream ) );
+  if( fd_amd_launch_zgather( (uint32_t)n, s->d_toff, s->d_tsz, d_dc, s->d_pub, s->d_sig, s->d_off, s->d_sz, s->stream ) )
+    return FD_ED25519_AMD_ERR_DEVICE;
+  if( fd_amd_launch_verify( (uint32_t)n, s->d_pub, s->d_sig, s->d_off, s->d_sz, d_dc, s->d_err, s->d_ws, s->stream, 1, NULL,
+                            NULL, s->dsm_mode ) )
+    return FD_ED25519_AMD_ERR_DEVICE;
+  HIPCHK( hipMemcpyAsync( s->h_err, s->d_err, n, hipMemcpyDeviceToHost, s->stream ) );
+  ws_layout_t L = fd_amd_ws_layout( n );
+  HIPCHK( hipMemcpyAsync( s->h_tag, (uint8_t *)s->d_ws + L.tag, 8UL*n, hipMemcpyDeviceToHost, s->stream ) );
+  HIPCHK( hipEventRecord( s->done, s->stream ) );
+  s->out = NULL; s->n = n; s->busy = 1; s->want_tag = 1;
   return FD_ED25519_AMD_OK;
 }
 
@@ -206,7 +225,7 @@ fd_amd_slot_launch_txn( slot_t * s, ulong c, ulong nslot, ulong blob_sz, schar *
                                s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_skip, s->stream ) )
     return FD_ED25519_AMD_ERR_DEVICE;
   if( nslot && fd_amd_launch_verify( (uint32_t)nslot, s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_blob, s->d_err,
-                                     s->d_ws, s->stream, 0, NULL, s->d_skip ) )
+                                     s->d_ws, s->stream, 0, NULL, s->d_skip, s->dsm_mode ) )
     return FD_ED25519_AMD_ERR_DEVICE;
   if( fd_amd_launch_txn_reduce( (uint32_t)c, s->d_fp, s->d_tbase, s->d_err, s->d_terr, s->stream ) )
     return FD_ED25519_AMD_ERR_DEVICE;

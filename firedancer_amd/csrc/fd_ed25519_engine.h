@@ -20,6 +20,7 @@ struct slot_t {
   uint8_t  * d_pack; uint8_t * h_pack;   /* packed [pub|sig|off|sz|blob] for n: one H2D per chunk */
   uint64_t * h_tag;      /* dedup tags (pinned, allocated with the txn buffers) */
   int        want_tag;
+  int        dsm_mode;   /* kernel path for the next launch (fd_amd_launch_verify dsm_mode) */
   /* the chunk in flight: where its verdicts go */
   schar *    out;
   ulong      n;
@@ -55,6 +56,9 @@ fd_ed25519_amd_t * fd_amd_engine_new( int device, ulong batch_max, ulong blob_ma
    dedup tags in s->h_tag when want_tag) once s->done has fired; `out`
    (may be NULL) is where slot_drain copies the verdicts. */
 int  fd_amd_slot_launch( slot_t * s, ulong n, ulong blob_sz, schar * out, int want_tag );
+/* Zero-copy tile chunk: h_off[i] = chunk, h_sz[i] = frag size of frag i in
+   the GPU-mapped data region d_dc (pub|sig|msg framing); tags wanted. */
+int  fd_amd_slot_launch_zc( slot_t * s, ulong n, uint8_t const * d_dc );
 /* Same, inputs staged in s->h_pack as [pub 32n | sig 64n | off 4n | sz 4n | blob]. */
 int  fd_amd_slot_launch_packed( slot_t * s, ulong n, ulong blob_sz, schar * out );
 /* 1 if the slot's chunk finished (or nothing is in flight), 0 if still

@@ -22,7 +22,10 @@ ws_layout_t fd_amd_ws_layout( size_t n );
 int fd_amd_launch_verify( uint32_t n, uint8_t const * d_pub, uint8_t const * d_sig, uint32_t const * d_off,
                           uint32_t const * d_sz, uint8_t const * d_blob, int8_t * d_err, void * d_ws,
                           hipStream_t stream, int want_stats, hipEvent_t const * ev /* 4 or NULL */,
-                          int8_t const * d_skip = NULL );
+                          int8_t const * d_skip = NULL, int dsm_mode = 0 );
+/* dsm_mode: 0 = by batch size (fd_ed25519_amd_set_small_batch_max), 1 = the
+   throughput path (k_prep, k_decomp, k_dsm), 2 = the latency path
+   (k_front, k_dsm4). */
 
 /* Transaction front end (fd_txn_kernels.hip).
    k_txn_parse: one lane per transaction t = d_payload[d_toff[t] .. +d_tsz[t]).
@@ -45,5 +48,11 @@ int fd_amd_launch_txn_reduce( uint32_t txn_cnt, uint32_t const * d_fp, uint32_t 
    blob[off[i] .. +sz[i]) -> pub[n][32], sig[n][64].  0 on success. */
 int fd_amd_launch_sign( uint32_t n, uint8_t const * d_prv, uint32_t const * d_off, uint32_t const * d_sz,
                         uint8_t const * d_blob, uint8_t * d_pub, uint8_t * d_sig, hipStream_t stream );
+
+/* Zero-copy tile staging (k_zgather): frag i at d_dc + 64*d_chunk[i]
+   (host memory mapped into the GPU), d_fsz[i] bytes pub|sig|msg -> SoA
+   planes, msg_off relative to d_dc. */
+int fd_amd_launch_zgather( uint32_t n, uint32_t const * d_chunk, uint32_t const * d_fsz, uint8_t const * d_dc,
+                           uint8_t * d_pub, uint8_t * d_sig, uint32_t * d_off, uint32_t * d_sz, hipStream_t stream );
 
 #endif

@@ -907,6 +907,33 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
 }
 
 /* ------------------------------------------------------------------ */
+/* k_zgather: zero-copy staging for the streaming tile.  The tango data
+   region is host memory registered with the GPU (hipHostRegister); frag i
+   lives at chunk[i]*64 in it, framed public_key | signature | message.  Copy
+   the 96 header bytes into the SoA planes and point msg_off at the message
+   inside the mapped region, which k_prep then reads over PCIe in place. */
+__global__ void __launch_bounds__(64)
+k_zgather( u32 n, u32 const * __restrict__ chunk, u32 const * __restrict__ fsz, u8 const * __restrict__ dc,
+           u8 * __restrict__ pub, u8 * __restrict__ sig, u32 * __restrict__ moff, u32 * __restrict__ msz ) {
+  u32 i = blockIdx.x * 64u + threadIdx.x;
+  if( i >= n ) return;
+  uint4 const * src = (uint4 const *)(dc + ((size_t)chunk[i] << 6));    /* chunks are 64-aligned */
+  uint4 a0 = src[0], a1 = src[1], s0 = src[2], s1 = src[3], s2 = src[4], s3 = src[5];
+  uint4 * P = (uint4 *)(pub + 32UL*i); P[0] = a0; P[1] = a1;
+  uint4 * S = (uint4 *)(sig + 64UL*i); S[0] = s0; S[1] = s1; S[2] = s2; S[3] = s3;
+  moff[i] = (chunk[i] << 6) + 96u;
+  msz[i]  = fsz[i] - 96u;
+}
+
+int
+fd_amd_launch_zgather( uint32_t n, uint32_t const * d_chunk, uint32_t const * d_fsz, uint8_t const * d_dc,
+                       uint8_t * d_pub, uint8_t * d_sig, uint32_t * d_off, uint32_t * d_sz, hipStream_t stream ) {
+  if( !n ) return 0;
+  hipLaunchKernelGGL( k_zgather, dim3((n + 63u)/64u), dim3(64), 0, stream, n, d_chunk, d_fsz, d_dc, d_pub, d_sig, d_off, d_sz );
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+/* ------------------------------------------------------------------ */
 /* launch                                                               */
 
 /* Batches up to this size use k_dsm4 (fd_ed25519_amd_set_small_batch_max). */
@@ -921,12 +948,12 @@ fd_ed25519_amd_set_small_batch_max( unsigned long n ) {
 int
 fd_amd_launch_verify( u32 n, u8 const * d_pub, u8 const * d_sig, u32 const * d_off, u32 const * d_sz,
                       u8 const * d_blob, i8 * d_err, void * d_ws, hipStream_t stream, int want_stats,
-                      hipEvent_t const * ev, i8 const * d_skip ) {
+                      hipEvent_t const * ev, i8 const * d_skip, int dsm_mode ) {
   if( !n ) return 0;
   ws_layout_t L = fd_amd_ws_layout( n );
   u8 * ws = (u8 *)d_ws;
   u32 nb = (n + 63u) / 64u;
-  bool small = n <= fd_amd_dsm4_max();
+  bool small = dsm_mode == 2 || (dsm_mode == 0 && n <= fd_amd_dsm4_max());
   if( ev ) (void)hipEventRecord( ev[0], stream );
   if( small ) {   /* latency path: one front launch (hash || decompress), then k_dsm4 */
     hipLaunchKernelGGL( k_front, dim3(3u*nb), dim3(64), 0, stream, n, nb, d_pub, d_sig, d_off, d_sz, d_blob, d_err, ws, L, d_skip );

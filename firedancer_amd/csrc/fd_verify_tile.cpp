@@ -112,8 +112,26 @@ struct fd_verify_amd_tile {
   tcache_t           tc;
   int                nslot;
   int                framing;   /* FD_VERIFY_AMD_FRAMING_* */
+  uint8_t *          reg_base;  /* host data region mapped into the GPU (zero copy) */
+  ulong              reg_sz;
+  uint8_t *          reg_dev;
   std::vector<pending_t> meta[FD_AMD_SLOT_MAX];
 };
+
+extern "C" int
+fd_verify_amd_tile_register_dcache( fd_verify_amd_tile_t * t, void * base, ulong sz ) {
+  if( !t || !base || !sz ) return FD_ED25519_AMD_ERR_INVAL;
+  if( hipSetDevice( t->eng->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  uintptr_t lo = (uintptr_t)base & ~(uintptr_t)4095, hi = ((uintptr_t)base + sz + 4095) & ~(uintptr_t)4095;
+  if( hipHostRegister( (void *)lo, hi - lo, hipHostRegisterMapped ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  void * dev = NULL;
+  if( hipHostGetDevicePointer( &dev, (void *)lo, 0 ) != hipSuccess ) {
+    (void)hipHostUnregister( (void *)lo );
+    return FD_ED25519_AMD_ERR_DEVICE;
+  }
+  t->reg_base = (uint8_t *)lo; t->reg_sz = hi - lo; t->reg_dev = (uint8_t *)dev;
+  return FD_ED25519_AMD_OK;
+}
 
 extern "C" int
 fd_verify_amd_tile_set_framing( fd_verify_amd_tile_t * t, int framing ) {
@@ -149,6 +167,7 @@ fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong 
 extern "C" void
 fd_verify_amd_tile_delete( fd_verify_amd_tile_t * t ) {
   if( !t ) return;
+  if( t->reg_base ) { (void)hipSetDevice( t->eng->device ); (void)hipHostUnregister( t->reg_base ); }
   fd_ed25519_amd_delete( t->eng );
   delete t;
 }
@@ -171,6 +190,13 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
   int   rc;
 
   bool txn = t->framing == FD_VERIFY_AMD_FRAMING_TXN;
+  /* zero copy: the input data region is mapped into the GPU; frags are
+     handed over as (chunk, size) and gathered on the device */
+  uint8_t const * zc_dev = NULL;
+  if( !txn && t->reg_base && (uint8_t const *)in_chunk0 >= t->reg_base &&
+      (uint8_t const *)in_chunk0 < t->reg_base + t->reg_sz &&
+      t->reg_sz - (ulong)((uint8_t const *)in_chunk0 - t->reg_base) <= (1UL << 32) )
+    zc_dev = t->reg_dev + ((uint8_t const *)in_chunk0 - t->reg_base);
   auto publish = [&]( int k ) -> int {
     slot_t * s = &e->slot[k];
     if( (rc = fd_amd_slot_drain( s )) ) return rc;
@@ -227,12 +253,16 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
         if( sz < 96UL || sz - 96UL > FD_ED25519_AMD_MSG_MAX ) { diag->bad_frag_cnt++; continue; }
         ulong ha_tag; memcpy( &ha_tag, p + 32, 8 );                      /* first 8 signature bytes */
         if( t->tc.insert( ha_tag ) ) { diag->ha_filt_cnt++; diag->ha_filt_sz += sz; continue; }
-        ulong msz = sz - 96UL;                                           /* blob_cap = batch_max*MSG_MAX: fits */
-        memcpy( s->h_pub + 32UL*staged, p,      32 );
-        memcpy( s->h_sig + 64UL*staged, p + 32, 64 );
-        memcpy( s->h_blob + blob_at,    p + 96, msz );
-        s->h_off[staged] = (uint32_t)blob_at; s->h_sz[staged] = (uint32_t)msz;
-        blob_at += msz;
+        if( zc_dev ) {                                                   /* zero copy: metadata only */
+          s->h_off[staged] = (uint32_t)chunk; s->h_sz[staged] = (uint32_t)sz;
+        } else {
+          ulong msz = sz - 96UL;                                         /* blob_cap = batch_max*MSG_MAX: fits */
+          memcpy( s->h_pub + 32UL*staged, p,      32 );
+          memcpy( s->h_sig + 64UL*staged, p + 32, 64 );
+          memcpy( s->h_blob + blob_at,    p + 96, msz );
+          s->h_off[staged] = (uint32_t)blob_at; s->h_sz[staged] = (uint32_t)msz;
+          blob_at += msz;
+        }
       } else {
         /* wire transaction (fd_txn.h layout): dedup on its first signature */
         if( sz > FD_ED25519_AMD_MSG_MAX ) { diag->bad_frag_cnt++; continue; }
@@ -265,10 +295,17 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
     bool greedy = idle_in && (!t->wait_ns || !nfly);
     if( staged && ( staged == t->batch_max || full || greedy || done_in ||
                     (t->wait_ns && now_ns() - stage_t0 >= t->wait_ns) ) ) {
+      /* kernel path by batch size (tile batches are small next to the GPU,
+         so even with 4 in flight the 4-lane latency kernels finish sooner:
+         measured, forcing the 1-lane kernels when busy halved throughput) */
+      s->dsm_mode = 0;
       if( txn ) {
         s->h_tbase[staged] = (uint32_t)slots;
         if( (rc = fd_amd_slot_launch_txn( s, staged, slots, blob_at, NULL, NULL, 1 )) ) return rc;
         diag->batch_sig_cnt += slots;
+      } else if( zc_dev ) {
+        if( (rc = fd_amd_slot_launch_zc( s, staged, zc_dev )) ) return rc;
+        diag->batch_sig_cnt += staged;
       } else {
         if( (rc = fd_amd_slot_launch( s, staged, blob_at, NULL, 1 )) ) return rc;
         diag->batch_sig_cnt += staged;
@@ -285,22 +322,31 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
 /* streaming benchmark: producer -> tile -> consumer                    */
 
 extern "C" int
-fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, double rate, ulong pool_n,
-                            uchar const * pub, uchar const * sig, uint const * msg_off, uint const * msg_sz,
-                            uchar const * blob, ulong frag_cnt, double * out ) {
+fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, double rate, int zero_copy,
+                            ulong pool_n, uchar const * pub, uchar const * sig, uint const * msg_off,
+                            uint const * msg_sz, uchar const * blob, ulong frag_cnt, double * out ) {
   if( !pool_n || !frag_cnt || !out ) return FD_ED25519_AMD_ERR_INVAL;
   ulong depth = 1UL; while( depth < 8UL*batch_max + 1024UL ) depth <<= 1;   /* > batches in flight + staging */
   ulong mtu = 96UL + FD_ED25519_AMD_MSG_MAX;
   ulong chunk_mtu = ((mtu + 2UL*FD_CHUNK_SZ - 1UL) >> (1 + FD_CHUNK_LG_SZ)) << 1;
-  ulong data_chunks = chunk_mtu * (depth + 2UL);
+  /* The data region holds every pool frame once (what a NIC would have
+     DMA'd): the producer publishes metadata only, so the bench measures the
+     tile, not a producer-side memcpy. */
+  ulong data_chunks = chunk_mtu * pool_n;
   std::vector<fd_frag_meta_t> in_mc( depth ), out_mc( depth );
   for( ulong i=0; i<depth; i++ ) { in_mc[i].seq = i - depth; out_mc[i].seq = i - depth; }   /* "never published" */
-  uchar * dcache = (uchar *)aligned_alloc( 64, data_chunks * FD_CHUNK_SZ );
+  uchar * dcache = (uchar *)aligned_alloc( 4096, ((data_chunks * FD_CHUNK_SZ + 4095UL) & ~4095UL) );
   if( !dcache ) return FD_ED25519_AMD_ERR_INVAL;
-  ulong wmark = data_chunks - chunk_mtu;
+  for( ulong k=0; k<pool_n; k++ ) {
+    uchar * p = dcache + k * chunk_mtu * FD_CHUNK_SZ;
+    memcpy( p, pub + 32UL*k, 32 ); memcpy( p + 32, sig + 64UL*k, 64 ); memcpy( p + 96, blob + msg_off[k], msg_sz[k] );
+  }
 
   fd_verify_amd_tile_t * tile = fd_verify_amd_tile_new( device, batch_max, batch_wait_ns, 0UL );
   if( !tile ) { free( dcache ); return FD_ED25519_AMD_ERR_DEVICE; }
+  if( zero_copy && fd_verify_amd_tile_register_dcache( tile, dcache, data_chunks * FD_CHUNK_SZ ) ) {
+    fd_verify_amd_tile_delete( tile ); free( dcache ); return FD_ED25519_AMD_ERR_DEVICE;
+  }
 
   std::atomic<ulong> in_fseq( 0UL ), out_fseq( 0UL );   /* consumer progress (credits) */
   std::vector<uint> lat( frag_cnt );
@@ -309,20 +355,16 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   ulong t0 = now_ns();
 
   std::thread prod( [&]() {
-    ulong chunk = 0;
     ulong p0 = now_ns();
     for( ulong seq=0; seq<frag_cnt; seq++ ) {
       ulong due = rate > 0.0 ? p0 + (ulong)((double)seq * 1e9 / rate) : 0UL;   /* paced: open loop */
       if( due ) while( now_ns() < due ) { /* spin */ }
       /* credit: do not lap the tile's consumption of the input mcache */
       while( seq - __atomic_load_n( &diag.in_cnt, __ATOMIC_ACQUIRE ) >= depth - 16UL ) { /* spin */ }
-      ulong k = seq % pool_n, msz = msg_sz[k], sz = 96UL + msz;
-      uchar * p = dcache + chunk * FD_CHUNK_SZ;
-      memcpy( p, pub + 32UL*k, 32 ); memcpy( p + 32, sig + 64UL*k, 64 ); memcpy( p + 96, blob + msg_off[k], msz );
+      ulong k = seq % pool_n, sz = 96UL + msg_sz[k];
       /* tsorig = the scheduled send time when paced, so producer stalls count as latency */
       uint tso = due ? (uint)due : fd_verify_amd_tickcount();
-      fd_mcache_publish( in_mc.data(), depth, seq, 0UL, chunk, sz, 3UL, tso, 0UL );
-      chunk = fd_dcache_compact_next( chunk, sz, 0UL, wmark );
+      fd_mcache_publish( in_mc.data(), depth, seq, 0UL, k * chunk_mtu, sz, 3UL, tso, 0UL );
     }
   } );
   std::thread cons( [&]() {

@@ -80,6 +80,8 @@ def lib():
     L.fd_ed25519_amd_set_small_batch_max.restype = None
     L.fd_verify_amd_tile_new.argtypes = [i, ul, ul, ul]
     L.fd_verify_amd_tile_new.restype = vp
+    L.fd_verify_amd_tile_register_dcache.argtypes = [vp, vp, ul]
+    L.fd_verify_amd_tile_register_dcache.restype = i
     L.fd_verify_amd_tile_set_framing.argtypes = [vp, i]
     L.fd_verify_amd_tile_set_framing.restype = i
     L.fd_verify_amd_tile_delete.argtypes = [vp]
@@ -88,7 +90,7 @@ def lib():
     L.fd_verify_amd_tile_run.restype = i
     L.fd_verify_amd_tickcount.argtypes = []
     L.fd_verify_amd_tickcount.restype = ui
-    L.fd_verify_amd_bench_stream.argtypes = [i, ul, ul, ctypes.c_double, ul, vp, vp, vp, vp, vp, ul, vp]
+    L.fd_verify_amd_bench_stream.argtypes = [i, ul, ul, ctypes.c_double, i, ul, vp, vp, vp, vp, vp, ul, vp]
     L.fd_verify_amd_bench_stream.restype = i
     _lib = L
     return L

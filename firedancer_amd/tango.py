@@ -78,6 +78,14 @@ class VerifyTile:
         except Exception:
             pass
 
+    def register_dcache(self, region):
+        """Map the numpy data region into the GPU (zero-copy staging)."""
+        self._region = region
+        rc = ed25519.lib().fd_verify_amd_tile_register_dcache(self._h, ctypes.c_void_p(region.ctypes.data),
+                                                             region.nbytes)
+        if rc:
+            raise ed25519.EngineError("fd_verify_amd_tile_register_dcache rc=%d" % rc)
+
     def run(self, in_mcache, in_chunk0, in_seq0, out_mcache, out_seq0, frag_cnt, lat_max=0):
         """Consume frag_cnt input frags; returns (diag dict, latency samples)."""
         diag = (ctypes.c_ulong * len(DIAG_FIELDS))()
@@ -93,14 +101,15 @@ class VerifyTile:
         return d, lat[:min(lat_max, d["out_cnt"])]
 
 
-def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, blob, frag_cnt, rate=0.0):
+def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, blob, frag_cnt, rate=0.0,
+                 zero_copy=False):
     """fd_verify_amd_bench_stream: producer (rate frags/s, 0 = saturate) -> tile -> consumer; returns
     dict(frags_per_s, p50_ns, p99_ns, p999_ns, mean_batch, published, sv_filt)."""
     out = (ctypes.c_double * 7)()
     p = [np.ascontiguousarray(a) for a in (pub, sig, msg_off, msg_sz, blob)]
     vp = ctypes.c_void_p
     rc = ed25519.lib().fd_verify_amd_bench_stream(int(device), int(batch_max), int(batch_wait_ns), float(rate),
-                                                  p[0].shape[0],
+                                                  int(bool(zero_copy)), p[0].shape[0],
                                                   *[vp(a.ctypes.data) for a in p], int(frag_cnt), out)
     if rc:
         raise ed25519.EngineError("fd_verify_amd_bench_stream rc=%d" % rc)

@@ -126,6 +126,14 @@ fd_verify_amd_tile_delete( fd_verify_amd_tile_t * tile );
    iff it parses and all its signatures pass; HA dedup uses its first
    signature, the published tag is that signature's SHA-512 tag.  A frag
    that fails to parse counts as SV_FILT. */
+/* Zero-copy staging: map the host data region [base, base+sz) holding
+   the input frags into the GPU (hipHostRegister).  When a run's in_chunk0
+   lies inside it and the framing is PUB_SIG_MSG, the tile hands the GPU
+   only (chunk, size) per frag; a gather kernel reads the 96 header bytes
+   and k_prep reads the message over PCIe in place (no host memcpy). */
+int
+fd_verify_amd_tile_register_dcache( fd_verify_amd_tile_t * tile, void * base, ulong sz );
+
 #define FD_VERIFY_AMD_FRAMING_PUB_SIG_MSG (0)
 #define FD_VERIFY_AMD_FRAMING_TXN         (1)
 int
@@ -166,8 +174,9 @@ fd_verify_amd_tickcount( void );
    layout of fd_ed25519_amd_verify_soa) into a private mcache/dcache --
    at `rate` frags/s (open loop; tsorig = scheduled send time) or, with
    rate 0, as fast as the tile accepts (credit-based flow control) -- the
-   tile runs on `device` with 4 batches in flight, and a consumer drains
-   the output.  Runs until frag_cnt frags were published.  out[0] = frags/s through the tile,
+   tile runs on `device` with 4 batches in flight (zero_copy: the data
+   region is mapped into the GPU, fd_verify_amd_tile_register_dcache), and
+   a consumer drains the output.  Runs until frag_cnt frags were published.  out[0] = frags/s through the tile,
    out[1..3] = p50 / p99 / p999 latency in ns (producer publish -> tile
    publish), out[4] = mean GPU batch size, out[5] = frags published,
    out[6] = frags dropped by verification.  Returns 0 or an error code. */
@@ -176,6 +185,7 @@ fd_verify_amd_bench_stream( int           device,
                             ulong         batch_max,
                             ulong         batch_wait_ns,
                             double        rate,
+                            int           zero_copy,
                             ulong         pool_n,
                             uchar const * pub,
                             uchar const * sig,

@@ -24,7 +24,7 @@ def _feed(pub, sig, msgs, order, depth):
     mtu = 96 + 1232
     chunk_mtu = ((mtu + 2 * 64 - 1) >> 7) << 1
     nchunk = chunk_mtu * (len(order) + 2)
-    dcache = tango._aligned(64 * nchunk)
+    dcache = tango._aligned((64 * nchunk + 4095) & ~4095, 4096)   # page-aligned: can be GPU-mapped
     mc = tango.mcache_new(depth)
     chunk, chunks, sizes, ts = 0, [], [], []
     wmark = nchunk - chunk_mtu
@@ -66,8 +66,9 @@ def _pool(golden):
     return pub, sig, msgs, golden.expect[pick]
 
 
-@pytest.mark.parametrize("batch_max,tc_depth", [(512, 1 << 12), (37, 8), (1, 0)])
-def test_tile_publishes_passing_frags_in_order(golden, batch_max, tc_depth):
+@pytest.mark.parametrize("batch_max,tc_depth,zero_copy", [(512, 1 << 12, False), (37, 8, False), (1, 0, False),
+                                                         (512, 1 << 12, True), (37, 8, True)])
+def test_tile_publishes_passing_frags_in_order(golden, batch_max, tc_depth, zero_copy):
     from firedancer_amd import tango
     pub, sig, msgs, verdict = _pool(golden)
     rng = np.random.default_rng(batch_max)
@@ -76,6 +77,8 @@ def test_tile_publishes_passing_frags_in_order(golden, batch_max, tc_depth):
     mc_in, dc, chunks, sizes, ts = _feed(pub, sig, msgs, order, 2048)
     mc_out = tango.mcache_new(2048)
     tile = tango.VerifyTile(0, batch_max=batch_max, tcache_depth=tc_depth)
+    if zero_copy:
+        tile.register_dcache(dc)        # frags gathered on the GPU from the mapped data region
     try:
         diag, lat = tile.run(mc_in, dc, 0, mc_out, 0, n, lat_max=n)
     finally:
@@ -133,6 +136,8 @@ def test_stream_bench_smoke():
     assert r["frags_per_s"] > 0 and 0 < r["p50_ns"] <= r["p99_ns"]
     r = tango.bench_stream(0, 256, 0, pub, sig, off, sz, blob, 5000, rate=50000.0)
     assert r["published"] == 5000 and r["p50_ns"] > 0
+    r = tango.bench_stream(0, 1024, 0, pub, sig, off, sz, blob, 20000, zero_copy=True)
+    assert r["published"] == 20000 and r["sv_filt"] == 0
 
 
 def test_tile_txn_framing_vs_oracle():
