@@ -67,7 +67,7 @@ def parse():
     ap.add_argument("--no-stream", action="store_true", help="skip the streaming-tile sweep (config 5)")
     ap.add_argument("--workload", choices=("sigs", "txn"), default="sigs",
                     help="sigs: configs[1] (default bench line); txn: configs[3] multi-signer transactions")
-    ap.add_argument("--stream-frags", type=int, default=1 << 18, help="frags per streaming-tile run")
+    ap.add_argument("--stream-frags", type=int, default=1 << 20, help="frags per streaming-tile run")
     return ap.parse_args()
 
 
@@ -292,6 +292,25 @@ def main():
         lat = np.array(lat[3:])
         out["latency_ms_4096"] = {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
                                   "path": "host SoA -> pinned staging -> H2D -> 3 kernels -> D2H"}
+    if not args.no_latency:
+        # PCIe-inclusive rate: the same 2^20 batch handed over as host SoA
+        # buffers (pinned double-buffered staging, chunks of 2^17), priced
+        # against the measured pinned H2D ceiling.  Never the headline value.
+        chunk = 1 << 17
+        eng = ed25519.Engine(device=local, batch_max=chunk, blob_max=chunk * args.msg_sz)
+        eng.verify_soa(pub[:chunk], sig[:chunk], off[:chunk], sz[:chunk], blob)
+        reps, t1 = 3, time.perf_counter()
+        for _ in range(reps):
+            herr = eng.verify_soa(pub, sig, off, sz, blob)
+        dt = (time.perf_counter() - t1) / reps
+        eng.close()
+        h2d_gbs = hip.h2d_bandwidth()
+        per_sig = 104 + args.msg_sz
+        out["host_soa"] = {"verifies_per_s": n / dt, "chunk": chunk, "h2d_bytes_per_sig": per_sig,
+                           "h2d_gb_per_s": n * per_sig / dt / 1e9, "pinned_h2d_peak_gb_per_s": h2d_gbs,
+                           "pcie_bound_verifies_per_s": h2d_gbs * 1e9 / per_sig,
+                           "verdicts_match_resident": bool((herr == err).all()),
+                           "path": "host SoA -> pinned packed staging (2 chunks in flight) -> H2D -> kernels -> D2H"}
     if world == 1 and not args.no_stream:
         # config 5: tango mcache/dcache feed -> verify tile -> consumer, per batch cap
         from firedancer_amd import tango

@@ -16,6 +16,7 @@
 #include <string.h>
 #include <stdint.h>
 #include <mutex>
+#include <thread>
 
 #include "../../include/fd_ed25519_amd.h"
 #include "../../include/fd_txn_amd.h"
@@ -27,6 +28,19 @@
     return FD_ED25519_AMD_ERR_DEVICE; } } while(0)
 
 #include "fd_ed25519_engine.h"
+
+/* Results go device -> host through a small kernel that writes the mapped,
+   coherent pinned buffer, not through a DMA copy: the copy engine serves
+   the streams' commands in order, so a D2H queued behind one batch's
+   kernels would hold up the next batch's H2D on another stream. */
+static hipError_t
+slot_out( slot_t * s, void * h_dst, void const * d_src, ulong n ) {
+  void * d_dst = h_dst == (void *)s->h_err  ? s->m_err  :
+                 h_dst == (void *)s->h_terr ? s->m_terr :
+                 h_dst == (void *)s->h_tag  ? s->m_tag  : NULL;
+  if( !d_dst ) return hipErrorInvalidValue;
+  return fd_amd_launch_copy_out( d_dst, d_src, n, s->stream ) ? hipErrorLaunchFailure : hipSuccess;
+}
 
 static void
 slot_free( slot_t * s ) {
@@ -77,17 +91,26 @@ slot_alloc( slot_t * s, ulong cap, ulong blob_cap ) {
   HIPCHK( hipHostMalloc( (void **)&s->h_blob, blob_cap + 64UL, hipHostMallocDefault ) );
   HIPCHK( hipHostMalloc( (void **)&s->h_off,  4UL*cap, hipHostMallocDefault ) );
   HIPCHK( hipHostMalloc( (void **)&s->h_sz,   4UL*cap, hipHostMallocDefault ) );
-  HIPCHK( hipHostMalloc( (void **)&s->h_err,  cap, hipHostMallocDefault ) );
+  HIPCHK( hipHostMalloc( (void **)&s->h_err,  cap, hipHostMallocMapped | hipHostMallocCoherent ) );
+  HIPCHK( hipHostGetDevicePointer( &s->m_err, s->h_err, 0 ) );
   HIPCHK( hipMalloc( (void **)&s->d_pack, 104UL*cap + blob_cap + 64UL ) );
   HIPCHK( hipHostMalloc( (void **)&s->h_pack, 104UL*cap + blob_cap + 64UL, hipHostMallocDefault ) );
   HIPCHK( hipStreamCreateWithFlags( &s->stream, hipStreamNonBlocking ) );
   HIPCHK( hipEventCreateWithFlags( &s->done, hipEventDisableTiming ) );
+  /* first use of a stream (its hardware queue) and of a staging pair costs
+     ~8 ms inside the first hipMemcpyAsync: pay it here, not in a batch */
+  memset( s->h_pack, 0, 104UL*cap + blob_cap + 64UL );
+  HIPCHK( hipMemcpyAsync( s->d_pack, s->h_pack, 104UL*cap + blob_cap + 64UL, hipMemcpyHostToDevice, s->stream ) );
+  HIPCHK( hipStreamSynchronize( s->stream ) );
   return FD_ED25519_AMD_OK;
 }
 
 extern "C" fd_ed25519_amd_t *
 fd_ed25519_amd_new( int device, ulong batch_max, ulong blob_max ) {
-  return fd_amd_engine_new( device, batch_max, blob_max, 2 );
+  int nslot = 2;
+  char const * ev = getenv( "FD_ED25519_AMD_NSLOT" );
+  if( ev && atoi( ev ) >= 2 && atoi( ev ) <= FD_AMD_SLOT_MAX ) nslot = atoi( ev );
+  return fd_amd_engine_new( device, batch_max, blob_max, nslot );
 }
 
 fd_ed25519_amd_t *
@@ -132,8 +155,10 @@ fd_amd_slot_alloc_aux( slot_t * s, ulong cap ) {
   HIPCHK( hipHostMalloc( (void **)&s->h_toff,  4UL*cap, hipHostMallocDefault ) );
   HIPCHK( hipHostMalloc( (void **)&s->h_tsz,   4UL*cap, hipHostMallocDefault ) );
   HIPCHK( hipHostMalloc( (void **)&s->h_tbase, 4UL*(cap+1UL), hipHostMallocDefault ) );
-  HIPCHK( hipHostMalloc( (void **)&s->h_terr,  cap, hipHostMallocDefault ) );
-  HIPCHK( hipHostMalloc( (void **)&s->h_tag,   8UL*cap, hipHostMallocDefault ) );
+  HIPCHK( hipHostMalloc( (void **)&s->h_terr,  cap, hipHostMallocMapped | hipHostMallocCoherent ) );
+  HIPCHK( hipHostGetDevicePointer( &s->m_terr, s->h_terr, 0 ) );
+  HIPCHK( hipHostMalloc( (void **)&s->h_tag,   8UL*cap, hipHostMallocMapped | hipHostMallocCoherent ) );
+  HIPCHK( hipHostGetDevicePointer( &s->m_tag, s->h_tag, 0 ) );
   return FD_ED25519_AMD_OK;
 }
 
@@ -161,10 +186,10 @@ fd_amd_slot_launch( slot_t * s, ulong n, ulong blob_sz, schar * out, int want_ta
   if( fd_amd_launch_verify( (uint32_t)n, s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_blob, s->d_err, s->d_ws, s->stream, 1, NULL,
                             NULL, s->dsm_mode ) )
     return FD_ED25519_AMD_ERR_DEVICE;
-  HIPCHK( hipMemcpyAsync( s->h_err, s->d_err, n, hipMemcpyDeviceToHost, s->stream ) );
+  HIPCHK( slot_out( s, s->h_err, s->d_err, n ) );
   if( want_tag ) {
     ws_layout_t L = fd_amd_ws_layout( n );
-    HIPCHK( hipMemcpyAsync( s->h_tag, (uint8_t *)s->d_ws + L.tag, 8UL*n, hipMemcpyDeviceToHost, s->stream ) );
+    HIPCHK( slot_out( s, s->h_tag, (uint8_t *)s->d_ws + L.tag, 8UL*n ) );
   }
   HIPCHK( hipEventRecord( s->done, s->stream ) );
   s->out = out; s->n = n; s->busy = 1; s->want_tag = want_tag;
@@ -181,9 +206,9 @@ fd_amd_slot_launch_zc( slot_t * s, ulong n, uint8_t const * d_dc ) {
   if( fd_amd_launch_verify( (uint32_t)n, s->d_pub, s->d_sig, s->d_off, s->d_sz, d_dc, s->d_err, s->d_ws, s->stream, 1, NULL,
                             NULL, s->dsm_mode ) )
     return FD_ED25519_AMD_ERR_DEVICE;
-  HIPCHK( hipMemcpyAsync( s->h_err, s->d_err, n, hipMemcpyDeviceToHost, s->stream ) );
+  HIPCHK( slot_out( s, s->h_err, s->d_err, n ) );
   ws_layout_t L = fd_amd_ws_layout( n );
-  HIPCHK( hipMemcpyAsync( s->h_tag, (uint8_t *)s->d_ws + L.tag, 8UL*n, hipMemcpyDeviceToHost, s->stream ) );
+  HIPCHK( slot_out( s, s->h_tag, (uint8_t *)s->d_ws + L.tag, 8UL*n ) );
   HIPCHK( hipEventRecord( s->done, s->stream ) );
   s->out = NULL; s->n = n; s->busy = 1; s->want_tag = 1;
   return FD_ED25519_AMD_OK;
@@ -196,7 +221,7 @@ fd_amd_slot_launch_packed( slot_t * s, ulong n, ulong blob_sz, schar * out ) {
   if( fd_amd_launch_verify( (uint32_t)n, d, d + 32UL*n, (uint32_t *)(d + 96UL*n), (uint32_t *)(d + 100UL*n),
                             d + 104UL*n, s->d_err, s->d_ws, s->stream, 1, NULL ) )
     return FD_ED25519_AMD_ERR_DEVICE;
-  HIPCHK( hipMemcpyAsync( s->h_err, s->d_err, n, hipMemcpyDeviceToHost, s->stream ) );
+  HIPCHK( slot_out( s, s->h_err, s->d_err, n ) );
   HIPCHK( hipEventRecord( s->done, s->stream ) );
   s->out = out; s->n = n; s->busy = 1; s->want_tag = 0;
   return FD_ED25519_AMD_OK;
@@ -229,11 +254,11 @@ fd_amd_slot_launch_txn( slot_t * s, ulong c, ulong nslot, ulong blob_sz, schar *
     return FD_ED25519_AMD_ERR_DEVICE;
   if( fd_amd_launch_txn_reduce( (uint32_t)c, s->d_fp, s->d_tbase, s->d_err, s->d_terr, s->stream ) )
     return FD_ED25519_AMD_ERR_DEVICE;
-  HIPCHK( hipMemcpyAsync( s->h_terr, s->d_terr, c, hipMemcpyDeviceToHost, s->stream ) );
-  if( s_out && nslot ) HIPCHK( hipMemcpyAsync( s->h_err, s->d_err, nslot, hipMemcpyDeviceToHost, s->stream ) );
+  HIPCHK( slot_out( s, s->h_terr, s->d_terr, c ) );
+  if( s_out && nslot ) HIPCHK( slot_out( s, s->h_err, s->d_err, nslot ) );
   if( want_tag && nslot ) {
     ws_layout_t L = fd_amd_ws_layout( nslot );
-    HIPCHK( hipMemcpyAsync( s->h_tag, (uint8_t *)s->d_ws + L.tag, 8UL*nslot, hipMemcpyDeviceToHost, s->stream ) );
+    HIPCHK( slot_out( s, s->h_tag, (uint8_t *)s->d_ws + L.tag, 8UL*nslot ) );
   }
   HIPCHK( hipEventRecord( s->done, s->stream ) );
   s->t_out = t_out; s->t_n = c;
@@ -290,6 +315,69 @@ fd_ed25519_amd_verify_batch( fd_ed25519_amd_t * e, ulong n, void const * const *
   } );
 }
 
+/* memcpy split over up to 4 host threads for large copies (the staging
+   copy is the host-side limit of the SoA path: ~300 B per signature). */
+static void
+copy_par( void * dst, void const * src, ulong sz ) {
+  ulong const min_part = 4UL << 20;
+  int nt = (int)( sz / min_part ); if( nt > 4 ) nt = 4;
+  if( nt < 2 ) { if( sz ) memcpy( dst, src, sz ); return; }
+  std::thread th[3];
+  ulong part = ( sz / (ulong)nt + 63UL ) & ~63UL;
+  for( int t=1; t<nt; t++ ) {
+    ulong lo = part*(ulong)t, hi = lo + part < sz ? lo + part : sz;
+    if( lo < hi ) th[t-1] = std::thread( [=]{ memcpy( (uint8_t *)dst + lo, (uint8_t const *)src + lo, hi - lo ); } );
+  }
+  memcpy( dst, src, part < sz ? part : sz );
+  for( int t=1; t<nt; t++ ) if( th[t-1].joinable() ) th[t-1].join();
+}
+
+/* SoA staging with block copies: pub and sig are contiguous per chunk, and
+   when the chunk's messages sit in a window of the blob not much larger
+   than their total size, the window is copied as one block and the offsets
+   rebased (no per-message copy).  Other layouts gather message by message. */
+static int
+run_soa( fd_ed25519_amd_t * e, ulong n, uchar const * pub, uchar const * sig, uint const * msg_off,
+         uint const * msg_sz, uchar const * blob, schar * err ) {
+  if( hipSetDevice( e->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  ulong i = 0; int k = 0; int rc = FD_ED25519_AMD_OK;
+  while( i < n ) {
+    slot_t * s = &e->slot[k];
+    if( (rc = fd_amd_slot_drain( s )) ) return rc;
+    ulong c = 0, bsz = 0, lo = ~0UL, hi = 0UL;
+    while( i + c < n && c < e->cap ) {
+      ulong sz = msg_sz[i+c];
+      if( sz > e->blob_cap ) return FD_ED25519_AMD_ERR_INVAL;
+      if( bsz + sz > e->blob_cap ) break;
+      if( sz ) { ulong o = msg_off[i+c]; lo = o < lo ? o : lo; hi = o + sz > hi ? o + sz : hi; }
+      bsz += sz; c++;
+    }
+    uint8_t * hp = s->h_pack;
+    uint8_t * h_blob = hp + 104UL*c;
+    uint32_t * h_off = (uint32_t *)(hp + 96UL*c), * h_sz = (uint32_t *)(hp + 100UL*c);
+    copy_par( hp, pub + 32UL*i, 32UL*c );
+    copy_par( hp + 32UL*c, sig + 64UL*i, 64UL*c );
+    memcpy( h_sz, msg_sz + i, 4UL*c );
+    ulong win = hi > lo ? hi - lo : 0UL;
+    if( win <= e->blob_cap && win <= bsz + bsz/4UL + 4096UL ) {
+      copy_par( h_blob, blob + (hi > lo ? lo : 0UL), win );
+      for( ulong j=0; j<c; j++ ) h_off[j] = msg_sz[i+j] ? (uint32_t)(msg_off[i+j] - lo) : 0U;
+      bsz = win;
+    } else {
+      bsz = 0;
+      for( ulong j=0; j<c; j++ ) {
+        ulong sz = msg_sz[i+j];
+        if( sz ) memcpy( h_blob + bsz, blob + msg_off[i+j], sz );
+        h_off[j] = (uint32_t)bsz; bsz += sz;
+      }
+    }
+    if( (rc = fd_amd_slot_launch_packed( s, c, bsz, err + i )) ) return rc;
+    i += c; k = (k + 1) % e->nslot;
+  }
+  for( int j=0; j<e->nslot; j++ ) if( (rc = fd_amd_slot_drain( &e->slot[j] )) ) return rc;
+  return FD_ED25519_AMD_OK;
+}
+
 extern "C" int
 fd_ed25519_amd_verify_soa( fd_ed25519_amd_t * e, ulong n, uchar const * pub, uchar const * sig,
                            uint const * msg_off, uint const * msg_sz, uchar const * blob, ulong blob_sz,
@@ -297,9 +385,7 @@ fd_ed25519_amd_verify_soa( fd_ed25519_amd_t * e, ulong n, uchar const * pub, uch
   if( !e || (n && (!pub || !sig || !msg_off || !msg_sz || !err)) ) return FD_ED25519_AMD_ERR_INVAL;
   for( ulong i=0; i<n; i++ )
     if( msg_sz[i] && ((ulong)msg_off[i] + msg_sz[i] > blob_sz || !blob) ) return FD_ED25519_AMD_ERR_INVAL;
-  return run_chunked( e, n, err, [&]( ulong i, uint8_t const ** m, ulong * s, uint8_t const ** g, uint8_t const ** p ) {
-    *m = blob + msg_off[i]; *s = msg_sz[i]; *g = sig + 64UL*i; *p = pub + 32UL*i;
-  } );
+  return run_soa( e, n, pub, sig, msg_off, msg_sz, blob, err );
 }
 
 /* Signature slots the engine reserves for a payload: its first byte when

@@ -936,6 +936,25 @@ fd_amd_launch_zgather( uint32_t n, uint32_t const * d_chunk, uint32_t const * d_
 /* ------------------------------------------------------------------ */
 /* launch                                                               */
 
+/* device -> mapped host result copy: 16 B per lane where both ends are
+   16-aligned (every result buffer is), bytes otherwise. */
+__global__ void __launch_bounds__(256)
+k_copy_out( u8 * __restrict__ dst, u8 const * __restrict__ src, size_t n ) {
+  size_t i = (size_t)blockIdx.x * 256u + threadIdx.x, stride = (size_t)gridDim.x * 256u;
+  size_t nv = (((size_t)dst | (size_t)src) & 15u) ? 0 : (n >> 4);
+  for( size_t k = i; k < nv; k += stride ) ((uint4 *)dst)[k] = ((uint4 const *)src)[k];
+  for( size_t k = (nv << 4) + i; k < n; k += stride ) dst[k] = src[k];
+}
+
+int
+fd_amd_launch_copy_out( void * d_dst, void const * d_src, size_t n, hipStream_t stream ) {
+  if( !n ) return 0;
+  size_t nb = ( (n >> 4) + 256u ) / 256u;
+  if( nb > 4096u ) nb = 4096u;
+  hipLaunchKernelGGL( k_copy_out, dim3((unsigned)nb), dim3(256), 0, stream, (u8 *)d_dst, (u8 const *)d_src, n );
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 /* Batches up to this size use k_dsm4 (fd_ed25519_amd_set_small_batch_max). */
 static volatile u32 g_dsm4_max = 16384u;
 static u32 fd_amd_dsm4_max( void ) { return g_dsm4_max; }

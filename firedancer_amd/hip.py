@@ -49,6 +49,8 @@ def hip():
     H.hipEventRecord.argtypes = [vp, vp]
     H.hipEventSynchronize.argtypes = [vp]
     H.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), vp, vp]
+    H.hipHostMalloc.argtypes = [ctypes.POINTER(vp), sz, u]
+    H.hipHostFree.argtypes = [vp]
     H.hipGetErrorString.argtypes = [i]
     H.hipGetErrorString.restype = ctypes.c_char_p
     H.hipDeviceGetName = getattr(H, "hipDeviceGetName", None)
@@ -124,6 +126,49 @@ class DeviceBuffer:
             self.free()
         except Exception:
             pass
+
+
+class PinnedBuffer:
+    """Page-locked host memory (hipHostMalloc), viewable as a numpy array."""
+
+    def __init__(self, nbytes):
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        check(hip().hipHostMalloc(ctypes.byref(p), max(self.nbytes, 1), 0), "hipHostMalloc(%d)" % self.nbytes)
+        self.ptr = p.value
+
+    def array(self, dtype=np.uint8):
+        n = self.nbytes // np.dtype(dtype).itemsize
+        return np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr)).view(dtype)[:n]
+
+    def free(self):
+        if self.ptr:
+            hip().hipHostFree(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def h2d_bandwidth(nbytes=256 << 20, reps=5):
+    """Measured pinned host -> device copy rate in GB/s (the PCIe ceiling
+    the host-staged paths are priced against)."""
+    src, dst, st = PinnedBuffer(nbytes), DeviceBuffer(nbytes), Stream()
+    e0, e1 = Event(), Event()
+    H = hip()
+    check(H.hipMemcpyAsync(dst.ptr, src.ptr, nbytes, H2D, st.handle), "hipMemcpyAsync")
+    st.synchronize()
+    e0.record(st)
+    for _ in range(reps):
+        check(H.hipMemcpyAsync(dst.ptr, src.ptr, nbytes, H2D, st.handle), "hipMemcpyAsync")
+    e1.record(st)
+    e1.synchronize()
+    ms = e0.elapsed_ms(e1)
+    st.destroy(); src.free(); dst.free()
+    return nbytes * reps / (ms * 1e-3) / 1e9
 
 
 class Stream:

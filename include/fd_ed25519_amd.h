@@ -109,7 +109,8 @@ typedef struct fd_ed25519_amd fd_ed25519_amd_t;
    call (larger calls are split internally).  Owns its HIP stream, device
    buffers and pinned, double-buffered host staging.  NULL on failure.
    One engine per host thread; engines on different devices run
-   independently (multi-GPU = one engine per device). */
+   independently (multi-GPU = one engine per device).  Chunks in flight:
+   2, or FD_ED25519_AMD_NSLOT (2..6) from the environment. */
 fd_ed25519_amd_t *
 fd_ed25519_amd_new( int device, ulong batch_max, ulong blob_max );
 

@@ -77,6 +77,45 @@ def test_small_engine_chunking(golden):
     assert np.array_equal(err, golden.expect)
 
 
+@pytest.mark.parametrize("layout", ["permuted", "reversed", "sparse", "shared"])
+@pytest.mark.parametrize("small", [False, True])
+def test_soa_blob_layouts(engine, golden, layout, small):
+    """verify_soa stages a chunk's message window as one block when it is
+    dense (any order inside it) and gathers message by message otherwise;
+    every layout must give the golden verdicts."""
+    from firedancer_amd import ed25519
+    n = len(golden)
+    msgs = [golden.msg(i) for i in range(n)]
+    rng = np.random.default_rng(5)
+    if layout == "shared":   # duplicate messages share one copy in the blob
+        uniq = {}
+        parts, off, pos = [], np.zeros(n, np.uint32), 0
+        for i, m in enumerate(msgs):
+            if m not in uniq:
+                uniq[m] = pos
+                parts.append(m)
+                pos += len(m)
+            off[i] = uniq[m]
+        blob = b"".join(parts)
+    else:
+        order = {"permuted": rng.permutation(n), "reversed": np.arange(n)[::-1], "sparse": np.arange(n)}[layout]
+        gap = 3000 if layout == "sparse" else 0
+        off, parts, pos = np.zeros(n, np.uint32), [], 0
+        for j in order:
+            off[j] = pos
+            parts.append(msgs[j] + bytes(gap))
+            pos += len(msgs[j]) + gap
+        blob = b"".join(parts)
+    blob = np.frombuffer(blob + b"\0", np.uint8)
+    eng = ed25519.Engine(device=0, batch_max=100, blob_max=8192) if small else engine
+    try:
+        err = eng.verify_soa(golden.pub, golden.sig, off, golden.msg_sz, blob)
+    finally:
+        if small:
+            eng.close()
+    assert np.array_equal(err, golden.expect)
+
+
 def test_empty_and_single(engine, golden):
     e0 = engine.verify_soa(np.zeros((0, 32), np.uint8), np.zeros((0, 64), np.uint8), np.zeros(0, np.uint32),
                            np.zeros(0, np.uint32), np.zeros(1, np.uint8))
