@@ -711,6 +711,66 @@ quad_body_own( p1p1 & t, fe const & pm, fe const & qrow, bool isD, u64 mD, u64 m
   }
 }
 
+/* Own-coordinate form of the step (FD_DSM4_OWNC): after the body mul,
+   lane q computes only the ONE p1p1 coordinate C = (Z, T, X, Y)[q] that it
+   owns, as x*A + y*B + z*D over three DPP-read products with per-lane
+   coefficients in {-1,0,1,2} (three v_mad_i64_i32, low 32 bits = the
+   reference's wrapping limb adds), instead of every lane mixing all four
+   coordinates.  The next p1p1->p3 then reads its operands a = (Z,Z,X,X)[q],
+   b = (T,Y,T,Y)[q] with two quad_perm DPP reads per limb.
+     DBL  Z = m1-m2   T = m3-m1+m2   X = m0-m1-m2   Y = m1+m2
+     ADD  Z = 2m2+-m3 T = 2m2-+m3    X = m0-m1      Y = m0+m1
+   A/B/D sources: q0,q1 <- m1,m2,m3; q2,q3 <- m0,m1,m2. */
+#ifndef FD_DSM4_OWNC
+#define FD_DSM4_OWNC 1
+#endif
+__device__ __forceinline__ fe
+quad_p3_ownc( fe const & C ) {
+  fe a, b;
+  _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = qp<0,0,2,2>( C.v[k] ); b.v[k] = qp<1,3,1,3>( C.v[k] ); }
+  return fe_mul( a, b );
+}
+
+__device__ __forceinline__ i32
+lin3( i32 x, i32 A, i32 y, i32 B, i32 z, i32 D ) {
+  i64 acc = fd_pin( (i64)x * (i64)A );
+  acc = fd_pin( (i64)y * (i64)B + acc );
+  acc = fd_pin( (i64)z * (i64)D + acc );
+  return (i32)acc;
+}
+
+__device__ __forceinline__ i32
+lin2( i32 x, i32 A, i32 y, i32 B ) {
+  i64 acc = fd_pin( (i64)x * (i64)A );
+  acc = fd_pin( (i64)y * (i64)B + acc );
+  return (i32)acc;
+}
+
+__device__ __forceinline__ void
+quad_body_ownc( fe & C, fe const & pm, fe const & qrow, bool isD, bool neg, u64 mD, int qd ) {
+  /* operand a = c1*P1 + c2*P2 with P1 = quad_perm(2,2,2,0) -> X X X Z and
+     P2 = quad_perm(1,1,0,3) -> Y Y Z T:  DBL a = [X+Y, Y, X, Z],
+     ADD a = [X+Y, Y-X, Z, T];  b = DBL ? a << (q==3) : qrow */
+  i32 c1 = (qd == 0) ? 1 : (qd == 1) ? (isD ? 0 : -1) : (isD ? 1 : 0);
+  i32 c2 = (qd <= 1 || !isD) ? 1 : 0;
+  i32 sh = (qd == 3) ? 1 : 0;
+  asm( "" : "+v"(c1), "+v"(c2) );
+  fe a, b;
+  _Pragma("unroll") for( int k=0; k<10; k++ ) {
+    i32 av = lin2( c1, qp<2,2,2,0>( pm.v[k] ), c2, qp<1,1,0,3>( pm.v[k] ) );
+    a.v[k] = av;
+    b.v[k] = vsel( mD, (i32)((u32)av << sh), qrow.v[k] );
+  }
+  fe m = fe_mul( a, b );
+  i32 s0 = neg ? -1 : 1;
+  i32 x = isD ? (qd == 1 ? -1 : (qd == 3 ? 0 : 1)) : (qd >= 2 ? 1 : 0);
+  i32 y = isD ? ((qd & 1) ? 1 : -1)               : (qd <= 1 ? 2 : (qd == 2 ? -1 : 1));
+  i32 z = isD ? (qd == 0 ? 0 : (qd == 2 ? -1 : 1)) : (qd == 0 ? s0 : (qd == 1 ? -s0 : 0));
+  asm( "" : "+v"(x), "+v"(y), "+v"(z) );   /* opaque: keep full v_mad_i64_i32 (no small-range rewrites) */
+  _Pragma("unroll") for( int k=0; k<10; k++ )
+    C.v[k] = lin3( x, qp<1,1,0,0>( m.v[k] ), y, qp<2,2,1,1>( m.v[k] ), z, qp<3,3,2,2>( m.v[k] ) );
+}
+
 /* op body + mix on a quad.  qrow: this lane's table row (ADD); isD/neg per
    lane (uniform within the quad). */
 __device__ __forceinline__ void
@@ -830,11 +890,19 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
   if( ph == PH_FIN ) {
     _Pragma("unroll") for( int k=0; k<10; k++ ) qrow.v[k] = Rw[(size_t)((qd & 1)*10 + k)*N + ii];
   }
+#if FD_DSM4_OWNC
+  fe C = (qd == 2) ? fe_zero() : fe_one();   /* identity: own coordinate (Z, T, X, Y)[q] = (1, 1, 0, 1) */
+#else
   p1p1 t;
   t.X = fe_zero(); t.Y = fe_one(); t.Z = fe_one(); t.T = fe_one();
+#endif
 
   for( ;; ) {
+#if FD_DSM4_OWNC
+    fe pm = quad_p3_ownc( C );              /* q0 u.Z, q1 u.Y, q2 u.X, q3 u.T */
+#else
     fe pm = quad_p3_own( t, m1, m2 );       /* q0 u.Z, q1 u.Y, q2 u.X, q3 u.T */
+#endif
 
     bool fin = (ph == PH_FIN);
     if( __any( fin ) ) {
@@ -857,8 +925,13 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
     if( __all( ph == PH_DONE ) ) break;
 
     bool isD = (ph == PH_DBL);
-    u64 mD = __builtin_amdgcn_ballot_w64( isD ), mN = __builtin_amdgcn_ballot_w64( qneg );
+    u64 mD = __builtin_amdgcn_ballot_w64( isD );
+#if FD_DSM4_OWNC
+    quad_body_ownc( C, pm, qrow, isD, qneg, mD, qd );
+#else
+    u64 mN = __builtin_amdgcn_ballot_w64( qneg );
     quad_body_own( t, pm, qrow, isD, mD, mN, qd );
+#endif
 
     int da = (int)(i8)(cur & 0xff), db = (int)(i8)(cur >> 8);
     int nph;
