@@ -10,5 +10,5 @@ timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeou
 tail -3 $O/tests.log
 timeout -k 10 300 python3 bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-latency > $O/prof.log 2>&1 || { echo "rocprof failed"; tail -20 $O/prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-latency --no-stream > $O/prof.log 2>&1 || { echo "rocprof failed"; tail -20 $O/prof.log; exit 1; }
 find $O/prof -name "*kernel_stats.csv" -exec cat {} \;
