@@ -94,7 +94,8 @@ slot_alloc( slot_t * s, ulong cap, ulong blob_cap ) {
   HIPCHK( hipHostMalloc( (void **)&s->h_err,  cap, hipHostMallocMapped | hipHostMallocCoherent ) );
   HIPCHK( hipHostGetDevicePointer( &s->m_err, s->h_err, 0 ) );
   HIPCHK( hipMalloc( (void **)&s->d_pack, 104UL*cap + blob_cap + 64UL ) );
-  HIPCHK( hipHostMalloc( (void **)&s->h_pack, 104UL*cap + blob_cap + 64UL, hipHostMallocDefault ) );
+  HIPCHK( hipHostMalloc( (void **)&s->h_pack, 104UL*cap + blob_cap + 64UL, hipHostMallocMapped | hipHostMallocCoherent ) );
+  HIPCHK( hipHostGetDevicePointer( (void **)&s->m_pack, s->h_pack, 0 ) );
   HIPCHK( hipStreamCreateWithFlags( &s->stream, hipStreamNonBlocking ) );
   HIPCHK( hipEventCreateWithFlags( &s->done, hipEventDisableTiming ) );
   /* first use of a stream (its hardware queue) and of a staging pair costs
@@ -216,8 +217,14 @@ fd_amd_slot_launch_zc( slot_t * s, ulong n, uint8_t const * d_dc ) {
 
 int
 fd_amd_slot_launch_packed( slot_t * s, ulong n, ulong blob_sz, schar * out ) {
-  uint8_t * d = s->d_pack;
-  HIPCHK( hipMemcpyAsync( d, s->h_pack, 104UL*n + blob_sz, hipMemcpyHostToDevice, s->stream ) );
+  /* latency path: k_front reads the staging in place over PCIe (one pass,
+     ~300 B per signature), which saves the H2D and its launch gap; larger
+     batches copy first (their kernels re-read the inputs) */
+  uint8_t * d = s->m_pack;
+  if( !fd_amd_uses_latency_path( (uint32_t)n, 0 ) ) {
+    d = s->d_pack;
+    HIPCHK( hipMemcpyAsync( d, s->h_pack, 104UL*n + blob_sz, hipMemcpyHostToDevice, s->stream ) );
+  }
   if( fd_amd_launch_verify( (uint32_t)n, d, d + 32UL*n, (uint32_t *)(d + 96UL*n), (uint32_t *)(d + 100UL*n),
                             d + 104UL*n, s->d_err, s->d_ws, s->stream, 1, NULL ) )
     return FD_ED25519_AMD_ERR_DEVICE;

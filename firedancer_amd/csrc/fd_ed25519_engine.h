@@ -18,6 +18,7 @@ struct slot_t {
   hipStream_t stream;
   hipEvent_t  done;
   uint8_t  * d_pack; uint8_t * h_pack;   /* packed [pub|sig|off|sz|blob] for n: one H2D per chunk */
+  uint8_t  * m_pack;                     /* device address of the mapped h_pack (latency path reads it in place) */
   void * m_err, * m_terr, * m_tag;   /* device addresses of the mapped h_err / h_terr / h_tag */
   uint64_t * h_tag;      /* dedup tags (pinned, allocated with the txn buffers) */
   int        want_tag;

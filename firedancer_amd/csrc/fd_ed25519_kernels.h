@@ -55,6 +55,9 @@ int fd_amd_launch_sign( uint32_t n, uint8_t const * d_prv, uint32_t const * d_of
 int fd_amd_launch_zgather( uint32_t n, uint32_t const * d_chunk, uint32_t const * d_fsz, uint8_t const * d_dc,
                            uint8_t * d_pub, uint8_t * d_sig, uint32_t * d_off, uint32_t * d_sz, hipStream_t stream );
 
+/* 1 when a batch of n takes the latency kernels (k_front + k_dsm4). */
+int fd_amd_uses_latency_path( uint32_t n, int dsm_mode );
+
 /* n bytes device -> mapped host memory by a kernel (no DMA engine). */
 int fd_amd_launch_copy_out( void * d_dst_mapped, void const * d_src, size_t n, hipStream_t stream );
 

@@ -1038,6 +1038,11 @@ fd_ed25519_amd_set_small_batch_max( unsigned long n ) {
 }
 
 int
+fd_amd_uses_latency_path( uint32_t n, int dsm_mode ) {
+  return dsm_mode == 2 || (dsm_mode == 0 && n <= fd_amd_dsm4_max());
+}
+
+int
 fd_amd_launch_verify( u32 n, u8 const * d_pub, u8 const * d_sig, u32 const * d_off, u32 const * d_sz,
                       u8 const * d_blob, i8 * d_err, void * d_ws, hipStream_t stream, int want_stats,
                       hipEvent_t const * ev, i8 const * d_skip, int dsm_mode ) {
@@ -1045,7 +1050,7 @@ fd_amd_launch_verify( u32 n, u8 const * d_pub, u8 const * d_sig, u32 const * d_o
   ws_layout_t L = fd_amd_ws_layout( n );
   u8 * ws = (u8 *)d_ws;
   u32 nb = (n + 63u) / 64u;
-  bool small = dsm_mode == 2 || (dsm_mode == 0 && n <= fd_amd_dsm4_max());
+  bool small = fd_amd_uses_latency_path( n, dsm_mode );
   if( ev ) (void)hipEventRecord( ev[0], stream );
   if( small ) {   /* latency path: one front launch (hash || decompress), then k_dsm4 */
     hipLaunchKernelGGL( k_front, dim3(3u*nb), dim3(64), 0, stream, n, nb, d_pub, d_sig, d_off, d_sz, d_blob, d_err, ws, L, d_skip );
