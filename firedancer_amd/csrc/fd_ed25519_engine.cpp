@@ -248,15 +248,20 @@ fd_amd_slot_ready( slot_t * s ) {
    h_blob, rebased offsets in h_toff/h_tsz, signature-slot bases in
    h_tbase[0..c]), nslot = h_tbase[c] signature slots. */
 int
-fd_amd_slot_launch_txn( slot_t * s, ulong c, ulong nslot, ulong blob_sz, schar * t_out, schar * s_out, int want_tag ) {
+fd_amd_slot_launch_txn( slot_t * s, ulong c, ulong nslot, ulong blob_sz, schar * t_out, schar * s_out, int want_tag,
+                        uint8_t const * d_payload ) {
   HIPCHK( hipMemcpyAsync( s->d_toff,  s->h_toff,  4UL*c,        hipMemcpyHostToDevice, s->stream ) );
   HIPCHK( hipMemcpyAsync( s->d_tsz,   s->h_tsz,   4UL*c,        hipMemcpyHostToDevice, s->stream ) );
   HIPCHK( hipMemcpyAsync( s->d_tbase, s->h_tbase, 4UL*(c+1UL),  hipMemcpyHostToDevice, s->stream ) );
-  if( blob_sz ) HIPCHK( hipMemcpyAsync( s->d_blob, s->h_blob, blob_sz, hipMemcpyHostToDevice, s->stream ) );
-  if( fd_amd_launch_txn_parse( (uint32_t)c, s->d_blob, s->d_toff, s->d_tsz, s->d_fp, NULL, 0, s->d_tbase,
+  uint8_t const * pl = d_payload;
+  if( !pl ) {
+    pl = s->d_blob;
+    if( blob_sz ) HIPCHK( hipMemcpyAsync( s->d_blob, s->h_blob, blob_sz, hipMemcpyHostToDevice, s->stream ) );
+  }
+  if( fd_amd_launch_txn_parse( (uint32_t)c, pl, s->d_toff, s->d_tsz, s->d_fp, NULL, 0, s->d_tbase,
                                s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_skip, s->stream ) )
     return FD_ED25519_AMD_ERR_DEVICE;
-  if( nslot && fd_amd_launch_verify( (uint32_t)nslot, s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_blob, s->d_err,
+  if( nslot && fd_amd_launch_verify( (uint32_t)nslot, s->d_pub, s->d_sig, s->d_off, s->d_sz, pl, s->d_err,
                                      s->d_ws, s->stream, 0, NULL, s->d_skip, s->dsm_mode ) )
     return FD_ED25519_AMD_ERR_DEVICE;
   if( fd_amd_launch_txn_reduce( (uint32_t)c, s->d_fp, s->d_tbase, s->d_err, s->d_terr, s->stream ) )
@@ -435,7 +440,7 @@ fd_ed25519_amd_verify_txns( fd_ed25519_amd_t * e, ulong txn_cnt, uchar const * p
       bsz += sz; ns += k2; c++;
     }
     s->h_tbase[c] = (uint32_t)ns;
-    if( (rc = fd_amd_slot_launch_txn( s, c, ns, bsz, txn_err + t, sig_err ? sig_err + gsig : NULL, 0 )) ) return rc;
+    if( (rc = fd_amd_slot_launch_txn( s, c, ns, bsz, txn_err + t, sig_err ? sig_err + gsig : NULL, 0, NULL )) ) return rc;
     t += c; gsig += ns; k ^= 1;
   }
   for( int j=0; j<2; j++ ) if( (rc = fd_amd_slot_drain( &e->slot[j] )) ) return rc;

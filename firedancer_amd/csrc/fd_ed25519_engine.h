@@ -72,7 +72,8 @@ int  fd_amd_slot_alloc_aux( slot_t * s, ulong cap );
 /* Transaction chunk: c payloads staged in h_blob / h_toff / h_tsz with
    signature-slot bases h_tbase[0..c] (nslot = h_tbase[c]); per-transaction
    verdicts land in h_terr, slot tags in h_tag when want_tag. */
-int  fd_amd_slot_launch_txn( slot_t * s, ulong c, ulong nslot, ulong blob_sz, schar * t_out, schar * s_out, int want_tag );
+int  fd_amd_slot_launch_txn( slot_t * s, ulong c, ulong nslot, ulong blob_sz, schar * t_out, schar * s_out, int want_tag,
+                             uint8_t const * d_payload );   /* d_payload != NULL: payloads read in place (h_toff index it), no blob H2D */
 /* signature slots reserved for a payload (fd_txn_parse.c:79-82 rule) */
 ulong fd_amd_txn_slots1( uchar const * p, ulong sz );
 

@@ -193,7 +193,7 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
   /* zero copy: the input data region is mapped into the GPU; frags are
      handed over as (chunk, size) and gathered on the device */
   uint8_t const * zc_dev = NULL;
-  if( !txn && t->reg_base && (uint8_t const *)in_chunk0 >= t->reg_base &&
+  if( t->reg_base && (uint8_t const *)in_chunk0 >= t->reg_base &&
       (uint8_t const *)in_chunk0 < t->reg_base + t->reg_sz &&
       t->reg_sz - (ulong)((uint8_t const *)in_chunk0 - t->reg_base) <= (1UL << 32) )
     zc_dev = t->reg_dev + ((uint8_t const *)in_chunk0 - t->reg_base);
@@ -276,9 +276,15 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
           ulong ha_tag; memcpy( &ha_tag, p + 1, 8 );
           if( t->tc.insert( ha_tag ) ) { diag->ha_filt_cnt++; diag->ha_filt_sz += sz; continue; }
         }
-        memcpy( s->h_blob + blob_at, p, sz );
-        s->h_toff[staged] = (uint32_t)blob_at; s->h_tsz[staged] = (uint32_t)sz; s->h_tbase[staged] = (uint32_t)slots;
-        blob_at += sz; slots += k2;
+        if( zc_dev ) {                                                   /* zero copy: parsed in place */
+          s->h_toff[staged] = (uint32_t)(chunk << FD_CHUNK_LG_SZ);
+        } else {
+          memcpy( s->h_blob + blob_at, p, sz );
+          s->h_toff[staged] = (uint32_t)blob_at;
+          blob_at += sz;
+        }
+        s->h_tsz[staged] = (uint32_t)sz; s->h_tbase[staged] = (uint32_t)slots;
+        slots += k2;
       }
       t->meta[stage][staged] = pending_t{ (uint)chunk, (ushort)sz, (ushort)ctl, (uint)tsorig };
       if( !staged ) stage_t0 = now_ns();
@@ -301,7 +307,7 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
       s->dsm_mode = 0;
       if( txn ) {
         s->h_tbase[staged] = (uint32_t)slots;
-        if( (rc = fd_amd_slot_launch_txn( s, staged, slots, blob_at, NULL, NULL, 1 )) ) return rc;
+        if( (rc = fd_amd_slot_launch_txn( s, staged, slots, blob_at, NULL, NULL, 1, zc_dev )) ) return rc;
         diag->batch_sig_cnt += slots;
       } else if( zc_dev ) {
         if( (rc = fd_amd_slot_launch_zc( s, staged, zc_dev )) ) return rc;

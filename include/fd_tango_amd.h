@@ -128,9 +128,10 @@ fd_verify_amd_tile_delete( fd_verify_amd_tile_t * tile );
    that fails to parse counts as SV_FILT. */
 /* Zero-copy staging: map the host data region [base, base+sz) holding
    the input frags into the GPU (hipHostRegister).  When a run's in_chunk0
-   lies inside it and the framing is PUB_SIG_MSG, the tile hands the GPU
-   only (chunk, size) per frag; a gather kernel reads the 96 header bytes
-   and k_prep reads the message over PCIe in place (no host memcpy). */
+   lies inside it, the tile hands the GPU only (chunk, size) per frag (no
+   host memcpy): PUB_SIG_MSG frags are gathered by a kernel that reads the
+   96 header bytes, and k_prep reads the message over PCIe in place; TXN
+   frags are parsed and hashed in place. */
 int
 fd_verify_amd_tile_register_dcache( fd_verify_amd_tile_t * tile, void * base, ulong sz );
 

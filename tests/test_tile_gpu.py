@@ -140,7 +140,8 @@ def test_stream_bench_smoke():
     assert r["published"] == 20000 and r["sv_filt"] == 0
 
 
-def test_tile_txn_framing_vs_oracle():
+@pytest.mark.parametrize("zero_copy", [False, True])
+def test_tile_txn_framing_vs_oracle(zero_copy):
     """Frags carrying wire transactions (multi-signer, legacy + v0, some
     corrupted, some duplicated): the tile publishes exactly the
     transactions the oracle accepts (fd_txn_parse + every signature), in
@@ -173,6 +174,8 @@ def test_tile_txn_framing_vs_oracle():
     blob, off, sz = _txn.pack(pays)
     eterr, _, _ = _oracle.txn_verify_batch(blob, off, sz)
     tile = tango.VerifyTile(0, batch_max=64, tcache_depth=4096, framing=tango.VerifyTile.FRAMING_TXN)
+    if zero_copy:
+        tile.register_dcache(dcache)    # transactions parsed in place from the mapped data region
     try:
         diag, _ = tile.run(mc_in, dcache, 0, mc_out, 0, len(order))
     finally:
