@@ -67,9 +67,25 @@ def build_oracle(verbose=False):
         subprocess.check_call(["make", "-C", od, "-j8", "ref", "tools"], stdout=out)
 
 
+def build_clients(verbose=False):
+    """Plain-C callers of the boundary (gcc, include/*.h only, linked against
+    the built library): tests/c/dropin_client."""
+    src = os.path.join(ROOT, "tests", "c", "dropin_client.c")
+    exe = os.path.join(ROOT, "tests", "c", "dropin_client")
+    cmd = ["gcc", "-O2", "-std=gnu11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), src,
+           "-L", os.path.join(ROOT, "firedancer_amd"), "-lfd_ed25519_amd",
+           "-Wl,-rpath,$ORIGIN/../../firedancer_amd", "-o", exe]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    return exe
+
+
 def build(force=False, verbose=False):
     build_oracle(verbose)
-    return build_engine(force, verbose)
+    so = build_engine(force, verbose)
+    build_clients(verbose)
+    return so
 
 
 if __name__ == "__main__":

@@ -99,3 +99,32 @@ int main( void ) {
                            "-L", libdir, "-lfd_ed25519_amd", "-Wl,-rpath," + libdir, "-o", str(exe)])
     out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
     assert out[0] == "bad" and out[1] == "message"
+
+
+CLIENT = os.path.join(ROOT, "tests", "c", "dropin_client")
+
+
+def _client():
+    if not os.path.exists(CLIENT):          # built by __graft_entry__.build(); build it here if missing
+        from firedancer_amd import build
+        build.build_clients()
+    return CLIENT
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="GPU host: see the gpu test")
+def test_plain_c_client_host_entry_points():
+    """tests/c/dropin_client.c: a gcc-compiled C caller that includes only
+    include/*.h and links the library by name, as a relinked Firedancer
+    would.  Host mode: RFC 8032 test 1 bytes, strerror, the engine refusing
+    to start without a device."""
+    r = subprocess.run([_client(), "cpu"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "dropin_client cpu: OK" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_plain_c_client_on_gpu():
+    """The same C caller on the GPU: fd_ed25519_verify codes, then 2000
+    signatures (10 % corrupted) through verify_soa and verify_batch, every
+    verdict equal to the drop-in call's."""
+    r = subprocess.run([_client(), "gpu"], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and "dropin_client gpu: OK" in r.stdout, r.stdout + r.stderr
