@@ -326,27 +326,68 @@ FD_DEV int fe_isnegative( fe const & f ) { i32 h[10]; fe_reduce( h, f ); return 
 
 __constant__ static u64 const SHA512_K[80] = FD_AMD_SHA512_K;
 
-FD_DEV u64 rotr64( u64 x, int n ) { return (x >> n) | (x << (64-n)); }
+/* 64-bit rotate / shift on the two 32-bit halves with v_alignbit_b32 (two
+   instructions; the generic form costs two 64-bit shifts and two ORs).  n is
+   a compile-time constant at every call site. */
+FD_DEV u64 rotr64( u64 x, int n ) {
+  u32 lo = (u32)x, hi = (u32)(x >> 32);
+  if( n >= 32 ) { u32 t = lo; lo = hi; hi = t; n -= 32; }
+  if( !n ) return ((u64)hi << 32) | lo;
+  return ((u64)__builtin_amdgcn_alignbit( lo, hi, (u32)n ) << 32) | __builtin_amdgcn_alignbit( hi, lo, (u32)n );
+}
+FD_DEV u64 shr64( u64 x, int n ) {
+  u32 lo = (u32)x, hi = (u32)(x >> 32);
+  return ((u64)(hi >> n) << 32) | __builtin_amdgcn_alignbit( hi, lo, (u32)n );
+}
+
+/* 3-input bitwise ops as one v_bitop3_b32 per half (gfx950): 0x96 = x^y^z,
+   0xE8 = majority (both symmetric in their inputs) */
+#define FD_BITOP3_64( x, y, z, LUT ) \
+  ( ((u64)(u32)__builtin_amdgcn_bitop3_b32( (u32)((x) >> 32), (u32)((y) >> 32), (u32)((z) >> 32), LUT ) << 32) | \
+    (u64)(u32)__builtin_amdgcn_bitop3_b32( (u32)(x), (u32)(y), (u32)(z), LUT ) )
+
+/* One SHA-512 round on renamed state (FIPS 180-4 s6.4.2): the caller
+   rotates the argument order instead of moving a..h, so every index is
+   static and the state never moves between registers. */
+FD_DEV void
+sha512_round( u64 a, u64 b, u64 c, u64 & d, u64 e, u64 f, u64 g, u64 & h, u64 k, u64 w ) {
+  u64 S1 = FD_BITOP3_64( rotr64( e, 14 ), rotr64( e, 18 ), rotr64( e, 41 ), 0x96 );
+  u64 ch = (e & f) ^ (~e & g);
+  u64 t1 = h + S1 + ch + k + w;
+  u64 S0 = FD_BITOP3_64( rotr64( a, 28 ), rotr64( a, 34 ), rotr64( a, 39 ), 0x96 );
+  u64 mj = FD_BITOP3_64( a, b, c, 0xE8 );
+  d += t1;
+  h  = t1 + S0 + mj;
+}
+
+/* 8 rounds starting at round r (r % 8 == 0), message words w[j0 .. j0+7] */
+FD_DEV void
+sha512_round8( u64 & a, u64 & b, u64 & c, u64 & d, u64 & e, u64 & f, u64 & g, u64 & h, int r, u64 const * w ) {
+  sha512_round( a, b, c, d, e, f, g, h, SHA512_K[r+0], w[0] );
+  sha512_round( h, a, b, c, d, e, f, g, SHA512_K[r+1], w[1] );
+  sha512_round( g, h, a, b, c, d, e, f, SHA512_K[r+2], w[2] );
+  sha512_round( f, g, h, a, b, c, d, e, SHA512_K[r+3], w[3] );
+  sha512_round( e, f, g, h, a, b, c, d, SHA512_K[r+4], w[4] );
+  sha512_round( d, e, f, g, h, a, b, c, SHA512_K[r+5], w[5] );
+  sha512_round( c, d, e, f, g, h, a, b, SHA512_K[r+6], w[6] );
+  sha512_round( b, c, d, e, f, g, h, a, SHA512_K[r+7], w[7] );
+}
 
 FD_DEV void sha512_compress( u64 st[8], u64 w[16] ) {
   u64 a=st[0], b=st[1], c=st[2], d=st[3], e=st[4], f=st[5], g=st[6], h=st[7];
-  _Pragma("unroll 16")
-  for( int i=0; i<80; i++ ) {
-    u64 wi;
-    if( i < 16 ) wi = w[i & 15];
-    else {
-      u64 w15 = w[(i-15) & 15], w2 = w[(i-2) & 15];
-      u64 s0 = rotr64( w15, 1 ) ^ rotr64( w15, 8 ) ^ (w15 >> 7);
-      u64 s1 = rotr64( w2, 19 ) ^ rotr64( w2, 61 ) ^ (w2 >> 6);
-      wi = w[i & 15] + s0 + w[(i-7) & 15] + s1;
-      w[i & 15] = wi;
+  sha512_round8( a, b, c, d, e, f, g, h, 0, w     );
+  sha512_round8( a, b, c, d, e, f, g, h, 8, w + 8 );
+  _Pragma("unroll 1")
+  for( int r=16; r<80; r+=16 ) {
+    /* message schedule for rounds r .. r+15 in place: w[k] <- W[r+k] */
+    _Pragma("unroll") for( int k=0; k<16; k++ ) {
+      u64 w15 = w[(k+1) & 15], w2 = w[(k+14) & 15];
+      u64 s0 = FD_BITOP3_64( rotr64( w15, 1 ), rotr64( w15, 8 ), shr64( w15, 7 ), 0x96 );
+      u64 s1 = FD_BITOP3_64( rotr64( w2, 19 ), rotr64( w2, 61 ), shr64( w2, 6 ), 0x96 );
+      w[k] = w[k] + s0 + w[(k+9) & 15] + s1;
     }
-    u64 S1 = rotr64( e, 14 ) ^ rotr64( e, 18 ) ^ rotr64( e, 41 );
-    u64 ch = (e & f) ^ (~e & g);
-    u64 t1 = h + S1 + ch + SHA512_K[i] + wi;
-    u64 S0 = rotr64( a, 28 ) ^ rotr64( a, 34 ) ^ rotr64( a, 39 );
-    u64 mj = (a & b) ^ (a & c) ^ (b & c);
-    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+    sha512_round8( a, b, c, d, e, f, g, h, r,     w     );
+    sha512_round8( a, b, c, d, e, f, g, h, r + 8, w + 8 );
   }
   st[0]+=a; st[1]+=b; st[2]+=c; st[3]+=d; st[4]+=e; st[5]+=f; st[6]+=g; st[7]+=h;
 }
