@@ -574,7 +574,7 @@ fd_ed25519_amd_debug_digits_dev( ulong n, void const * d_ws, ushort * d_dig, int
   if( !n ) return FD_ED25519_AMD_OK;
   ws_layout_t L = fd_amd_ws_layout( n );
   uint8_t const * ws = (uint8_t const *)d_ws;
-  HIPCHK( hipMemcpyAsync( d_dig, ws + L.dig, 512UL*n, hipMemcpyDeviceToDevice, (hipStream_t)stream ) );
+  if( fd_amd_launch_digits_dense( (uint32_t)n, d_ws, d_dig, (hipStream_t)stream ) ) return FD_ED25519_AMD_ERR_DEVICE;
   HIPCHK( hipMemcpyAsync( d_top, ws + L.top, 4UL*n,   hipMemcpyDeviceToDevice, (hipStream_t)stream ) );
   return FD_ED25519_AMD_OK;
 }

@@ -9,7 +9,7 @@
 
 typedef struct {
   size_t N;      /* n rounded up to 64 */
-  size_t dig, top, A, R, Ai, st, tag, ds;   /* byte offsets of the workspace planes */
+  size_t dig, evn, top, A, R, Ai, st, tag, ds;   /* byte offsets of the workspace planes */
   size_t total;  /* footprint in bytes */
 } ws_layout_t;
 
@@ -54,6 +54,11 @@ int fd_amd_launch_sign( uint32_t n, uint8_t const * d_prv, uint32_t const * d_of
    planes, msg_off relative to d_dc. */
 int fd_amd_launch_zgather( uint32_t n, uint32_t const * d_chunk, uint32_t const * d_fsz, uint8_t const * d_dc,
                            uint8_t * d_pub, uint8_t * d_sig, uint32_t * d_off, uint32_t * d_sz, hipStream_t stream );
+
+/* Dense slide digits of the last call on workspace d_ws (debug): u16
+   [n][256] (low byte h digit, high byte s digit) rebuilt from the event
+   lists k_prep writes. */
+int fd_amd_launch_digits_dense( uint32_t n, void const * d_ws, uint16_t * d_dig, hipStream_t stream );
 
 /* 1 when a batch of n takes the latency kernels (k_front + k_dsm4). */
 int fd_amd_uses_latency_path( uint32_t n, int dsm_mode );

@@ -54,7 +54,8 @@ fd_amd_ws_layout( size_t n ) {
   size_t N = (n + 63UL) & ~(size_t)63UL; if( !N ) N = 64;
   size_t o = 0;
   L.N   = N;
-  L.dig = o; o = ws_al( o + 2UL*256UL*N );   /* u16 [N][256] */
+  L.dig = o; o = ws_al( o + 2UL*128UL*N );   /* u16 [N][128] digit events: h [0,64), s [64,128) */
+  L.evn = o; o = ws_al( o + 4UL*N );          /* u32 [N]: h event count | s count << 8 */
   L.top = o; o = ws_al( o + 4UL*N );
   L.A   = o; o = ws_al( o + 4UL*30UL*N );
   L.R   = o; o = ws_al( o + 4UL*20UL*N );
@@ -121,6 +122,7 @@ prep_body( u32 i, u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ si
   if( i >= n ) return;
   if( skip && skip[i] ) {   /* slot of a transaction that failed to parse (fd_txn_kernels.hip) */
     ((int *)(ws + L.top))[i] = -1;
+    ((u32 *)(ws + L.evn))[i] = 0u;
     ((u64 *)(ws + L.tag))[i] = 0UL;
     err[i] = (i8)skip[i];
     return;
@@ -151,7 +153,8 @@ prep_body( u32 i, u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ si
     }
   }
 
-  u16 * dig = (u16 *)(ws + L.dig) + (size_t)i*256u;
+  u64 * evw = (u64 *)(ws + L.dig) + (size_t)i*32u;   /* this signature's event row: 16 words h, 16 words s */
+  u32 nh = 0u, ns = 0u;
   int top = -1;
   u64 tag = 0UL;
   u64 st[8] = FD_AMD_SHA512_H0;
@@ -186,13 +189,28 @@ prep_body( u32 i, u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ si
     u32 h[8];
     sc_reduce( h, hd );
 
-    /* digits: per-lane contiguous (da, db) u16 pairs, zero-filled first */
-    uint4 * d4 = (uint4 *)dig;
-    _Pragma("unroll 8") for( int k=0; k<32; k++ ) d4[k] = make_uint4( 0u, 0u, 0u, 0u );
-    u8 * db8 = (u8 *)dig;
-    slide_reg( h,  [&]( int pos, int r ) { db8[2*pos]     = (u8)(i8)r; top = max( top, pos ); } );
-    slide_reg( sw, [&]( int pos, int r ) { db8[2*pos + 1] = (u8)(i8)r; top = max( top, pos ); } );
+    /* digits as sparse EVENTS, u16 = position | digit << 8, ascending, four
+       per 64-bit word (the consumer walks them from the top).  Consecutive
+       nonzero digits of the slide are >= 5 positions apart (bits i+1..i+4
+       are always absorbed), so a 253-bit scalar has at most 52 events: the
+       16-word halves never overflow.  Only the words holding events are
+       written -- no dense 256-entry row, no zero fill. */
+    u64 buf = 0UL;
+    slide_reg( h, [&]( int pos, int r ) {
+      buf |= (u64)((u32)pos | ((u32)(u8)(i8)r << 8)) << (16u*(nh & 3u));
+      if( !(++nh & 3u) ) { evw[(nh >> 2) - 1u] = buf; buf = 0UL; }
+      top = max( top, pos );
+    } );
+    if( nh & 3u ) evw[nh >> 2] = buf;
+    buf = 0UL;
+    slide_reg( sw, [&]( int pos, int r ) {
+      buf |= (u64)((u32)pos | ((u32)(u8)(i8)r << 8)) << (16u*(ns & 3u));
+      if( !(++ns & 3u) ) { evw[16u + (ns >> 2) - 1u] = buf; buf = 0UL; }
+      top = max( top, pos );
+    } );
+    if( ns & 3u ) evw[16u + (ns >> 2)] = buf;
   }
+  ((u32 *)(ws + L.evn))[i] = nh | (ns << 8);
   ((int *)(ws + L.top))[i] = top;
   ((u64 *)(ws + L.tag))[i] = tag;
   err[i] = (i8)code;
@@ -371,6 +389,22 @@ __device__ __forceinline__ i32 vsel( u64 m, i32 t, i32 f ) {
 
 enum { PH_DBL = 0, PH_ADDA = 1, PH_ADDB = 2, PH_FIN = 3, PH_DONE = 4 };
 
+/* One scalar's slide-digit events (k_prep), walked from the top.  The
+   kernel first copies the signature's event row into LDS, so a pop is one
+   ds_read_u16 (an LDS wait, not a memory wait, when it lands in a
+   divergent branch). */
+struct evq {
+  u16 const * e;     /* the list in LDS */
+  int j, pos, dig;   /* current event index (descending), its position (-1: none left) and digit */
+  __device__ __forceinline__ void load() {
+    u32 x = (j >= 0) ? (u32)e[j] : 0xffffu;
+    pos = (j >= 0) ? (int)(x & 0xffu) : -1;
+    dig = (int)(i8)(x >> 8);
+  }
+  __device__ __forceinline__ void init( u16 const * e_, int n ) { e = e_; j = n - 1; load(); }
+  __device__ __forceinline__ void pop() { j--; load(); }
+};
+
 /* k_dsm: [h](-A) + [s]B as a per-lane STEP STREAM.
  *
  * The reference loop (avx/fd_ed25519_ge.c:488-523) is, per bit position p
@@ -458,12 +492,20 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
   }
 
   /* lane state */
-  u64 const * dg = (u64 const *)((u16 const *)(ws + L.dig) + (size_t)ii*256u);
+  u64 const * dg = (u64 const *)(ws + L.dig) + (size_t)ii*32u;
   int p   = act ? ((int const *)(ws + L.top))[ii] : -1;
   int ph  = act ? (p >= 0 ? PH_DBL : PH_FIN) : PH_DONE;
-  u64 dc  = (p >= 0) ? dg[p >> 2] : 0UL;             /* digits of the 4-position group of p */
-  u64 dn  = (p >= 4) ? dg[(p >> 2) - 1] : 0UL;       /* next (lower) group, prefetched */
-  int cur = (int)((dc >> (16 * (p & 3))) & 0xffffu); /* (a_p, b_p) as int8 pair */
+  evq eva, evb;                                      /* digit events of h and s */
+  {
+    __shared__ u64 evl[64][33];                      /* this wave's event rows (33: bank spread) */
+    u64 * row = evl[threadIdx.x];
+    u32 ne = act ? ((u32 const *)(ws + L.evn))[ii] : 0u;
+    u32 wa = ((ne & 0xffu) + 3u) >> 2, wb = (((ne >> 8) & 0xffu) + 3u) >> 2;
+    for( u32 k=0; k<wa; k++ ) row[k]       = dg[k];
+    for( u32 k=0; k<wb; k++ ) row[16u + k] = dg[16u + k];
+    eva.init( (u16 const *)row,        (int)(ne & 0xffu) );
+    evb.init( (u16 const *)(row + 16), (int)((ne >> 8) & 0xffu) );
+  }
   i32 const * Rw = (i32 const *)(ws + L.R);
   u32 nha = 0, nhb = 0;
   u32 nit = (u32)(p + 1);
@@ -549,21 +591,20 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
       t.T.v[k] = vsel( mD, dT, aT );
     }
 
-    /* advance the lane's op stream */
-    int da = (int)(i8)(cur & 0xff), db = (int)(i8)(cur >> 8);
+    /* advance the lane's op stream: the event just executed is consumed; the next op follows from the
+       event heads (an event at position p means a digit at p) */
+    if( ph == PH_ADDA ) eva.pop();
+    else if( ph == PH_ADDB ) evb.pop();
+    bool ha = eva.pos == p, hb = evb.pos == p;
+    int da = eva.dig, db = evb.dig;
     int nph;
-    if( ph == PH_DBL )       nph = da ? PH_ADDA : (db ? PH_ADDB : -1);
-    else if( ph == PH_ADDA ) nph = db ? PH_ADDB : -1;
+    if( ph == PH_DBL )       nph = ha ? PH_ADDA : (hb ? PH_ADDB : -1);
+    else if( ph == PH_ADDA ) nph = hb ? PH_ADDB : -1;
     else if( ph == PH_ADDB ) nph = -1;
     else                     nph = PH_DONE;
     if( nph == -1 ) {
       p--;
-      if( p < 0 ) nph = PH_FIN;
-      else {
-        if( (p & 3) == 3 ) { dc = dn; dn = (p >= 4) ? dg[(p >> 2) - 1] : 0UL; }
-        cur = (int)((dc >> (16 * (p & 3))) & 0xffffu);
-        nph = PH_DBL;
-      }
+      nph = (p < 0) ? PH_FIN : PH_DBL;
     }
     ph = nph;
 
@@ -875,12 +916,21 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
 #   undef AI_ROW4
   }
 
-  u64 const * dg = (u64 const *)((u16 const *)(ws + L.dig) + (size_t)ii*256u);
+  u64 const * dg = (u64 const *)(ws + L.dig) + (size_t)ii*32u;
   int p   = act ? ((int const *)(ws + L.top))[ii] : -1;
   int ph  = act ? (p >= 0 ? PH_DBL : PH_FIN) : PH_DONE;
-  u64 dc  = (p >= 0) ? dg[p >> 2] : 0UL;
-  u64 dn  = (p >= 4) ? dg[(p >> 2) - 1] : 0UL;
-  int cur = (int)((dc >> (16 * (p & 3))) & 0xffffu);
+  evq eva, evb;                                      /* digit events of h and s */
+  {
+    __shared__ u64 evl[16][33];                      /* one row per signature of the wave */
+    u64 * row = evl[threadIdx.x >> 2];
+    u32 ne = act ? ((u32 const *)(ws + L.evn))[ii] : 0u;
+    u32 wa = ((ne & 0xffu) + 3u) >> 2, wb = (((ne >> 8) & 0xffu) + 3u) >> 2;
+    for( u32 k=(u32)qd; k<wa; k+=4u ) row[k]       = dg[k];        /* the quad copies the row together */
+    for( u32 k=(u32)qd; k<wb; k+=4u ) row[16u + k] = dg[16u + k];
+    __syncthreads();
+    eva.init( (u16 const *)row,        (int)(ne & 0xffu) );
+    evb.init( (u16 const *)(row + 16), (int)((ne >> 8) & 0xffu) );
+  }
   i32 const * Rw = (i32 const *)(ws + L.R);
   u32 nha = 0, nhb = 0;
   u32 nit = (u32)(p + 1);
@@ -933,20 +983,20 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
     quad_body_own( t, pm, qrow, isD, mD, mN, qd );
 #endif
 
-    int da = (int)(i8)(cur & 0xff), db = (int)(i8)(cur >> 8);
+    /* the event just executed is consumed; the next op follows from the
+       event heads (an event at position p means a digit at p) */
+    if( ph == PH_ADDA ) eva.pop();
+    else if( ph == PH_ADDB ) evb.pop();
+    bool ha = eva.pos == p, hb = evb.pos == p;
+    int da = eva.dig, db = evb.dig;
     int nph;
-    if( ph == PH_DBL )       nph = da ? PH_ADDA : (db ? PH_ADDB : -1);
-    else if( ph == PH_ADDA ) nph = db ? PH_ADDB : -1;
+    if( ph == PH_DBL )       nph = ha ? PH_ADDA : (hb ? PH_ADDB : -1);
+    else if( ph == PH_ADDA ) nph = hb ? PH_ADDB : -1;
     else if( ph == PH_ADDB ) nph = -1;
     else                     nph = PH_DONE;
     if( nph == -1 ) {
       p--;
-      if( p < 0 ) nph = PH_FIN;
-      else {
-        if( (p & 3) == 3 ) { dc = dn; dn = (p >= 4) ? dg[(p >> 2) - 1] : 0UL; }
-        cur = (int)((dc >> (16 * (p & 3))) & 0xffffu);
-        nph = PH_DBL;
-      }
+      nph = (p < 0) ? PH_FIN : PH_DBL;
     }
     ph = nph;
 
@@ -1008,6 +1058,26 @@ fd_amd_launch_zgather( uint32_t n, uint32_t const * d_chunk, uint32_t const * d_
 
 /* ------------------------------------------------------------------ */
 /* launch                                                               */
+
+/* debug: dense u16 [n][256] digits from the event lists */
+__global__ void __launch_bounds__(64)
+k_digits_dense( u32 n, u8 const * __restrict__ ws, ws_layout_t L, u16 * __restrict__ out ) {
+  u32 i = blockIdx.x * 64u + threadIdx.x;
+  if( i >= n ) return;
+  u16 * o = out + (size_t)i*256u;
+  for( int k=0; k<256; k++ ) o[k] = 0;
+  u32 ne = ((u32 const *)(ws + L.evn))[i];
+  u16 const * ev = (u16 const *)(ws + L.dig) + (size_t)i*128u;
+  for( u32 j=0; j<(ne & 0xffu); j++ )        { u16 e = ev[j];      o[e & 0xffu] = (u16)(o[e & 0xffu] | (e >> 8)); }
+  for( u32 j=0; j<((ne >> 8) & 0xffu); j++ ) { u16 e = ev[64u + j]; o[e & 0xffu] = (u16)(o[e & 0xffu] | (e & 0xff00u)); }
+}
+
+int
+fd_amd_launch_digits_dense( uint32_t n, void const * d_ws, uint16_t * d_dig, hipStream_t stream ) {
+  if( !n ) return 0;
+  hipLaunchKernelGGL( k_digits_dense, dim3((n + 63u)/64u), dim3(64), 0, stream, n, (u8 const *)d_ws, fd_amd_ws_layout( n ), d_dig );
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 /* device -> mapped host result copy: 16 B per lane where both ends are
    16-aligned (every result buffer is), bytes otherwise. */
