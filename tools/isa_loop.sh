@@ -25,13 +25,18 @@ for k in ("k_prep", "k_decomp", "k_dsm", "k_dsm4"):
     ins = [l.split()[0] for l in body if l.startswith("\t") and not l.strip().startswith(";") and not l.strip().startswith(".")]
     print("%-9s vgpr %s occ %s  static instrs %d" % (k, vg, occ, len(ins)))
     if k in ("k_dsm", "k_dsm4"):
-        # largest loop: header with "Inner Loop Header" whose back-edge is farthest
-        hdrs = [(n, re.match(r"^(\.LBB\d+_\d+):", body[n]).group(1)) for n in range(len(body)) if "Loop Header" in body[n]]
+        # largest loop: any label with a backward branch to it, farthest back-edge wins
+        labs = {}
+        for n in range(len(body)):
+            m = re.match(r"^(\.LBB\d+_\d+):", body[n])
+            if m: labs[m.group(1)] = n
         best = None
-        for n, lab in hdrs:
-            ends = [m for m in range(n, len(body)) if re.search(r"s_(c)?branch\w*\s+" + re.escape(lab) + r"$", body[m])]
-            if ends and (best is None or ends[-1] - n > best[1] - best[0]):
-                best = (n, ends[-1])
+        for m_ in range(len(body)):
+            mm = re.search(r"s_(?:c)?branch\w*\s+(\.LBB\d+_\d+)\s*$", body[m_])
+            if mm and mm.group(1) in labs and labs[mm.group(1)] < m_:
+                n = labs[mm.group(1)]
+                if best is None or m_ - n > best[1] - best[0]:
+                    best = (n, m_)
         loop = [l.split()[0] for l in body[best[0]:best[1]+1] if l.startswith("\t") and not l.strip().startswith(";")]
         c = collections.Counter(loop)
         heavy = sum(v for k2, v in c.items() if k2.startswith(("v_mad_i64", "v_mad_u64", "v_mul_lo", "v_lshl_add_u64", "v_ashrrev_i64", "v_lshrrev_b64", "v_lshlrev_b64", "v_mul_hi")))
