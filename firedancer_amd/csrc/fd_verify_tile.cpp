@@ -27,6 +27,8 @@
 #include <string.h>
 #include <time.h>
 #include <thread>
+#include <sched.h>
+#include <pthread.h>
 #include <vector>
 #include <atomic>
 #include <algorithm>
@@ -354,6 +356,23 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
     fd_verify_amd_tile_delete( tile ); free( dcache ); return FD_ED25519_AMD_ERR_DEVICE;
   }
 
+  /* the three spinning threads (producer, tile, consumer) each get a CPU of
+     their own from the process's allowed set, so the scheduler does not
+     stack them (the saturated rate otherwise varies run to run) */
+  cpu_set_t allowed, saved; CPU_ZERO( &allowed ); CPU_ZERO( &saved );
+  int cpus[3] = { -1, -1, -1 }, ncpu = 0;
+  bool pin = !sched_getaffinity( 0, sizeof allowed, &allowed ) && CPU_COUNT( &allowed ) >= 4;
+  if( pin ) {
+    saved = allowed;
+    for( int c=0; c<CPU_SETSIZE && ncpu<3; c++ ) if( CPU_ISSET( c, &allowed ) ) cpus[ncpu++] = c;
+    pin = ncpu == 3;
+  }
+  auto pin_to = [&]( int k ) {
+    if( !pin ) return;
+    cpu_set_t one; CPU_ZERO( &one ); CPU_SET( cpus[k], &one );
+    (void)pthread_setaffinity_np( pthread_self(), sizeof one, &one );
+  };
+
   std::atomic<ulong> in_fseq( 0UL ), out_fseq( 0UL );   /* consumer progress (credits) */
   std::vector<uint> lat( frag_cnt );
   fd_verify_amd_diag_t diag; memset( &diag, 0, sizeof diag );
@@ -361,6 +380,7 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   ulong t0 = now_ns();
 
   std::thread prod( [&]() {
+    pin_to( 1 );
     ulong p0 = now_ns();
     for( ulong seq=0; seq<frag_cnt; seq++ ) {
       ulong due = rate > 0.0 ? p0 + (ulong)((double)seq * 1e9 / rate) : 0UL;   /* paced: open loop */
@@ -374,6 +394,7 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
     }
   } );
   std::thread cons( [&]() {
+    pin_to( 2 );
     ulong seq = 0;
     for( ;; ) {
       if( __atomic_load_n( &tile_rc, __ATOMIC_ACQUIRE ) == 1 ) {   /* tile finished: drain what is there */
@@ -385,11 +406,13 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
     }
   } );
   ulong const * ofs = (ulong const *)&out_fseq;
+  pin_to( 0 );
   int rc = fd_verify_amd_tile_run( tile, in_mc.data(), depth, dcache, 0UL, out_mc.data(), depth, 0UL, ofs,
                                    frag_cnt, NULL, &diag, lat.data(), frag_cnt );
   ulong t1 = now_ns();
   __atomic_store_n( &tile_rc, 1, __ATOMIC_RELEASE );
   prod.join(); cons.join();
+  if( pin ) (void)pthread_setaffinity_np( pthread_self(), sizeof saved, &saved );
   fd_verify_amd_tile_delete( tile );
   free( dcache );
   if( rc ) return rc;
