@@ -39,7 +39,7 @@ struct slot_t {
   ulong      s_n;
 };
 
-#define FD_AMD_SLOT_MAX (6)
+#define FD_AMD_SLOT_MAX (16)
 
 struct fd_ed25519_amd {
   int    device;

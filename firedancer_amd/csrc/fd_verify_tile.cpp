@@ -26,6 +26,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <x86intrin.h>
 #include <thread>
 #include <sched.h>
 #include <pthread.h>
@@ -100,9 +101,37 @@ struct pending_t {            /* one staged / in-flight frag */
   uint   tsorig;
 };
 
-inline ulong now_ns( void ) {
+inline ulong mono_ns( void ) {
   struct timespec ts; clock_gettime( CLOCK_MONOTONIC, &ts );
   return (ulong)ts.tv_sec * 1000000000UL + (ulong)ts.tv_nsec;
+}
+
+/* CLOCK_MONOTONIC nanoseconds read from the invariant TSC (as the
+   reference stamps frags with fd_tickcount, not a syscall-class clock):
+   clock_gettime costs ~20 ns, a per-frag cost on both sides of the tile at
+   ~20 M frags/s.  Calibrated once against CLOCK_MONOTONIC over 20 ms. */
+struct tsc_clock_t {
+  ulong  ns0, tsc0;
+  double ns_per_tick;
+  tsc_clock_t() {
+    ulong a_ns = mono_ns(), a_t = __rdtsc();
+    while( mono_ns() - a_ns < 20000000UL ) { /* spin */ }
+    ulong b_ns = mono_ns(), b_t = __rdtsc();
+    ns_per_tick = (double)(b_ns - a_ns) / (double)(b_t - a_t);
+    ns0 = b_ns; tsc0 = b_t;
+  }
+};
+
+int g_clock_tsc = -1;   /* FD_AMD_TILE_CLOCK=mono selects clock_gettime (A/B) */
+
+inline ulong now_ns( void ) {
+  static tsc_clock_t const c;
+  if( __builtin_expect( g_clock_tsc < 0, 0 ) ) {
+    char const * v = getenv( "FD_AMD_TILE_CLOCK" );
+    g_clock_tsc = !(v && !strcmp( v, "mono" ));
+  }
+  if( !g_clock_tsc ) return mono_ns();
+  return c.ns0 + (ulong)((double)(long)(__rdtsc() - c.tsc0) * c.ns_per_tick);
 }
 
 } /* namespace */
@@ -143,7 +172,8 @@ fd_verify_amd_tile_set_framing( fd_verify_amd_tile_t * t, int framing ) {
   return FD_ED25519_AMD_OK;
 }
 
-#define TILE_NSLOT (4)   /* batches in flight: one wave's verify takes ~0.7 ms, so small
+#define TILE_NSLOT (4)   /* batches in flight (FD_AMD_TILE_NSLOT overrides; 6 or 8 measured: higher
+                            p50 at every batch_max, higher saturated rate only at 16384): one wave's verify takes ~0.7 ms, so small
                             batches need several in flight to keep the GPU busy */
 
 extern "C" uint
@@ -154,15 +184,18 @@ fd_verify_amd_tickcount( void ) {
 extern "C" fd_verify_amd_tile_t *
 fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong tcache_depth ) {
   if( !batch_max ) return NULL;
-  fd_ed25519_amd_t * eng = fd_amd_engine_new( device, batch_max, batch_max * FD_ED25519_AMD_MSG_MAX, TILE_NSLOT );
+  int nslot = TILE_NSLOT;
+  if( char const * v = getenv( "FD_AMD_TILE_NSLOT" ) ) nslot = atoi( v );
+  if( nslot < 2 || nslot > FD_AMD_SLOT_MAX ) return NULL;
+  fd_ed25519_amd_t * eng = fd_amd_engine_new( device, batch_max, batch_max * FD_ED25519_AMD_MSG_MAX, nslot );
   if( !eng ) return NULL;
-  for( int k=0; k<TILE_NSLOT; k++ )
+  for( int k=0; k<nslot; k++ )
     if( fd_amd_slot_alloc_aux( &eng->slot[k], batch_max ) ) { fd_ed25519_amd_delete( eng ); return NULL; }
   fd_verify_amd_tile_t * t = new fd_verify_amd_tile_t();
-  t->eng = eng; t->batch_max = batch_max; t->wait_ns = batch_wait_ns; t->nslot = TILE_NSLOT;
+  t->eng = eng; t->batch_max = batch_max; t->wait_ns = batch_wait_ns; t->nslot = nslot;
   t->framing = FD_VERIFY_AMD_FRAMING_PUB_SIG_MSG;
   t->tc.init( tcache_depth );
-  for( int k=0; k<TILE_NSLOT; k++ ) t->meta[k].resize( batch_max );
+  for( int k=0; k<nslot; k++ ) t->meta[k].resize( batch_max );
   return t;
 }
 
@@ -303,9 +336,13 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
     bool greedy = idle_in && (!t->wait_ns || !nfly);
     if( staged && ( staged == t->batch_max || full || greedy || done_in ||
                     (t->wait_ns && now_ns() - stage_t0 >= t->wait_ns) ) ) {
-      /* kernel path by batch size (tile batches are small next to the GPU,
-         so even with 4 in flight the 4-lane latency kernels finish sooner:
-         measured, forcing the 1-lane kernels when busy halved throughput) */
+      /* kernel path by batch size: tile batches are small next to the GPU,
+         so the 4-lane latency kernels are used even with 4 in flight.
+         Measured (tools/dbg/dbg_tile_policy.py history): switching batches
+         of >= 4096/8192 to the 1-lane kernel while others were in flight
+         lowered the saturated rate at every batch_max and doubled latency;
+         the in-flight work (4 x batch_max) is too small for the 1-lane
+         kernel to fill the GPU. */
       s->dsm_mode = 0;
       if( txn ) {
         s->h_tbase[staged] = (uint32_t)slots;

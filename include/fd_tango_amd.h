@@ -165,8 +165,11 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t *  tile,
                         uint *                  lat,
                         ulong                   lat_max );
 
-/* The tile's timestamp clock (tsorig/tspub units): nanoseconds of
-   CLOCK_MONOTONIC, low 32 bits (fd_frag_meta_ts_comp-style compression). */
+/* The tile's timestamp clock (tsorig/tspub units): nanoseconds on the
+   CLOCK_MONOTONIC scale, low 32 bits (fd_frag_meta_ts_comp-style
+   compression), read from the invariant TSC calibrated once against
+   CLOCK_MONOTONIC (the reference stamps frags with fd_tickcount;
+   FD_AMD_TILE_CLOCK=mono reads clock_gettime instead). */
 uint
 fd_verify_amd_tickcount( void );
 
