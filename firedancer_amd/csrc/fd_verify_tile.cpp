@@ -122,15 +122,15 @@ struct tsc_clock_t {
   }
 };
 
-int g_clock_tsc = -1;   /* FD_AMD_TILE_CLOCK=mono selects clock_gettime (A/B) */
+inline bool use_tsc( void ) {   /* FD_AMD_TILE_CLOCK=mono selects clock_gettime (A/B) */
+  char const * v = getenv( "FD_AMD_TILE_CLOCK" );
+  return !(v && !strcmp( v, "mono" ));
+}
 
 inline ulong now_ns( void ) {
+  static bool        const tsc = use_tsc();   /* thread-safe one-time init */
   static tsc_clock_t const c;
-  if( __builtin_expect( g_clock_tsc < 0, 0 ) ) {
-    char const * v = getenv( "FD_AMD_TILE_CLOCK" );
-    g_clock_tsc = !(v && !strcmp( v, "mono" ));
-  }
-  if( !g_clock_tsc ) return mono_ns();
+  if( !tsc ) return mono_ns();
   return c.ns0 + (ulong)((double)(long)(__rdtsc() - c.tsc0) * c.ns_per_tick);
 }
 

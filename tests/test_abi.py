@@ -67,6 +67,23 @@ def test_workspace_footprint_monotone():
     assert c % 256 == 0
 
 
+def test_tile_tickcount_tracks_monotonic_ns():
+    """fd_verify_amd_tickcount (TSC-derived) stays on the CLOCK_MONOTONIC
+    nanosecond scale: low 32 bits within 1 ms of time.monotonic_ns, and it
+    advances at the monotonic rate over a 50 ms interval (1 %)."""
+    import time
+    from firedancer_amd import ed25519
+    f = ed25519.lib().fd_verify_amd_tickcount
+    f.restype = ctypes.c_uint
+    f()                                               # one-time calibration
+    d = (f() - (time.monotonic_ns() & 0xFFFFFFFF)) & 0xFFFFFFFF
+    assert min(d, (1 << 32) - d) < 1_000_000
+    a, ma = f(), time.monotonic_ns()
+    time.sleep(0.05)
+    b, mb = f(), time.monotonic_ns()
+    assert abs(((b - a) & 0xFFFFFFFF) / (mb - ma) - 1.0) < 0.01
+
+
 def test_engine_fails_loudly_without_device():
     """On a host without a HIP device the engine must refuse, not fall back."""
     from firedancer_amd import ed25519, hip
