@@ -223,6 +223,12 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
   int   oldest = 0, nfly = 0;      /* in-flight ones are oldest, oldest+1, ... (mod K)      */
   ulong staged = 0, blob_at = 0, stage_t0 = 0, slots = 0;
   int   rc;
+  /* Flow-control state shared with other threads is exchanged in strides,
+     not per frag (the reference's tiles publish fseq and refresh credits
+     in housekeeping, fd_fctl): diag->in_cnt is published every 256 frags
+     and at the end of each staging pass; out_fseq is re-read only when the
+     cached credit runs out. */
+  ulong in_cnt = diag->in_cnt, out_cr = 0;
 
   bool txn = t->framing == FD_VERIFY_AMD_FRAMING_TXN;
   /* zero copy: the input data region is mapped into the GPU; frags are
@@ -242,9 +248,12 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
       if( bad ) { diag->sv_filt_cnt++; diag->sv_filt_sz += m.sz; continue; }
       /* dedup tag: the verify's SHA-512 tag of the (first) signature */
       ulong tag = txn ? s->h_tag[ s->h_tbase[i] ] : s->h_tag[i];
-      if( out_fseq && out_seq - __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) >= out_depth ) {
-        diag->backp_cnt++;         /* credit check against the slowest consumer */
-        while( out_seq - __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) >= out_depth ) { /* spin */ }
+      if( out_fseq && (long)(out_seq - out_cr) >= 0 ) {   /* credit check against the slowest consumer */
+        out_cr = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) + out_depth;
+        if( (long)(out_seq - out_cr) >= 0 ) {
+          diag->backp_cnt++;
+          do out_cr = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) + out_depth; while( (long)(out_seq - out_cr) >= 0 );
+        }
       }
       uint tspub = fd_verify_amd_tickcount();
       fd_mcache_publish( out_mcache, out_depth, out_seq, tag, m.chunk, m.sz, m.ctl, m.tsorig, tspub );
@@ -264,7 +273,7 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
       if( (rc = publish( oldest )) ) return rc;
       oldest = (oldest + 1) % K; nfly--;
     }
-    bool done_in = frag_cnt ? (diag->in_cnt >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
+    bool done_in = frag_cnt ? (in_cnt >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
     if( done_in && !staged && !nfly ) break;
     if( nfly == K ) continue;      /* every slot in flight: the staging slot is busy */
 
@@ -272,7 +281,8 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
     slot_t * s = &e->slot[stage];
     bool idle_in = false, full = false;
     while( !done_in && staged < t->batch_max ) {
-      if( frag_cnt && diag->in_cnt >= frag_cnt ) break;
+      if( frag_cnt && in_cnt >= frag_cnt ) break;
+      if( !(in_cnt & 255UL) ) __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
       fd_frag_meta_t const * m = in_mcache + (in_seq & (in_depth-1UL));
       ulong seq_found = __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE );
       long  d = (long)(seq_found - in_seq);
@@ -283,7 +293,7 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
       if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != in_seq ) { diag->ovrn_cnt++; in_seq++; continue; }
       uchar const * p = (uchar const *)fd_chunk_to_laddr_const( in_chunk0, chunk );
       in_seq++;
-      __atomic_store_n( &diag->in_cnt, diag->in_cnt + 1UL, __ATOMIC_RELEASE );
+      in_cnt++;
       if( !txn ) {
         if( sz < 96UL || sz - 96UL > FD_ED25519_AMD_MSG_MAX ) { diag->bad_frag_cnt++; continue; }
         ulong ha_tag; memcpy( &ha_tag, p + 32, 8 );                      /* first 8 signature bytes */
@@ -303,7 +313,7 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
         if( sz > FD_ED25519_AMD_MSG_MAX ) { diag->bad_frag_cnt++; continue; }
         ulong k2 = fd_amd_txn_slots1( p, sz );
         if( slots + k2 > t->batch_max ) {                              /* no room for its signatures: next batch */
-          in_seq--; __atomic_store_n( &diag->in_cnt, diag->in_cnt - 1UL, __ATOMIC_RELEASE );
+          in_seq--; in_cnt--;
           full = true;
           break;
         }
@@ -325,7 +335,8 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
       if( !staged ) stage_t0 = now_ns();
       staged++;
     }
-    done_in = frag_cnt ? (diag->in_cnt >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
+    __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
+    done_in = frag_cnt ? (in_cnt >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
 
     /* 3. adaptive launch (a free slot exists here): full batch, input
           momentarily drained (greedy: under light load batches stay small
@@ -418,12 +429,13 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
 
   std::thread prod( [&]() {
     pin_to( 1 );
-    ulong p0 = now_ns();
+    ulong p0 = now_ns(), cr = 0;   /* cr: first seq not covered by the cached credit */
     for( ulong seq=0; seq<frag_cnt; seq++ ) {
       ulong due = rate > 0.0 ? p0 + (ulong)((double)seq * 1e9 / rate) : 0UL;   /* paced: open loop */
       if( due ) while( now_ns() < due ) { /* spin */ }
-      /* credit: do not lap the tile's consumption of the input mcache */
-      while( seq - __atomic_load_n( &diag.in_cnt, __ATOMIC_ACQUIRE ) >= depth - 16UL ) { /* spin */ }
+      /* credit: do not lap the tile's consumption of the input mcache
+         (refreshed only when the cached credit runs out) */
+      while( seq >= cr ) cr = __atomic_load_n( &diag.in_cnt, __ATOMIC_ACQUIRE ) + depth - 16UL;
       ulong k = seq % pool_n, sz = 96UL + msg_sz[k];
       /* tsorig = the scheduled send time when paced, so producer stalls count as latency */
       uint tso = due ? (uint)due : fd_verify_amd_tickcount();
@@ -432,14 +444,17 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   } );
   std::thread cons( [&]() {
     pin_to( 2 );
-    ulong seq = 0;
+    ulong seq = 0, fseq = 0;   /* fseq: last value published to out_fseq (every 64 frags, or when idle) */
     for( ;; ) {
       if( __atomic_load_n( &tile_rc, __ATOMIC_ACQUIRE ) == 1 ) {   /* tile finished: drain what is there */
         fd_frag_meta_t const * m = &out_mc[ seq & (depth-1UL) ];
         if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != seq ) break;
       }
       fd_frag_meta_t const * m = &out_mc[ seq & (depth-1UL) ];
-      if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) == seq ) { seq++; out_fseq.store( seq, std::memory_order_release ); }
+      if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) == seq ) {
+        seq++;
+        if( seq - fseq >= 64UL ) { fseq = seq; out_fseq.store( seq, std::memory_order_release ); }
+      } else if( fseq != seq ) { fseq = seq; out_fseq.store( seq, std::memory_order_release ); }
     }
   } );
   ulong const * ofs = (ulong const *)&out_fseq;
