@@ -343,6 +343,15 @@ ge_p1p1_to_p3( p1p1 const & t ) {
   return u;
 }
 
+/* the same products as interleaved, carry-folded pairs (fe_mul_fold2) */
+__device__ __forceinline__ p3
+ge_p1p1_to_p3_fold( p1p1 const & t ) {
+  p3 u;
+  fe_mul_fold2( u.Z, t.Z, t.T, u.Y, t.Z, t.Y );
+  fe_mul_fold2( u.X, t.X, t.T, u.T, t.X, t.Y );
+  return u;
+}
+
 /* the add/sub (and madd/msub when qZ==1) body (:505-518).  qZ_one: the
    table Z lane is 1 (base-point table) so Z*1 is the carry chain. */
 template<bool QZ_ONE>
@@ -428,6 +437,9 @@ struct evq {
  */
 #ifndef FD_DSM_QLDS
 #define FD_DSM_QLDS 0      /* 1: stage the next op's table operand in LDS (LDS-DMA) instead of VGPRs */
+#endif
+#ifndef FD_DSM_FOLD
+#define FD_DSM_FOLD 1      /* 1: field muls as interleaved carry-folded pairs (fe_mul_fold2) */
 #endif
 #ifndef FD_DSM_WAVES
 #define FD_DSM_WAVES 0     /* >0: __launch_bounds__ min waves per SIMD */
@@ -537,7 +549,11 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
 
   for( ;; ) {
     /* p1p1 -> p3 (its X,Y,Z are the reference's p1p1 -> p2) */
+#if FD_DSM_FOLD
+    p3 u = ge_p1p1_to_p3_fold( t );
+#else
     p3 u = ge_p1p1_to_p3( t );
+#endif
 #if FD_DSM_QLDS
     asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );   /* LDS-DMA of q (issued last step) has landed */
 #endif
@@ -563,6 +579,20 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
     bool isD = (ph == PH_DBL);
     u64 mD = __builtin_amdgcn_ballot_w64( isD ), mN = __builtin_amdgcn_ballot_w64( qneg );
     fe m0, m1, m2, m3;
+#if FD_DSM_FOLD
+    {
+      fe a0, b0, a1, b1, a2, b2, a3, b3;
+      _Pragma("unroll") for( int k=0; k<10; k++ ) {
+        i32 xy = u.X.v[k] + u.Y.v[k];
+        a0.v[k] = xy;                                     b0.v[k] = vsel( mD, xy, QV( 2, k ) );
+        a1.v[k] = vsel( mD, u.Y.v[k], u.Y.v[k] - u.X.v[k] ); b1.v[k] = vsel( mD, u.Y.v[k], QV( 1, k ) );
+        a2.v[k] = vsel( mD, u.X.v[k], u.Z.v[k] );        b2.v[k] = vsel( mD, u.X.v[k], QV( 0, k ) );
+        a3.v[k] = vsel( mD, u.Z.v[k], u.T.v[k] );        b3.v[k] = vsel( mD, u.Z.v[k] + u.Z.v[k], QV( 3, k ) );
+      }
+      fe_mul_fold2( m0, a0, b0, m1, a1, b1 );
+      fe_mul_fold2( m2, a2, b2, m3, a3, b3 );
+    }
+#else
     {
       fe a, b;
       _Pragma("unroll") for( int k=0; k<10; k++ ) { i32 xy = u.X.v[k] + u.Y.v[k]; a.v[k] = xy; b.v[k] = vsel( mD, xy, QV( 2, k ) ); }
@@ -574,6 +604,7 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
       _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = vsel( mD, u.Z.v[k], u.T.v[k] ); b.v[k] = vsel( mD, u.Z.v[k] + u.Z.v[k], QV( 3, k ) ); }
       m3 = fe_mul( a, b );
     }
+#endif
     /* lanes that are done (PH_DONE) keep computing on don't-care values:
        nothing they compute is stored */
     _Pragma("unroll") for( int k=0; k<10; k++ ) {
