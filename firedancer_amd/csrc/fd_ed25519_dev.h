@@ -212,6 +212,44 @@ FD_DEV void fe_mul_fold2( fe & R1, fe const & F1, fe const & G1, fe & R2, fe con
   R2 = fe_carry_fold_out( b0, b1, b2, b3, b4, b5, b6, b7, b8, b9 );
 }
 
+/* Term i of column K of one fe_mul (same rule as fe_col2). */
+template<int K>
+FD_DEV void fe_term( int i, i32 const * f, i32 const * f_2, i32 const * g, i32 const * g_19, i64 & a ) {
+  int const j = (K - i + 10) % 10;
+  bool const dbl = (i & 1) && (j & 1), x19 = (i + j) >= 10;
+  a = mac( dbl ? f_2[i] : f[i], x19 ? g_19[j] : g[j], a );
+}
+
+/* One fe_mul with the carry fold for a lane that has no second product to
+   interleave with: the independent columns of the product are interleaved
+   instead (0,4,2,6,8 | 1,5 | 3,7,9).  Columns 1,3,5,7 start from the
+   previous column's carry; column 9 runs beside 3 and 7 from its own bias
+   and takes column 8's carry with an add.  Same limbs as fe_mul. */
+FD_DEV fe fe_mul_fold1( fe const & F, fe const & G ) {
+  i64 const kb = fd_opaque( (1L<<25) + (1L<<50) );
+  i64 const k8 = fd_opaque( 1L<<25 ), k9 = fd_opaque( 1L<<24 );   /* column 8 carries no bias for 9 */
+  i32 f_2[10], g_19[10];
+  _Pragma("unroll") for( int k=0; k<10; k++ ) { f_2[k] = wmul( F.v[k], 2 ); g_19[k] = wmul( G.v[k], 19 ); }
+  i32 const * f = F.v; i32 const * g = G.v;
+  i64 h0 = kb, h4 = kb, h2 = kb, h6 = kb, h8 = k8;
+  _Pragma("unroll") for( int i=0; i<10; i++ ) {
+    fe_term<0>( i, f, f_2, g, g_19, h0 ); fe_term<4>( i, f, f_2, g, g_19, h4 );
+    fe_term<2>( i, f, f_2, g, g_19, h2 ); fe_term<6>( i, f, f_2, g, g_19, h6 );
+    fe_term<8>( i, f, f_2, g, g_19, h8 );
+  }
+  i64 h1 = h0 >> 26, h5 = h4 >> 26;
+  _Pragma("unroll") for( int i=0; i<10; i++ ) { fe_term<1>( i, f, f_2, g, g_19, h1 ); fe_term<5>( i, f, f_2, g, g_19, h5 ); }
+  h2 += h1 >> 25; h6 += h5 >> 25;
+  i64 h3 = h2 >> 26, h7 = h6 >> 26, h9 = k9;
+  _Pragma("unroll") for( int i=0; i<10; i++ ) {
+    fe_term<3>( i, f, f_2, g, g_19, h3 ); fe_term<7>( i, f, f_2, g, g_19, h7 );
+    fe_term<9>( i, f, f_2, g, g_19, h9 );
+  }
+  h8 += h7 >> 25;
+  h9 += h8 >> 26;
+  return fe_carry_fold_out( h0, h1, h2, h3, h4, h5, h6, h7, h8, h9 );
+}
+
 /* FE_AVX_INL_SQN, one lane, n in {1,2} (avx/fd_ed25519_fe_avx_inl.h:592-674):
    55 products; the column sums are doubled before the carry when n==2. */
 template<int N>

@@ -796,11 +796,19 @@ quad_body_own( p1p1 & t, fe const & pm, fe const & qrow, bool isD, u64 mD, u64 m
 #ifndef FD_DSM4_OWNC
 #define FD_DSM4_OWNC 1
 #endif
+#ifndef FD_DSM4_FOLD
+#define FD_DSM4_FOLD 1     /* 1: the lane's field mul with the carry fold, columns interleaved (fe_mul_fold1) */
+#endif
+#if FD_DSM4_FOLD
+#define FD_DSM4_MUL fe_mul_fold1
+#else
+#define FD_DSM4_MUL fe_mul
+#endif
 __device__ __forceinline__ fe
 quad_p3_ownc( fe const & C ) {
   fe a, b;
   _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = qp<0,0,2,2>( C.v[k] ); b.v[k] = qp<1,3,1,3>( C.v[k] ); }
-  return fe_mul( a, b );
+  return FD_DSM4_MUL( a, b );
 }
 
 __device__ __forceinline__ i32
@@ -833,7 +841,7 @@ quad_body_ownc( fe & C, fe const & pm, fe const & qrow, bool isD, bool neg, u64 
     a.v[k] = av;
     b.v[k] = vsel( mD, (i32)((u32)av << sh), qrow.v[k] );
   }
-  fe m = fe_mul( a, b );
+  fe m = FD_DSM4_MUL( a, b );
   i32 s0 = neg ? -1 : 1;
   i32 x = isD ? (qd == 1 ? -1 : (qd == 3 ? 0 : 1)) : (qd >= 2 ? 1 : 0);
   i32 y = isD ? ((qd & 1) ? 1 : -1)               : (qd <= 1 ? 2 : (qd == 2 ? -1 : 1));
