@@ -212,6 +212,40 @@ FD_DEV void fe_mul_fold2( fe & R1, fe const & F1, fe const & G1, fe & R2, fe con
   R2 = fe_carry_fold_out( b0, b1, b2, b3, b4, b5, b6, b7, b8, b9 );
 }
 
+/* fe_mul_fold2 with every independent chain interleaved term by term: the
+   ten even columns of both products, then columns 1,5 (four chains), 3,7
+   (four), 9 (two).  Same limbs as fe_mul. */
+template<int K>
+FD_DEV void fe_term( int i, i32 const * f, i32 const * f_2, i32 const * g, i32 const * g_19, i64 & a );
+FD_DEV void fe_mul_fold2w( fe & R1, fe const & F1, fe const & G1, fe & R2, fe const & F2, fe const & G2 ) {
+  i64 const kb = fd_opaque( (1L<<25) + (1L<<50) );
+  i32 f1_2[10], g1_19[10], f2_2[10], g2_19[10];
+  _Pragma("unroll") for( int k=0; k<10; k++ ) {
+    f1_2[k] = wmul( F1.v[k], 2 ); g1_19[k] = wmul( G1.v[k], 19 );
+    f2_2[k] = wmul( F2.v[k], 2 ); g2_19[k] = wmul( G2.v[k], 19 );
+  }
+  i32 const * f1 = F1.v; i32 const * g1 = G1.v; i32 const * f2 = F2.v; i32 const * g2 = G2.v;
+# define FD_TA( K_, A_ ) fe_term<K_>( i, f1, f1_2, g1, g1_19, A_ )
+# define FD_TB( K_, B_ ) fe_term<K_>( i, f2, f2_2, g2, g2_19, B_ )
+  i64 a0 = kb, b0 = kb, a4 = kb, b4 = kb, a2 = kb, b2 = kb, a6 = kb, b6 = kb, a8 = kb, b8 = kb;
+  _Pragma("unroll") for( int i=0; i<10; i++ ) {
+    FD_TA( 0, a0 ); FD_TB( 0, b0 ); FD_TA( 4, a4 ); FD_TB( 4, b4 ); FD_TA( 2, a2 ); FD_TB( 2, b2 );
+    FD_TA( 6, a6 ); FD_TB( 6, b6 ); FD_TA( 8, a8 ); FD_TB( 8, b8 );
+  }
+  i64 a1 = a0 >> 26, b1 = b0 >> 26, a5 = a4 >> 26, b5 = b4 >> 26;
+  _Pragma("unroll") for( int i=0; i<10; i++ ) { FD_TA( 1, a1 ); FD_TB( 1, b1 ); FD_TA( 5, a5 ); FD_TB( 5, b5 ); }
+  a2 += a1 >> 25; b2 += b1 >> 25; a6 += a5 >> 25; b6 += b5 >> 25;
+  i64 a3 = a2 >> 26, b3 = b2 >> 26, a7 = a6 >> 26, b7 = b6 >> 26;
+  _Pragma("unroll") for( int i=0; i<10; i++ ) { FD_TA( 3, a3 ); FD_TB( 3, b3 ); FD_TA( 7, a7 ); FD_TB( 7, b7 ); }
+  a8 += a7 >> 25; b8 += b7 >> 25;
+  i64 a9 = a8 >> 26, b9 = b8 >> 26;
+  _Pragma("unroll") for( int i=0; i<10; i++ ) { FD_TA( 9, a9 ); FD_TB( 9, b9 ); }
+# undef FD_TA
+# undef FD_TB
+  R1 = fe_carry_fold_out( a0, a1, a2, a3, a4, a5, a6, a7, a8, a9 );
+  R2 = fe_carry_fold_out( b0, b1, b2, b3, b4, b5, b6, b7, b8, b9 );
+}
+
 /* Term i of column K of one fe_mul (same rule as fe_col2). */
 template<int K>
 FD_DEV void fe_term( int i, i32 const * f, i32 const * f_2, i32 const * g, i32 const * g_19, i64 & a ) {

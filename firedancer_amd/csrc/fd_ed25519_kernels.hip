@@ -344,11 +344,16 @@ ge_p1p1_to_p3( p1p1 const & t ) {
 }
 
 /* the same products as interleaved, carry-folded pairs (fe_mul_fold2) */
+#if FD_DSM_FOLD == 2
+#define FD_MUL2 fe_mul_fold2w
+#else
+#define FD_MUL2 fe_mul_fold2
+#endif
 __device__ __forceinline__ p3
 ge_p1p1_to_p3_fold( p1p1 const & t ) {
   p3 u;
-  fe_mul_fold2( u.Z, t.Z, t.T, u.Y, t.Z, t.Y );
-  fe_mul_fold2( u.X, t.X, t.T, u.T, t.X, t.Y );
+  FD_MUL2( u.Z, t.Z, t.T, u.Y, t.Z, t.Y );
+  FD_MUL2( u.X, t.X, t.T, u.T, t.X, t.Y );
   return u;
 }
 
@@ -439,7 +444,7 @@ struct evq {
 #define FD_DSM_QLDS 0      /* 1: stage the next op's table operand in LDS (LDS-DMA) instead of VGPRs */
 #endif
 #ifndef FD_DSM_FOLD
-#define FD_DSM_FOLD 1      /* 1: field muls as interleaved carry-folded pairs (fe_mul_fold2) */
+#define FD_DSM_FOLD 2      /* 1: field muls as interleaved carry-folded pairs (fe_mul_fold2); 2: every independent chain interleaved (fe_mul_fold2w, no s_nop) */
 #endif
 #ifndef FD_DSM_WAVES
 #define FD_DSM_WAVES 0     /* >0: __launch_bounds__ min waves per SIMD */
@@ -589,8 +594,8 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
         a2.v[k] = vsel( mD, u.X.v[k], u.Z.v[k] );        b2.v[k] = vsel( mD, u.X.v[k], QV( 0, k ) );
         a3.v[k] = vsel( mD, u.Z.v[k], u.T.v[k] );        b3.v[k] = vsel( mD, u.Z.v[k] + u.Z.v[k], QV( 3, k ) );
       }
-      fe_mul_fold2( m0, a0, b0, m1, a1, b1 );
-      fe_mul_fold2( m2, a2, b2, m3, a3, b3 );
+      FD_MUL2( m0, a0, b0, m1, a1, b1 );
+      FD_MUL2( m2, a2, b2, m3, a3, b3 );
     }
 #else
     {
