@@ -344,6 +344,9 @@ ge_p1p1_to_p3( p1p1 const & t ) {
 }
 
 /* the same products as interleaved, carry-folded pairs (fe_mul_fold2) */
+#ifndef FD_DSM_FOLD
+#define FD_DSM_FOLD 2      /* 1: field muls as interleaved carry-folded pairs (fe_mul_fold2); 2: every independent chain interleaved (fe_mul_fold2w, no s_nop) */
+#endif
 #if FD_DSM_FOLD == 2
 #define FD_MUL2 fe_mul_fold2w
 #else
@@ -442,9 +445,6 @@ struct evq {
  */
 #ifndef FD_DSM_QLDS
 #define FD_DSM_QLDS 0      /* 1: stage the next op's table operand in LDS (LDS-DMA) instead of VGPRs */
-#endif
-#ifndef FD_DSM_FOLD
-#define FD_DSM_FOLD 2      /* 1: field muls as interleaved carry-folded pairs (fe_mul_fold2); 2: every independent chain interleaved (fe_mul_fold2w, no s_nop) */
 #endif
 #ifndef FD_DSM_WAVES
 #define FD_DSM_WAVES 0     /* >0: __launch_bounds__ min waves per SIMD */
