@@ -1,7 +1,9 @@
 """The carry-chain rewrites used by the HIP field kernels give the
 reference's limbs (avx/fd_ed25519_fe_avx_inl.h:568-584) on every input:
-the biased chain (fe_carry_b) and the carry-folded chain (fe_sq_fold,
-fe_carry_fold_out in firedancer_amd/csrc/fd_ed25519_dev.h), modelled here
+the biased chain (fe_carry_b), the carry-folded chain (fe_sq_fold,
+fe_mul_fold2 / fe_mul_fold2w, fe_carry_fold_out) and the folded chain with
+an independent column 9 (fe_mul_fold1), all in
+firedancer_amd/csrc/fd_ed25519_dev.h, modelled here
 with Python integers (int64 semantics checked) over random and extreme
 column sums.  CPU only."""
 import random
@@ -84,6 +86,32 @@ def folded_carry(s):
     return fold_limbs(h, t0, t4, c0b, c4b)
 
 
+def folded_carry_k9(s):
+    """fe_mul_fold1: as folded_carry, but column 9 starts from its own bias
+    2^24 (it runs beside columns 3 and 7), column 8 from 2^25 alone, and
+    column 8's carry reaches 9 through an add."""
+    K = (1 << 25) + (1 << 50)
+    h = [0] * 10
+    for k in (0, 4, 2, 6):
+        h[k] = i64(K + s[k])
+    h[8] = i64((1 << 25) + s[8])
+    h[1] = i64((h[0] >> 26) + s[1])
+    h[5] = i64((h[4] >> 26) + s[5])
+    h[2] = i64(h[2] + (h[1] >> 25))
+    h[6] = i64(h[6] + (h[5] >> 25))
+    h[3] = i64((h[2] >> 26) + s[3])
+    h[7] = i64((h[6] >> 26) + s[7])
+    h[9] = i64((1 << 24) + s[9])
+    h[8] = i64(h[8] + (h[7] >> 25))
+    h[9] = i64(h[9] + (h[8] >> 26))
+    M26 = (1 << 26) - 1
+    t4 = (h[4] & M26) + (h[3] >> 25)
+    c4b = t4 >> 26
+    t0 = (h[0] & M26) + (h[9] >> 25) * 19
+    c0b = t0 >> 26
+    return fold_limbs(h, t0, t4, c0b, c4b)
+
+
 def test_carry_rewrites_match_reference_chain():
     rng = random.Random(7)
     bound = 1 << 61                  # |column sum| < 2^61.8 for the kernels' operand ranges
@@ -103,3 +131,4 @@ def test_carry_rewrites_match_reference_chain():
         r = ref_carry(s)
         assert biased_carry(s) == r, s
         assert folded_carry(s) == r, s
+        assert folded_carry_k9(s) == r, s
