@@ -344,6 +344,9 @@ ge_p1p1_to_p3( p1p1 const & t ) {
 }
 
 /* the same products as interleaved, carry-folded pairs (fe_mul_fold2) */
+#ifndef FD_DSM_REPAIR
+#define FD_DSM_REPAIR 1    /* 1: body pairs DBL Z*2Z with ADD Z*qZ (one fewer operand select per limb) */
+#endif
 #ifndef FD_DSM_FOLD
 #define FD_DSM_FOLD 2      /* 1: field muls as interleaved carry-folded pairs (fe_mul_fold2); 2: every independent chain interleaved (fe_mul_fold2w, no s_nop) */
 #endif
@@ -591,8 +594,14 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
         i32 xy = u.X.v[k] + u.Y.v[k];
         a0.v[k] = xy;                                     b0.v[k] = vsel( mD, xy, QV( 2, k ) );
         a1.v[k] = vsel( mD, u.Y.v[k], u.Y.v[k] - u.X.v[k] ); b1.v[k] = vsel( mD, u.Y.v[k], QV( 1, k ) );
+#if FD_DSM_REPAIR
+        /* DBL Z*2Z pairs with ADD Z*qZ (shared a = Z), DBL X^2 with ADD T*qT */
+        a2.v[k] = u.Z.v[k];                              b2.v[k] = vsel( mD, u.Z.v[k] + u.Z.v[k], QV( 0, k ) );
+        a3.v[k] = vsel( mD, u.X.v[k], u.T.v[k] );        b3.v[k] = vsel( mD, u.X.v[k], QV( 3, k ) );
+#else
         a2.v[k] = vsel( mD, u.X.v[k], u.Z.v[k] );        b2.v[k] = vsel( mD, u.X.v[k], QV( 0, k ) );
         a3.v[k] = vsel( mD, u.Z.v[k], u.T.v[k] );        b3.v[k] = vsel( mD, u.Z.v[k] + u.Z.v[k], QV( 3, k ) );
+#endif
       }
       FD_MUL2( m0, a0, b0, m1, a1, b1 );
       FD_MUL2( m2, a2, b2, m3, a3, b3 );
@@ -617,7 +626,12 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
       /* DBL mix [a-b-c, b+c, b-c, d-b+c] with a=m0 b=m1 c=m2 d=m3;
          ADD mix [P-M, P+M, 2Z+-T, 2Z-+T] with P=m0 M=m1 Z=m2 T=m3 */
       i32 z2 = A2 + A2;
+#if FD_DSM_FOLD && FD_DSM_REPAIR
+      /* DBL: m2 = 2Z^2, m3 = X^2 */
+      i32 dY = A1 + A3, dZ = A1 - A3, dX = A0 - dY, dT = A2 - dZ;
+#else
       i32 dX = A0 - A1 - A2, dY = A1 + A2, dZ = A1 - A2, dT = A3 - A1 + A2;
+#endif
       i32 aX = A0 - A1,      aY = A0 + A1;
       i32 zp = z2 + A3, zm = z2 - A3;
       i32 aZ = vsel( mN, zm, zp ), aT = vsel( mN, zp, zm );
