@@ -344,6 +344,9 @@ ge_p1p1_to_p3( p1p1 const & t ) {
 }
 
 /* the same products as interleaved, carry-folded pairs (fe_mul_fold2) */
+#ifndef FD_DSM_DEFER_FIN
+#define FD_DSM_DEFER_FIN 1 /* 1: finished lanes park R' and the limb compare runs once after the loop */
+#endif
 #ifndef FD_DSM_REPAIR
 #define FD_DSM_REPAIR 1    /* 1: body pairs DBL Z*2Z with ADD Z*qZ (one fewer operand select per limb) */
 #endif
@@ -549,9 +552,11 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
 # define Q_SET( R_, K_, V_ ) ( q[R_].v[K_] = (V_) )
 # define Q_GLOBAL( R_, K_, S_ ) ( q[R_].v[K_] = *(S_) )
 #endif
+#if !FD_DSM_DEFER_FIN
   if( ph == PH_FIN ) {   /* both scalars zero: R' = (0:1:1) */
     _Pragma("unroll") for( int k=0; k<10; k++ ) { Q_SET( 0, k, Rw[(size_t)k*N + ii] ); Q_SET( 1, k, Rw[(size_t)(10+k)*N + ii] ); }
   }
+#endif
   p1p1 t;   /* identity as a completed point: p1p1->p3 gives (0,1,1,0) */
   t.X = fe_zero(); t.Y = fe_one(); t.Z = fe_one(); t.T = fe_one();
 
@@ -567,6 +572,25 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
 #endif
 
     bool fin = (ph == PH_FIN);
+#if FD_DSM_DEFER_FIN
+    /* R' = u's (X, Y, Z) parks in the lane's own Ai rows (no ADD op reads
+       them any more); the compare runs once for the whole wave after the
+       loop instead of once per distinct finishing step */
+    if( __any( fin ) ) {
+      if( fin ) {
+        int4 * d_ = (int4 *)Ail;
+        d_[0] = make_int4( u.X.v[0], u.X.v[1], u.X.v[2], u.X.v[3] );
+        d_[1] = make_int4( u.X.v[4], u.X.v[5], u.X.v[6], u.X.v[7] );
+        d_[2] = make_int4( u.X.v[8], u.X.v[9], u.Y.v[0], u.Y.v[1] );
+        d_[3] = make_int4( u.Y.v[2], u.Y.v[3], u.Y.v[4], u.Y.v[5] );
+        d_[4] = make_int4( u.Y.v[6], u.Y.v[7], u.Y.v[8], u.Y.v[9] );
+        d_[5] = make_int4( u.Z.v[0], u.Z.v[1], u.Z.v[2], u.Z.v[3] );
+        d_[6] = make_int4( u.Z.v[4], u.Z.v[5], u.Z.v[6], u.Z.v[7] );
+        d_[7] = make_int4( u.Z.v[8], u.Z.v[9], 0, 0 );
+        ph = PH_DONE;
+      }
+    }
+#else
     if( __any( fin ) ) {
       if( fin ) {
         fe RX, RY;
@@ -579,6 +603,7 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
         ph = PH_DONE;
       }
     }
+#endif
     if( __all( ph == PH_DONE ) ) break;
 
     /* op body: 4 field muls with per-lane operands, paired so that DBL and
@@ -674,8 +699,10 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
       } while(0)
       Q_ROW( 0, 0 ); Q_ROW( 1, rowM ); Q_ROW( 2, rowP ); Q_ROW( 3, 3 );
 #     undef Q_ROW
+#if !FD_DSM_DEFER_FIN
     } else if( ph == PH_FIN ) {
       _Pragma("unroll") for( int k=0; k<10; k++ ) { Q_GLOBAL( 0, k, Rw + (size_t)k*N + ii ); Q_GLOBAL( 1, k, Rw + (size_t)(10+k)*N + ii ); }
+#endif
     } else if( ph == PH_ADDB ) {
       nhb++;
       int e = (db < 0 ? -db : db) >> 1;
@@ -693,6 +720,23 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
 # undef Q_SET
 # undef Q_GLOBAL
 
+#if FD_DSM_DEFER_FIN
+  /* the limb compare of fd_ed25519_user.c:417-425, once per wave */
+  if( act ) {
+    int4 const * s_ = (int4 const *)Ail;
+    int4 w0 = s_[0], w1 = s_[1], w2 = s_[2], w3 = s_[3], w4 = s_[4], w5 = s_[5], w6 = s_[6], w7 = s_[7];
+    fe X = {{ w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x, w2.y }};
+    fe Y = {{ w2.z, w2.w, w3.x, w3.y, w3.z, w3.w, w4.x, w4.y, w4.z, w4.w }};
+    fe Z = {{ w5.x, w5.y, w5.z, w5.w, w6.x, w6.y, w6.z, w6.w, w7.x, w7.y }};
+    fe RX, RY;
+    _Pragma("unroll") for( int k=0; k<10; k++ ) { RX.v[k] = Rw[(size_t)k*N + ii]; RY.v[k] = Rw[(size_t)(10+k)*N + ii]; }
+    fe xZ, yZ;
+    FD_MUL2( xZ, Z, RX, yZ, Z, RY );
+    bool eq = true;
+    _Pragma("unroll") for( int k=0; k<8; k++ ) eq = eq && (xZ.v[k] == X.v[k]) && (yZ.v[k] == Y.v[k]);
+    err[i] = (i8)(eq ? 0 : -3);
+  }
+#endif
   if( want_stats && i < n ) {
     u32 * st = (u32 *)(ws + L.st);
     st[i] = act ? nit : 0u; st[N + i] = act ? nha : 0u; st[2*N + i] = act ? nhb : 0u;
