@@ -859,6 +859,9 @@ quad_body_own( p1p1 & t, fe const & pm, fe const & qrow, bool isD, u64 mD, u64 m
 #ifndef FD_DSM4_OWNC
 #define FD_DSM4_OWNC 1
 #endif
+#ifndef FD_DSM4_DEFER_FIN
+#define FD_DSM4_DEFER_FIN 1 /* 1: finished quads park their products; the limb compare runs once after the loop */
+#endif
 #ifndef FD_DSM4_FOLD
 #define FD_DSM4_FOLD 1     /* 1: the lane's field mul with the carry fold, columns interleaved (fe_mul_fold1) */
 #endif
@@ -1038,10 +1041,12 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
   u32 nit = (u32)(p + 1);
   bool qneg = false;
   fe qrow = fe_zero();
+#if !FD_DSM4_DEFER_FIN
   /* lanes 0/1 hold R.X / R.Y for the final compare */
   if( ph == PH_FIN ) {
     _Pragma("unroll") for( int k=0; k<10; k++ ) qrow.v[k] = Rw[(size_t)((qd & 1)*10 + k)*N + ii];
   }
+#endif
 #if FD_DSM4_OWNC
   fe C = (qd == 2) ? fe_zero() : fe_one();   /* identity: own coordinate (Z, T, X, Y)[q] = (1, 1, 0, 1) */
 #else
@@ -1057,6 +1062,20 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
 #endif
 
     bool fin = (ph == PH_FIN);
+#if FD_DSM4_DEFER_FIN
+    /* each lane parks its own p1p1->p3 product in its row of entry 0 of the
+       signature's Ai table (no ADD op reads it any more); the compare runs
+       once after the loop */
+    if( __any( fin ) ) {
+      if( fin ) {
+        int4 * d_ = (int4 *)(Ail + qd*12);
+        d_[0] = make_int4( pm.v[0], pm.v[1], pm.v[2], pm.v[3] );
+        d_[1] = make_int4( pm.v[4], pm.v[5], pm.v[6], pm.v[7] );
+        d_[2] = make_int4( pm.v[8], pm.v[9], 0, 0 );
+        ph = PH_DONE;
+      }
+    }
+#else
     if( __any( fin ) ) {
       /* q0: Z*RX vs X, q1: Z*RY vs Y; lanes 2,3 compute don't-care values */
       fe Z, ref;
@@ -1074,6 +1093,7 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
         ph = PH_DONE;
       }
     }
+#endif
     if( __all( ph == PH_DONE ) ) break;
 
     bool isD = (ph == PH_DBL);
@@ -1120,10 +1140,37 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
         nhb++;
         _Pragma("unroll") for( int k=0; k<10; k++ ) qrow.v[k] = bi[e][row*10 + k];
       }
+#if !FD_DSM4_DEFER_FIN
     } else if( ph == PH_FIN ) {
       _Pragma("unroll") for( int k=0; k<10; k++ ) qrow.v[k] = Rw[(size_t)((qd & 1)*10 + k)*N + ii];
+#endif
     }
   }
+
+#if FD_DSM4_DEFER_FIN
+  /* the limb compare (fd_ed25519_user.c:417-425), once per wave, all lanes
+     converged: q0 Z*RX vs X, q1 Z*RY vs Y, quad AND */
+  {
+    fe pm;
+    int4 const * s_ = (int4 const *)(Ail + qd*12);
+    int4 x0 = s_[0], x1 = s_[1], x2 = s_[2];
+    pm.v[0] = x0.x; pm.v[1] = x0.y; pm.v[2] = x0.z; pm.v[3] = x0.w;
+    pm.v[4] = x1.x; pm.v[5] = x1.y; pm.v[6] = x1.z; pm.v[7] = x1.w;
+    pm.v[8] = x2.x; pm.v[9] = x2.y;
+    _Pragma("unroll") for( int k=0; k<10; k++ ) qrow.v[k] = Rw[(size_t)((qd & 1)*10 + k)*N + ii];
+    fe Z, ref;
+    _Pragma("unroll") for( int k=0; k<10; k++ ) {
+      Z.v[k] = qb<0>( pm.v[k] );
+      ref.v[k] = qp<2,1,2,1>( pm.v[k] );    /* q0 <- X (lane 2), q1 <- Y (own) */
+    }
+    fe xz = FD_DSM4_MUL( Z, qrow );
+    bool eq = true;
+    _Pragma("unroll") for( int k=0; k<8; k++ ) eq = eq && (xz.v[k] == ref.v[k]);
+    int e01 = (int)eq;
+    int both = qb<0>( e01 ) & qb<1>( e01 );
+    if( act && qd == 0 ) err[i] = (i8)(both ? 0 : -3);
+  }
+#endif
 
   if( want_stats && i < n && qd == 0 ) {
     u32 * st = (u32 *)(ws + L.st);
