@@ -28,7 +28,7 @@ import numpy as np
 
 # The streaming tile keeps 4 GPU batches in flight on 4 HIP streams; with
 # HIP's default of 4 hardware queues per process only 2 of them run
-# concurrently (measured, tools/dbg/dbg_conc.py), so give the process 8
+# concurrently (measured in round 1 with a concurrency probe), so give the process 8
 # (read at HIP runtime init, before any device call; well under the pool's
 # limit of 32).
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:

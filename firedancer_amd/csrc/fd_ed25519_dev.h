@@ -169,52 +169,15 @@ FD_DEV fe fe_mul( fe const & F, fe const & G ) {
   return fe_carry_b( h0, h1, h2, h3, h4, h5, h6, h7, h8, h9 );
 }
 
-/* Column K of fe_mul for TWO independent products, the two pinned MAC
-   chains interleaved term by term (each chain's dependent v_mad_i64_i32 is
-   separated by the other chain's).  Term (i, j = K-i mod 10): f_i doubled
-   when i and j are both odd, g_j x19 when i+j >= 10 (the pre-multiples of
-   fe_mul).  The sum is exact, so the term order does not change it. */
-template<int K>
-FD_DEV void fe_col2( i32 const * f1, i32 const * f1_2, i32 const * g1, i32 const * g1_19, i64 & a1,
-                     i32 const * f2, i32 const * f2_2, i32 const * g2, i32 const * g2_19, i64 & a2 ) {
-  _Pragma("unroll") for( int i=0; i<10; i++ ) {
-    int const j = (K - i + 10) % 10;
-    bool const dbl = (i & 1) && (j & 1), x19 = (i + j) >= 10;
-    a1 = mac( dbl ? f1_2[i] : f1[i], x19 ? g1_19[j] : g1[j], a1 );
-    a2 = mac( dbl ? f2_2[i] : f2[i], x19 ? g2_19[j] : g2[j], a2 );
-  }
-}
-
 /* Two fe_muls with the carry fold of fe_sq_fold (even columns start from
-   K = 2^25 + 2^50, odd columns start from the previous column's carry), on
-   interleaved pinned chains.  Same limbs as fe_mul. */
-FD_DEV void fe_mul_fold2( fe & R1, fe const & F1, fe const & G1, fe & R2, fe const & F2, fe const & G2 ) {
-  i64 const kb = fd_opaque( (1L<<25) + (1L<<50) );
-  i32 f1_2[10], g1_19[10], f2_2[10], g2_19[10];
-  _Pragma("unroll") for( int k=0; k<10; k++ ) {
-    f1_2[k] = wmul( F1.v[k], 2 ); g1_19[k] = wmul( G1.v[k], 19 );
-    f2_2[k] = wmul( F2.v[k], 2 ); g2_19[k] = wmul( G2.v[k], 19 );
-  }
-  i32 const * f1 = F1.v; i32 const * g1 = G1.v; i32 const * f2 = F2.v; i32 const * g2 = G2.v;
-# define FD_C2( K_, A_, B_ ) fe_col2<K_>( f1, f1_2, g1, g1_19, A_, f2, f2_2, g2, g2_19, B_ )
-  i64 a0 = kb, b0 = kb, a4 = kb, b4 = kb, a2 = kb, b2 = kb, a6 = kb, b6 = kb, a8 = kb, b8 = kb;
-  FD_C2( 0, a0, b0 ); FD_C2( 4, a4, b4 ); FD_C2( 2, a2, b2 ); FD_C2( 6, a6, b6 ); FD_C2( 8, a8, b8 );
-  i64 a1 = a0 >> 26, b1 = b0 >> 26, a5 = a4 >> 26, b5 = b4 >> 26;
-  FD_C2( 1, a1, b1 ); FD_C2( 5, a5, b5 );
-  a2 += a1 >> 25; b2 += b1 >> 25; a6 += a5 >> 25; b6 += b5 >> 25;
-  i64 a3 = a2 >> 26, b3 = b2 >> 26, a7 = a6 >> 26, b7 = b6 >> 26;
-  FD_C2( 3, a3, b3 ); FD_C2( 7, a7, b7 );
-  a8 += a7 >> 25; b8 += b7 >> 25;
-  i64 a9 = a8 >> 26, b9 = b8 >> 26;
-  FD_C2( 9, a9, b9 );
-# undef FD_C2
-  R1 = fe_carry_fold_out( a0, a1, a2, a3, a4, a5, a6, a7, a8, a9 );
-  R2 = fe_carry_fold_out( b0, b1, b2, b3, b4, b5, b6, b7, b8, b9 );
-}
-
-/* fe_mul_fold2 with every independent chain interleaved term by term: the
-   ten even columns of both products, then columns 1,5 (four chains), 3,7
-   (four), 9 (two).  Same limbs as fe_mul. */
+   K = 2^25 + 2^50, odd columns start from the previous column's carry), every
+   independent pinned MAC chain interleaved term by term: the ten even columns
+   of both products, then columns 1,5 (four chains), 3,7 (four), 9 (two), so
+   each chain's dependent v_mad_i64_i32 is separated by the others' and no
+   hazard wait remains.  Term (i, j = K-i mod 10) of column K: f_i doubled
+   when i and j are both odd, g_j x19 when i+j >= 10 (the pre-multiples of
+   fe_mul); the sum is exact, so the term order does not change it.  Same
+   limbs as fe_mul. */
 template<int K>
 FD_DEV void fe_term( int i, i32 const * f, i32 const * f_2, i32 const * g, i32 const * g_19, i64 & a );
 FD_DEV void fe_mul_fold2w( fe & R1, fe const & F1, fe const & G1, fe & R2, fe const & F2, fe const & G2 ) {
@@ -246,7 +209,7 @@ FD_DEV void fe_mul_fold2w( fe & R1, fe const & F1, fe const & G1, fe & R2, fe co
   R2 = fe_carry_fold_out( b0, b1, b2, b3, b4, b5, b6, b7, b8, b9 );
 }
 
-/* Term i of column K of one fe_mul (same rule as fe_col2). */
+/* Term i of column K of one fe_mul (the rule above fe_mul_fold2w). */
 template<int K>
 FD_DEV void fe_term( int i, i32 const * f, i32 const * f_2, i32 const * g, i32 const * g_19, i64 & a ) {
   int const j = (K - i + 10) % 10;
@@ -311,9 +274,6 @@ FD_DEV fe fe_sqn( fe const & F ) {
   return fe_carry_b( h0, h1, h2, h3, h4, h5, h6, h7, h8, h9 );
 }
 
-#ifndef FD_SQ_FOLD
-#define FD_SQ_FOLD 1
-#endif
 /* fe_sqn<1> with the carry fold (same limbs) */
 FD_DEV fe fe_sq_fold( fe const & F ) {
   i32 const * f = F.v;
@@ -338,13 +298,7 @@ FD_DEV fe fe_sq_fold( fe const & F ) {
   return fe_carry_fold_out( h0, h1, h2, h3, h4, h5, h6, h7, h8, h9 );
 }
 
-FD_DEV fe fe_sq( fe const & f ) {
-#if FD_SQ_FOLD
-  return fe_sq_fold( f );
-#else
-  return fe_sqn<1>( f );
-#endif
-}
+FD_DEV fe fe_sq( fe const & f ) { return fe_sq_fold( f ); }
 
 FD_DEV fe fe_sq_iter( fe h, int n ) {
   _Pragma("unroll 1")

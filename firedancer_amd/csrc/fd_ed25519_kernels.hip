@@ -227,9 +227,7 @@ k_prep( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
 /* ------------------------------------------------------------------ */
 /* k_decomp: lane 2i -> A = pub[i], lane 2i+1 -> R = sig[i][0:32]       */
 
-#ifndef FD_DECOMP_WAVES
-#define FD_DECOMP_WAVES 2
-#endif
+#define FD_DECOMP_WAVES 2   /* k_decomp / k_front occupancy target (222 VGPRs) */
 /* one point per lane: t = 2i (A = pub[i]) or 2i+1 (R = sig[i][0:32]).
    Independent of k_prep (reads no verdict) when `gate` is 0, so the two
    can run concurrently (k_front); with gate, signatures k_prep already
@@ -343,26 +341,12 @@ ge_p1p1_to_p3( p1p1 const & t ) {
   return u;
 }
 
-/* the same products as interleaved, carry-folded pairs (fe_mul_fold2) */
-#ifndef FD_DSM_DEFER_FIN
-#define FD_DSM_DEFER_FIN 1 /* 1: finished lanes park R' and the limb compare runs once after the loop */
-#endif
-#ifndef FD_DSM_REPAIR
-#define FD_DSM_REPAIR 1    /* 1: body pairs DBL Z*2Z with ADD Z*qZ (one fewer operand select per limb) */
-#endif
-#ifndef FD_DSM_FOLD
-#define FD_DSM_FOLD 2      /* 1: field muls as interleaved carry-folded pairs (fe_mul_fold2); 2: every independent chain interleaved (fe_mul_fold2w, no s_nop) */
-#endif
-#if FD_DSM_FOLD == 2
-#define FD_MUL2 fe_mul_fold2w
-#else
-#define FD_MUL2 fe_mul_fold2
-#endif
+/* the same products as interleaved, carry-folded pairs (fe_mul_fold2w) */
 __device__ __forceinline__ p3
 ge_p1p1_to_p3_fold( p1p1 const & t ) {
   p3 u;
-  FD_MUL2( u.Z, t.Z, t.T, u.Y, t.Z, t.Y );
-  FD_MUL2( u.X, t.X, t.T, u.T, t.X, t.Y );
+  fe_mul_fold2w( u.Z, t.Z, t.T, u.Y, t.Z, t.Y );
+  fe_mul_fold2w( u.X, t.X, t.T, u.T, t.X, t.Y );
   return u;
 }
 
@@ -449,19 +433,7 @@ struct evq {
  * takes one more step (PH_FIN): its p1p1->p2 result is R', compared with
  * the limb memcmp of fd_ed25519_user.c:417-425, then it idles (PH_DONE).
  */
-#ifndef FD_DSM_QLDS
-#define FD_DSM_QLDS 0      /* 1: stage the next op's table operand in LDS (LDS-DMA) instead of VGPRs */
-#endif
-#ifndef FD_DSM_WAVES
-#define FD_DSM_WAVES 0     /* >0: __launch_bounds__ min waves per SIMD */
-#endif
-#if FD_DSM_WAVES
-#define FD_DSM_LB __launch_bounds__(64, FD_DSM_WAVES)
-#else
-#define FD_DSM_LB __launch_bounds__(64)
-#endif
-
-__global__ void FD_DSM_LB
+__global__ void __launch_bounds__(64)
 k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats ) {
   __shared__ i32 bi[8][40];
   for( int k=threadIdx.x; k<8*40; k+=64 ) {
@@ -534,45 +506,19 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
   u32 nit = (u32)(p + 1);
   bool qneg = false;
 
-  /* The next op's table operand q = [qZ | qM | qP | qT] (40 limbs) lives in
-     LDS, qs[limb][lane], not in VGPRs: ADD(A) entries arrive by LDS-DMA
-     (global_load_lds, per-lane source row) one step ahead, ADD(B) entries
-     are copied from the LDS base table, R.X / R.Y land in rows 0..19 for
-     the final compare.  Freed VGPRs buy a third wave per SIMD. */
-#if FD_DSM_QLDS
-  int lane = (int)threadIdx.x;
-  __shared__ i32 qs[40][64];
-# define QV( R_, K_ ) qs[(R_)*10 + (K_)][lane]
-# define Q_SET( R_, K_, V_ ) ( qs[(R_)*10 + (K_)][lane] = (V_) )
-# define Q_GLOBAL( R_, K_, S_ ) __builtin_amdgcn_global_load_lds( (void const *)(S_), (void __attribute__((address_space(3))) *)&qs[(R_)*10 + (K_)][0], 4, 0, 0 )
-#else
+  /* the next op's table operand q = [qZ | qM | qP | qT] (40 limbs) */
   fe q[4];
   _Pragma("unroll") for( int r=0; r<4; r++ ) q[r] = fe_zero();
 # define QV( R_, K_ ) q[R_].v[K_]
 # define Q_SET( R_, K_, V_ ) ( q[R_].v[K_] = (V_) )
-# define Q_GLOBAL( R_, K_, S_ ) ( q[R_].v[K_] = *(S_) )
-#endif
-#if !FD_DSM_DEFER_FIN
-  if( ph == PH_FIN ) {   /* both scalars zero: R' = (0:1:1) */
-    _Pragma("unroll") for( int k=0; k<10; k++ ) { Q_SET( 0, k, Rw[(size_t)k*N + ii] ); Q_SET( 1, k, Rw[(size_t)(10+k)*N + ii] ); }
-  }
-#endif
   p1p1 t;   /* identity as a completed point: p1p1->p3 gives (0,1,1,0) */
   t.X = fe_zero(); t.Y = fe_one(); t.Z = fe_one(); t.T = fe_one();
 
   for( ;; ) {
     /* p1p1 -> p3 (its X,Y,Z are the reference's p1p1 -> p2) */
-#if FD_DSM_FOLD
     p3 u = ge_p1p1_to_p3_fold( t );
-#else
-    p3 u = ge_p1p1_to_p3( t );
-#endif
-#if FD_DSM_QLDS
-    asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );   /* LDS-DMA of q (issued last step) has landed */
-#endif
 
     bool fin = (ph == PH_FIN);
-#if FD_DSM_DEFER_FIN
     /* R' = u's (X, Y, Z) parks in the lane's own Ai rows (no ADD op reads
        them any more); the compare runs once for the whole wave after the
        loop instead of once per distinct finishing step */
@@ -590,20 +536,6 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
         ph = PH_DONE;
       }
     }
-#else
-    if( __any( fin ) ) {
-      if( fin ) {
-        fe RX, RY;
-        _Pragma("unroll") for( int k=0; k<10; k++ ) { RX.v[k] = QV( 0, k ); RY.v[k] = QV( 1, k ); }
-        fe xZ = fe_mul( u.Z, RX );
-        fe yZ = fe_mul( u.Z, RY );
-        bool eq = true;
-        _Pragma("unroll") for( int k=0; k<8; k++ ) eq = eq && (xZ.v[k] == u.X.v[k]) && (yZ.v[k] == u.Y.v[k]);
-        err[i] = (i8)(eq ? 0 : -3);
-        ph = PH_DONE;
-      }
-    }
-#endif
     if( __all( ph == PH_DONE ) ) break;
 
     /* op body: 4 field muls with per-lane operands, paired so that DBL and
@@ -612,38 +544,19 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
     bool isD = (ph == PH_DBL);
     u64 mD = __builtin_amdgcn_ballot_w64( isD ), mN = __builtin_amdgcn_ballot_w64( qneg );
     fe m0, m1, m2, m3;
-#if FD_DSM_FOLD
     {
       fe a0, b0, a1, b1, a2, b2, a3, b3;
       _Pragma("unroll") for( int k=0; k<10; k++ ) {
         i32 xy = u.X.v[k] + u.Y.v[k];
         a0.v[k] = xy;                                     b0.v[k] = vsel( mD, xy, QV( 2, k ) );
         a1.v[k] = vsel( mD, u.Y.v[k], u.Y.v[k] - u.X.v[k] ); b1.v[k] = vsel( mD, u.Y.v[k], QV( 1, k ) );
-#if FD_DSM_REPAIR
         /* DBL Z*2Z pairs with ADD Z*qZ (shared a = Z), DBL X^2 with ADD T*qT */
         a2.v[k] = u.Z.v[k];                              b2.v[k] = vsel( mD, u.Z.v[k] + u.Z.v[k], QV( 0, k ) );
         a3.v[k] = vsel( mD, u.X.v[k], u.T.v[k] );        b3.v[k] = vsel( mD, u.X.v[k], QV( 3, k ) );
-#else
-        a2.v[k] = vsel( mD, u.X.v[k], u.Z.v[k] );        b2.v[k] = vsel( mD, u.X.v[k], QV( 0, k ) );
-        a3.v[k] = vsel( mD, u.Z.v[k], u.T.v[k] );        b3.v[k] = vsel( mD, u.Z.v[k] + u.Z.v[k], QV( 3, k ) );
-#endif
       }
-      FD_MUL2( m0, a0, b0, m1, a1, b1 );
-      FD_MUL2( m2, a2, b2, m3, a3, b3 );
+      fe_mul_fold2w( m0, a0, b0, m1, a1, b1 );
+      fe_mul_fold2w( m2, a2, b2, m3, a3, b3 );
     }
-#else
-    {
-      fe a, b;
-      _Pragma("unroll") for( int k=0; k<10; k++ ) { i32 xy = u.X.v[k] + u.Y.v[k]; a.v[k] = xy; b.v[k] = vsel( mD, xy, QV( 2, k ) ); }
-      m0 = fe_mul( a, b );
-      _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = vsel( mD, u.Y.v[k], u.Y.v[k] - u.X.v[k] ); b.v[k] = vsel( mD, u.Y.v[k], QV( 1, k ) ); }
-      m1 = fe_mul( a, b );
-      _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = vsel( mD, u.X.v[k], u.Z.v[k] ); b.v[k] = vsel( mD, u.X.v[k], QV( 0, k ) ); }
-      m2 = fe_mul( a, b );
-      _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = vsel( mD, u.Z.v[k], u.T.v[k] ); b.v[k] = vsel( mD, u.Z.v[k] + u.Z.v[k], QV( 3, k ) ); }
-      m3 = fe_mul( a, b );
-    }
-#endif
     /* lanes that are done (PH_DONE) keep computing on don't-care values:
        nothing they compute is stored */
     _Pragma("unroll") for( int k=0; k<10; k++ ) {
@@ -651,12 +564,8 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
       /* DBL mix [a-b-c, b+c, b-c, d-b+c] with a=m0 b=m1 c=m2 d=m3;
          ADD mix [P-M, P+M, 2Z+-T, 2Z-+T] with P=m0 M=m1 Z=m2 T=m3 */
       i32 z2 = A2 + A2;
-#if FD_DSM_FOLD && FD_DSM_REPAIR
       /* DBL: m2 = 2Z^2, m3 = X^2 */
       i32 dY = A1 + A3, dZ = A1 - A3, dX = A0 - dY, dT = A2 - dZ;
-#else
-      i32 dX = A0 - A1 - A2, dY = A1 + A2, dZ = A1 - A2, dT = A3 - A1 + A2;
-#endif
       i32 aX = A0 - A1,      aY = A0 + A1;
       i32 zp = z2 + A3, zm = z2 - A3;
       i32 aZ = vsel( mN, zm, zp ), aT = vsel( mN, zp, zm );
@@ -699,10 +608,6 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
       } while(0)
       Q_ROW( 0, 0 ); Q_ROW( 1, rowM ); Q_ROW( 2, rowP ); Q_ROW( 3, 3 );
 #     undef Q_ROW
-#if !FD_DSM_DEFER_FIN
-    } else if( ph == PH_FIN ) {
-      _Pragma("unroll") for( int k=0; k<10; k++ ) { Q_GLOBAL( 0, k, Rw + (size_t)k*N + ii ); Q_GLOBAL( 1, k, Rw + (size_t)(10+k)*N + ii ); }
-#endif
     } else if( ph == PH_ADDB ) {
       nhb++;
       int e = (db < 0 ? -db : db) >> 1;
@@ -718,9 +623,7 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
   }
 # undef QV
 # undef Q_SET
-# undef Q_GLOBAL
 
-#if FD_DSM_DEFER_FIN
   /* the limb compare of fd_ed25519_user.c:417-425, once per wave */
   if( act ) {
     int4 const * s_ = (int4 const *)Ail;
@@ -731,12 +634,11 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
     fe RX, RY;
     _Pragma("unroll") for( int k=0; k<10; k++ ) { RX.v[k] = Rw[(size_t)k*N + ii]; RY.v[k] = Rw[(size_t)(10+k)*N + ii]; }
     fe xZ, yZ;
-    FD_MUL2( xZ, Z, RX, yZ, Z, RY );
+    fe_mul_fold2w( xZ, Z, RX, yZ, Z, RY );
     bool eq = true;
     _Pragma("unroll") for( int k=0; k<8; k++ ) eq = eq && (xZ.v[k] == X.v[k]) && (yZ.v[k] == Y.v[k]);
     err[i] = (i8)(eq ? 0 : -3);
   }
-#endif
   if( want_stats && i < n ) {
     u32 * st = (u32 *)(ws + L.st);
     st[i] = act ? nit : 0u; st[N + i] = act ? nha : 0u; st[2*N + i] = act ? nhb : 0u;
@@ -789,64 +691,13 @@ quad_p3( p3 & u, p1p1 const & t, u64 m1, u64 m2 ) {
   qgather( pm, u.Z, u.Y, u.X, u.T );
 }
 
-/* p1p1 -> p3 on a quad, keeping only this lane's product:
-   q0 u.Z, q1 u.Y, q2 u.X, q3 u.T */
-__device__ __forceinline__ fe
-quad_p3_own( p1p1 const & t, u64 m1, u64 m2 ) {
-  fe a, b;
-  _Pragma("unroll") for( int k=0; k<10; k++ ) {
-    a.v[k] = vsel( m2, t.X.v[k], t.Z.v[k] );
-    b.v[k] = vsel( m1, t.Y.v[k], t.T.v[k] );
-  }
-  return fe_mul( a, b );
-}
-
 /* DPP quad_perm with a per-destination source lane: lane q reads lane s_q */
 template<int S0, int S1, int S2, int S3>
 __device__ __forceinline__ i32 qp( i32 v ) {
   return __builtin_amdgcn_mov_dpp( v, S0 | (S1 << 2) | (S2 << 4) | (S3 << 6), 0xf, 0xf, false );
 }
 
-/* op body + mix on a quad from the lanes' own p3 products (q0 Z, q1 Y,
-   q2 X, q3 T).  Two DPP reads give every lane the two coordinates its
-   operand needs:  P1 = quad_perm(2,2,2,0) -> X X X Z,
-                   P2 = quad_perm(1,1,0,3) -> Y Y Z T,
-   then   a = [X+Y, Y | Y-X, X | Z, Z | T]  (DBL | ADD)
-          b = DBL ? [X+Y, Y, X, 2Z] : qrow.
-   Per lane 32-bit masks (constant per step): k1 keeps P1, k2 keeps P2,
-   n1 negates P1 (q1 ADD), k3 doubles (q3 DBL). */
-__device__ __forceinline__ void
-quad_body_own( p1p1 & t, fe const & pm, fe const & qrow, bool isD, u64 mD, u64 mN, int qd ) {
-  i32 const ones = -1;
-  i32 k1 = (qd == 0 || (qd == 1 && !isD) || (qd >= 2 && isD)) ? ones : 0;
-  i32 k2 = (qd <= 1 || !isD) ? ones : 0;
-  i32 n1 = (qd == 1 && !isD) ? ones : 0;
-  i32 k3 = (qd == 3) ? ones : 0;
-  fe a, b;
-  _Pragma("unroll") for( int k=0; k<10; k++ ) {
-    i32 P1 = qp<2,2,2,0>( pm.v[k] ), P2 = qp<1,1,0,3>( pm.v[k] );
-    i32 av = (P2 & k2) + (((P1 & k1) ^ n1) - n1);
-    a.v[k] = av;
-    b.v[k] = vsel( mD, av + (av & k3), qrow.v[k] );
-  }
-  fe m = fe_mul( a, b );
-  fe M0, M1, M2, M3;
-  qgather( m, M0, M1, M2, M3 );
-  _Pragma("unroll") for( int k=0; k<10; k++ ) {
-    i32 A0 = M0.v[k], A1 = M1.v[k], A2 = M2.v[k], A3 = M3.v[k];
-    i32 z2 = A2 + A2;
-    i32 dY = A1 + A2, dZ = A1 - A2, dX = A0 - dY, dT = A3 - dZ;
-    i32 aX = A0 - A1,      aY = A0 + A1;
-    i32 zp = z2 + A3, zm = z2 - A3;
-    i32 aZ = vsel( mN, zm, zp ), aT = vsel( mN, zp, zm );
-    t.X.v[k] = vsel( mD, dX, aX );
-    t.Y.v[k] = vsel( mD, dY, aY );
-    t.Z.v[k] = vsel( mD, dZ, aZ );
-    t.T.v[k] = vsel( mD, dT, aT );
-  }
-}
-
-/* Own-coordinate form of the step (FD_DSM4_OWNC): after the body mul,
+/* Own-coordinate form of the step: after the body mul,
    lane q computes only the ONE p1p1 coordinate C = (Z, T, X, Y)[q] that it
    owns, as x*A + y*B + z*D over three DPP-read products with per-lane
    coefficients in {-1,0,1,2} (three v_mad_i64_i32, low 32 bits = the
@@ -856,25 +707,11 @@ quad_body_own( p1p1 & t, fe const & pm, fe const & qrow, bool isD, u64 mD, u64 m
      DBL  Z = m1-m2   T = m3-m1+m2   X = m0-m1-m2   Y = m1+m2
      ADD  Z = 2m2+-m3 T = 2m2-+m3    X = m0-m1      Y = m0+m1
    A/B/D sources: q0,q1 <- m1,m2,m3; q2,q3 <- m0,m1,m2. */
-#ifndef FD_DSM4_OWNC
-#define FD_DSM4_OWNC 1
-#endif
-#ifndef FD_DSM4_DEFER_FIN
-#define FD_DSM4_DEFER_FIN 1 /* 1: finished quads park their products; the limb compare runs once after the loop */
-#endif
-#ifndef FD_DSM4_FOLD
-#define FD_DSM4_FOLD 1     /* 1: the lane's field mul with the carry fold, columns interleaved (fe_mul_fold1) */
-#endif
-#if FD_DSM4_FOLD
-#define FD_DSM4_MUL fe_mul_fold1
-#else
-#define FD_DSM4_MUL fe_mul
-#endif
 __device__ __forceinline__ fe
 quad_p3_ownc( fe const & C ) {
   fe a, b;
   _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = qp<0,0,2,2>( C.v[k] ); b.v[k] = qp<1,3,1,3>( C.v[k] ); }
-  return FD_DSM4_MUL( a, b );
+  return fe_mul_fold1( a, b );
 }
 
 __device__ __forceinline__ i32
@@ -907,7 +744,7 @@ quad_body_ownc( fe & C, fe const & pm, fe const & qrow, bool isD, bool neg, u64 
     a.v[k] = av;
     b.v[k] = vsel( mD, (i32)((u32)av << sh), qrow.v[k] );
   }
-  fe m = FD_DSM4_MUL( a, b );
+  fe m = fe_mul_fold1( a, b );
   i32 s0 = neg ? -1 : 1;
   i32 x = isD ? (qd == 1 ? -1 : (qd == 3 ? 0 : 1)) : (qd >= 2 ? 1 : 0);
   i32 y = isD ? ((qd & 1) ? 1 : -1)               : (qd <= 1 ? 2 : (qd == 2 ? -1 : 1));
@@ -1041,28 +878,12 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
   u32 nit = (u32)(p + 1);
   bool qneg = false;
   fe qrow = fe_zero();
-#if !FD_DSM4_DEFER_FIN
-  /* lanes 0/1 hold R.X / R.Y for the final compare */
-  if( ph == PH_FIN ) {
-    _Pragma("unroll") for( int k=0; k<10; k++ ) qrow.v[k] = Rw[(size_t)((qd & 1)*10 + k)*N + ii];
-  }
-#endif
-#if FD_DSM4_OWNC
   fe C = (qd == 2) ? fe_zero() : fe_one();   /* identity: own coordinate (Z, T, X, Y)[q] = (1, 1, 0, 1) */
-#else
-  p1p1 t;
-  t.X = fe_zero(); t.Y = fe_one(); t.Z = fe_one(); t.T = fe_one();
-#endif
 
   for( ;; ) {
-#if FD_DSM4_OWNC
     fe pm = quad_p3_ownc( C );              /* q0 u.Z, q1 u.Y, q2 u.X, q3 u.T */
-#else
-    fe pm = quad_p3_own( t, m1, m2 );       /* q0 u.Z, q1 u.Y, q2 u.X, q3 u.T */
-#endif
 
     bool fin = (ph == PH_FIN);
-#if FD_DSM4_DEFER_FIN
     /* each lane parks its own p1p1->p3 product in its row of entry 0 of the
        signature's Ai table (no ADD op reads it any more); the compare runs
        once after the loop */
@@ -1075,35 +896,11 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
         ph = PH_DONE;
       }
     }
-#else
-    if( __any( fin ) ) {
-      /* q0: Z*RX vs X, q1: Z*RY vs Y; lanes 2,3 compute don't-care values */
-      fe Z, ref;
-      _Pragma("unroll") for( int k=0; k<10; k++ ) {
-        Z.v[k] = qb<0>( pm.v[k] );
-        ref.v[k] = qp<2,1,2,1>( pm.v[k] );  /* q0 <- X (lane 2), q1 <- Y (own) */
-      }
-      fe xz = fe_mul( Z, qrow );
-      bool eq = true;
-      _Pragma("unroll") for( int k=0; k<8; k++ ) eq = eq && (xz.v[k] == ref.v[k]);
-      int e01 = (int)eq;
-      int both = qb<0>( e01 ) & qb<1>( e01 );
-      if( fin ) {
-        if( qd == 0 ) err[i] = (i8)(both ? 0 : -3);
-        ph = PH_DONE;
-      }
-    }
-#endif
     if( __all( ph == PH_DONE ) ) break;
 
     bool isD = (ph == PH_DBL);
     u64 mD = __builtin_amdgcn_ballot_w64( isD );
-#if FD_DSM4_OWNC
     quad_body_ownc( C, pm, qrow, isD, qneg, mD, qd );
-#else
-    u64 mN = __builtin_amdgcn_ballot_w64( qneg );
-    quad_body_own( t, pm, qrow, isD, mD, mN, qd );
-#endif
 
     /* the event just executed is consumed; the next op follows from the
        event heads (an event at position p means a digit at p) */
@@ -1140,14 +937,9 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
         nhb++;
         _Pragma("unroll") for( int k=0; k<10; k++ ) qrow.v[k] = bi[e][row*10 + k];
       }
-#if !FD_DSM4_DEFER_FIN
-    } else if( ph == PH_FIN ) {
-      _Pragma("unroll") for( int k=0; k<10; k++ ) qrow.v[k] = Rw[(size_t)((qd & 1)*10 + k)*N + ii];
-#endif
     }
   }
 
-#if FD_DSM4_DEFER_FIN
   /* the limb compare (fd_ed25519_user.c:417-425), once per wave, all lanes
      converged: q0 Z*RX vs X, q1 Z*RY vs Y, quad AND */
   {
@@ -1163,14 +955,13 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
       Z.v[k] = qb<0>( pm.v[k] );
       ref.v[k] = qp<2,1,2,1>( pm.v[k] );    /* q0 <- X (lane 2), q1 <- Y (own) */
     }
-    fe xz = FD_DSM4_MUL( Z, qrow );
+    fe xz = fe_mul_fold1( Z, qrow );
     bool eq = true;
     _Pragma("unroll") for( int k=0; k<8; k++ ) eq = eq && (xz.v[k] == ref.v[k]);
     int e01 = (int)eq;
     int both = qb<0>( e01 ) & qb<1>( e01 );
     if( act && qd == 0 ) err[i] = (i8)(both ? 0 : -3);
   }
-#endif
 
   if( want_stats && i < n && qd == 0 ) {
     u32 * st = (u32 *)(ws + L.st);

@@ -349,7 +349,7 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
                     (t->wait_ns && now_ns() - stage_t0 >= t->wait_ns) ) ) {
       /* kernel path by batch size: tile batches are small next to the GPU,
          so the 4-lane latency kernels are used even with 4 in flight.
-         Measured (tools/dbg/dbg_tile_policy.py history): switching batches
+         Measured (profiles/r01_tile_policy_ab.txt): switching batches
          of >= 4096/8192 to the 1-lane kernel while others were in flight
          lowered the saturated rate at every batch_max and doubled latency;
          the in-flight work (4 x batch_max) is too small for the 1-lane

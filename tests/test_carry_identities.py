@@ -1,7 +1,7 @@
 """The carry-chain rewrites used by the HIP field kernels give the
 reference's limbs (avx/fd_ed25519_fe_avx_inl.h:568-584) on every input:
 the biased chain (fe_carry_b), the carry-folded chain (fe_sq_fold,
-fe_mul_fold2 / fe_mul_fold2w, fe_carry_fold_out) and the folded chain with
+fe_mul_fold2w, fe_carry_fold_out) and the folded chain with
 an independent column 9 (fe_mul_fold1), all in
 firedancer_amd/csrc/fd_ed25519_dev.h, modelled here
 with Python integers (int64 semantics checked) over random and extreme
