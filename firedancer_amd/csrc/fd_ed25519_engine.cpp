@@ -16,6 +16,7 @@
 #include <string.h>
 #include <stdint.h>
 #include <mutex>
+#include <pthread.h>
 #include <thread>
 
 #include "../../include/fd_ed25519_amd.h"
@@ -40,6 +41,11 @@ slot_out( slot_t * s, void * h_dst, void const * d_src, ulong n ) {
                  h_dst == (void *)s->h_tag  ? s->m_tag  : NULL;
   if( !d_dst ) return hipErrorInvalidValue;
   return fd_amd_launch_copy_out( d_dst, d_src, n, s->stream ) ? hipErrorLaunchFailure : hipSuccess;
+}
+
+int
+fd_amd_slot_out( slot_t * s, void * h_dst, void const * d_src, ulong n ) {
+  return slot_out( s, h_dst, d_src, n ) == hipSuccess ? 0 : -1;
 }
 
 static void
@@ -176,43 +182,18 @@ fd_amd_slot_drain( slot_t * s ) {
   return FD_ED25519_AMD_OK;
 }
 
-/* Launch the staged chunk of slot s (inputs already in pinned memory). */
-int
-fd_amd_slot_launch( slot_t * s, ulong n, ulong blob_sz, schar * out, int want_tag ) {
-  HIPCHK( hipMemcpyAsync( s->d_pub,  s->h_pub,  32UL*n, hipMemcpyHostToDevice, s->stream ) );
-  HIPCHK( hipMemcpyAsync( s->d_sig,  s->h_sig,  64UL*n, hipMemcpyHostToDevice, s->stream ) );
-  HIPCHK( hipMemcpyAsync( s->d_off,  s->h_off,  4UL*n,  hipMemcpyHostToDevice, s->stream ) );
-  HIPCHK( hipMemcpyAsync( s->d_sz,   s->h_sz,   4UL*n,  hipMemcpyHostToDevice, s->stream ) );
-  if( blob_sz ) HIPCHK( hipMemcpyAsync( s->d_blob, s->h_blob, blob_sz, hipMemcpyHostToDevice, s->stream ) );
-  if( fd_amd_launch_verify( (uint32_t)n, s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_blob, s->d_err, s->d_ws, s->stream, 1, NULL,
-                            NULL, s->dsm_mode ) )
-    return FD_ED25519_AMD_ERR_DEVICE;
-  HIPCHK( slot_out( s, s->h_err, s->d_err, n ) );
-  if( want_tag ) {
-    ws_layout_t L = fd_amd_ws_layout( n );
-    HIPCHK( slot_out( s, s->h_tag, (uint8_t *)s->d_ws + L.tag, 8UL*n ) );
+/* Error exit of a batch call: wait for every chunk still in flight and
+   forget where its verdicts were to go, so no later call writes into the
+   caller's (by then possibly freed) output arrays. */
+static int
+engine_quiesce( fd_ed25519_amd_t * e, int rc ) {
+  for( int k=0; k<FD_AMD_SLOT_MAX; k++ ) {
+    slot_t * s = &e->slot[k];
+    if( s->busy ) (void)hipEventSynchronize( s->done );
+    s->out = s->t_out = s->s_out = NULL;
+    s->busy = 0;
   }
-  HIPCHK( hipEventRecord( s->done, s->stream ) );
-  s->out = out; s->n = n; s->busy = 1; s->want_tag = want_tag;
-  return FD_ED25519_AMD_OK;
-}
-
-int
-fd_amd_slot_launch_zc( slot_t * s, ulong n, uint8_t const * d_dc ) {
-  /* h_off / h_sz hold chunk / frag size; the SoA planes are built on the GPU */
-  HIPCHK( hipMemcpyAsync( s->d_toff, s->h_off, 4UL*n, hipMemcpyHostToDevice, s->stream ) );
-  HIPCHK( hipMemcpyAsync( s->d_tsz,  s->h_sz,  4UL*n, hipMemcpyHostToDevice, s->stream ) );
-  if( fd_amd_launch_zgather( (uint32_t)n, s->d_toff, s->d_tsz, d_dc, s->d_pub, s->d_sig, s->d_off, s->d_sz, s->stream ) )
-    return FD_ED25519_AMD_ERR_DEVICE;
-  if( fd_amd_launch_verify( (uint32_t)n, s->d_pub, s->d_sig, s->d_off, s->d_sz, d_dc, s->d_err, s->d_ws, s->stream, 1, NULL,
-                            NULL, s->dsm_mode ) )
-    return FD_ED25519_AMD_ERR_DEVICE;
-  HIPCHK( slot_out( s, s->h_err, s->d_err, n ) );
-  ws_layout_t L = fd_amd_ws_layout( n );
-  HIPCHK( slot_out( s, s->h_tag, (uint8_t *)s->d_ws + L.tag, 8UL*n ) );
-  HIPCHK( hipEventRecord( s->done, s->stream ) );
-  s->out = NULL; s->n = n; s->busy = 1; s->want_tag = 1;
-  return FD_ED25519_AMD_OK;
+  return rc;
 }
 
 int
@@ -285,16 +266,20 @@ template<typename GET>
 static int
 run_chunked( fd_ed25519_amd_t * e, ulong n, schar * err, GET get ) {
   if( hipSetDevice( e->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  for( ulong j=0; j<n; j++ ) {          /* every message must fit one chunk: checked before anything launches */
+    uint8_t const * msg; ulong sz; uint8_t const * sig; uint8_t const * pub;
+    get( j, &msg, &sz, &sig, &pub );
+    if( sz > e->blob_cap || (sz && !msg) ) return FD_ED25519_AMD_ERR_INVAL;
+  }
   ulong i = 0; int k = 0; int rc = FD_ED25519_AMD_OK;
   while( i < n ) {
     slot_t * s = &e->slot[k];
-    if( (rc = fd_amd_slot_drain( s )) ) return rc;
+    if( (rc = fd_amd_slot_drain( s )) ) return engine_quiesce( e, rc );
     /* size the chunk first, then stage it packed: [pub|sig|off|sz|blob] */
     ulong c = 0, bsz = 0;
     while( i + c < n && c < e->cap ) {
       uint8_t const * msg; ulong sz; uint8_t const * sig; uint8_t const * pub;
       get( i + c, &msg, &sz, &sig, &pub );
-      if( sz > e->blob_cap ) return FD_ED25519_AMD_ERR_INVAL;   /* cannot be staged in one chunk */
       if( bsz + sz > e->blob_cap ) break;
       bsz += sz; c++;
     }
@@ -311,10 +296,10 @@ run_chunked( fd_ed25519_amd_t * e, ulong n, schar * err, GET get ) {
       h_off[j] = (uint32_t)bsz; h_sz[j] = (uint32_t)sz;
       bsz += sz;
     }
-    if( (rc = fd_amd_slot_launch_packed( s, c, bsz, err + i )) ) return rc;
+    if( (rc = fd_amd_slot_launch_packed( s, c, bsz, err + i )) ) return engine_quiesce( e, rc );
     i += c; k ^= 1;
   }
-  for( int j=0; j<2; j++ ) if( (rc = fd_amd_slot_drain( &e->slot[j] )) ) return rc;
+  for( int j=0; j<2; j++ ) if( (rc = fd_amd_slot_drain( &e->slot[j] )) ) return engine_quiesce( e, rc );
   return FD_ED25519_AMD_OK;
 }
 
@@ -355,11 +340,10 @@ run_soa( fd_ed25519_amd_t * e, ulong n, uchar const * pub, uchar const * sig, ui
   ulong i = 0; int k = 0; int rc = FD_ED25519_AMD_OK;
   while( i < n ) {
     slot_t * s = &e->slot[k];
-    if( (rc = fd_amd_slot_drain( s )) ) return rc;
+    if( (rc = fd_amd_slot_drain( s )) ) return engine_quiesce( e, rc );
     ulong c = 0, bsz = 0, lo = ~0UL, hi = 0UL;
     while( i + c < n && c < e->cap ) {
-      ulong sz = msg_sz[i+c];
-      if( sz > e->blob_cap ) return FD_ED25519_AMD_ERR_INVAL;
+      ulong sz = msg_sz[i+c];                /* <= blob_cap: checked by the caller */
       if( bsz + sz > e->blob_cap ) break;
       if( sz ) { ulong o = msg_off[i+c]; lo = o < lo ? o : lo; hi = o + sz > hi ? o + sz : hi; }
       bsz += sz; c++;
@@ -383,10 +367,10 @@ run_soa( fd_ed25519_amd_t * e, ulong n, uchar const * pub, uchar const * sig, ui
         h_off[j] = (uint32_t)bsz; bsz += sz;
       }
     }
-    if( (rc = fd_amd_slot_launch_packed( s, c, bsz, err + i )) ) return rc;
+    if( (rc = fd_amd_slot_launch_packed( s, c, bsz, err + i )) ) return engine_quiesce( e, rc );
     i += c; k = (k + 1) % e->nslot;
   }
-  for( int j=0; j<e->nslot; j++ ) if( (rc = fd_amd_slot_drain( &e->slot[j] )) ) return rc;
+  for( int j=0; j<e->nslot; j++ ) if( (rc = fd_amd_slot_drain( &e->slot[j] )) ) return engine_quiesce( e, rc );
   return FD_ED25519_AMD_OK;
 }
 
@@ -395,9 +379,112 @@ fd_ed25519_amd_verify_soa( fd_ed25519_amd_t * e, ulong n, uchar const * pub, uch
                            uint const * msg_off, uint const * msg_sz, uchar const * blob, ulong blob_sz,
                            schar * err ) {
   if( !e || (n && (!pub || !sig || !msg_off || !msg_sz || !err)) ) return FD_ED25519_AMD_ERR_INVAL;
+  /* every message in bounds and small enough for one chunk: checked before
+     anything launches, so an error never leaves a chunk in flight */
   for( ulong i=0; i<n; i++ )
-    if( msg_sz[i] && ((ulong)msg_off[i] + msg_sz[i] > blob_sz || !blob) ) return FD_ED25519_AMD_ERR_INVAL;
+    if( msg_sz[i] && ((ulong)msg_off[i] + msg_sz[i] > blob_sz || !blob || msg_sz[i] > e->blob_cap) )
+      return FD_ED25519_AMD_ERR_INVAL;
   return run_soa( e, n, pub, sig, msg_off, msg_sz, blob, err );
+}
+
+/* ------------------------------------------------------------------ */
+/* zero-copy host batches (caller memory registered once)               */
+
+extern "C" int
+fd_ed25519_amd_host_register( void * base, ulong sz ) {
+  if( !base || !sz ) return FD_ED25519_AMD_ERR_INVAL;
+  if( hipHostRegister( base, sz, hipHostRegisterPortable ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  return FD_ED25519_AMD_OK;
+}
+
+extern "C" int
+fd_ed25519_amd_host_unregister( void * base ) {
+  if( !base ) return FD_ED25519_AMD_ERR_INVAL;
+  return hipHostUnregister( base ) == hipSuccess ? FD_ED25519_AMD_OK : FD_ED25519_AMD_ERR_DEVICE;
+}
+
+static bool
+host_registered( void const * p ) {
+  hipPointerAttribute_t a;
+  if( hipPointerGetAttributes( &a, p ) != hipSuccess ) { (void)hipGetLastError(); return false; }
+  return a.type == hipMemoryTypeHost;
+}
+
+/* One chunk straight from registered caller memory: the pub/sig/off/sz
+   slices and the message window [lo, lo+win) by DMA into the slot's
+   device planes, offsets rebased on the device. */
+static int
+slot_launch_dma( slot_t * s, ulong c, uchar const * pub, uchar const * sig, uint const * off, uint const * sz,
+                 uchar const * win_src, ulong win, uint lo, schar * out ) {
+  HIPCHK( hipMemcpyAsync( s->d_pub, pub, 32UL*c, hipMemcpyHostToDevice, s->stream ) );
+  HIPCHK( hipMemcpyAsync( s->d_sig, sig, 64UL*c, hipMemcpyHostToDevice, s->stream ) );
+  HIPCHK( hipMemcpyAsync( s->d_off, off, 4UL*c,  hipMemcpyHostToDevice, s->stream ) );
+  HIPCHK( hipMemcpyAsync( s->d_sz,  sz,  4UL*c,  hipMemcpyHostToDevice, s->stream ) );
+  if( win ) HIPCHK( hipMemcpyAsync( s->d_blob, win_src, win, hipMemcpyHostToDevice, s->stream ) );
+  if( fd_amd_launch_rebase_off( (uint32_t)c, s->d_off, s->d_sz, lo, s->stream ) ) return FD_ED25519_AMD_ERR_DEVICE;
+  if( fd_amd_launch_verify( (uint32_t)c, s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_blob, s->d_err, s->d_ws, s->stream,
+                            1, NULL ) )
+    return FD_ED25519_AMD_ERR_DEVICE;
+  HIPCHK( slot_out( s, s->h_err, s->d_err, c ) );
+  HIPCHK( hipEventRecord( s->done, s->stream ) );
+  s->out = out; s->n = c; s->busy = 1; s->want_tag = 0;
+  return FD_ED25519_AMD_OK;
+}
+
+extern "C" int
+fd_ed25519_amd_verify_soa_registered( fd_ed25519_amd_t * e, ulong n, uchar const * pub, uchar const * sig,
+                                      uint const * msg_off, uint const * msg_sz, uchar const * blob, ulong blob_sz,
+                                      schar * err ) {
+  if( !e || (n && (!pub || !sig || !msg_off || !msg_sz || !err)) ) return FD_ED25519_AMD_ERR_INVAL;
+  for( ulong i=0; i<n; i++ )
+    if( msg_sz[i] && ((ulong)msg_off[i] + msg_sz[i] > blob_sz || !blob || msg_sz[i] > e->blob_cap) )
+      return FD_ED25519_AMD_ERR_INVAL;
+  if( !n ) return FD_ED25519_AMD_OK;
+  if( !host_registered( pub ) || !host_registered( sig ) || !host_registered( msg_off ) || !host_registered( msg_sz ) ||
+      (blob && blob_sz && !host_registered( blob )) )
+    return FD_ED25519_AMD_ERR_INVAL;
+  if( hipSetDevice( e->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  ulong i = 0; int k = 0; int rc = FD_ED25519_AMD_OK;
+  while( i < n ) {
+    slot_t * s = &e->slot[k];
+    if( (rc = fd_amd_slot_drain( s )) ) return engine_quiesce( e, rc );
+    ulong c = 0, bsz = 0, lo = ~0UL, hi = 0UL;
+    while( i + c < n && c < e->cap ) {
+      ulong sz = msg_sz[i+c];
+      if( bsz + sz > e->blob_cap ) break;
+      if( sz ) {
+        ulong o = msg_off[i+c];
+        ulong nlo = o < lo ? o : lo, nhi = o + sz > hi ? o + sz : hi;
+        if( nhi - nlo > e->blob_cap ) break;     /* the window must fit the device blob */
+        lo = nlo; hi = nhi;
+      }
+      bsz += sz; c++;
+    }
+    ulong win = hi > lo ? hi - lo : 0UL;
+    if( win <= bsz + bsz/4UL + 4096UL ) {
+      rc = slot_launch_dma( s, c, pub + 32UL*i, sig + 64UL*i, msg_off + i, msg_sz + i, blob + (win ? lo : 0UL), win,
+                            (uint)(win ? lo : 0UL), err + i );
+    } else {
+      /* scattered messages: gather them through the pinned staging */
+      uint8_t * hp = s->h_pack;
+      uint8_t * h_blob = hp + 104UL*c;
+      uint32_t * h_off = (uint32_t *)(hp + 96UL*c), * h_sz = (uint32_t *)(hp + 100UL*c);
+      memcpy( hp, pub + 32UL*i, 32UL*c );
+      memcpy( hp + 32UL*c, sig + 64UL*i, 64UL*c );
+      memcpy( h_sz, msg_sz + i, 4UL*c );
+      ulong b = 0;
+      for( ulong j=0; j<c; j++ ) {
+        ulong sz = msg_sz[i+j];
+        if( sz ) memcpy( h_blob + b, blob + msg_off[i+j], sz );
+        h_off[j] = (uint32_t)b; b += sz;
+      }
+      rc = fd_amd_slot_launch_packed( s, c, b, err + i );
+    }
+    if( rc ) return engine_quiesce( e, rc );
+    i += c; k = (k + 1) % e->nslot;
+  }
+  for( int j=0; j<e->nslot; j++ ) if( (rc = fd_amd_slot_drain( &e->slot[j] )) ) return engine_quiesce( e, rc );
+  return FD_ED25519_AMD_OK;
 }
 
 /* Signature slots the engine reserves for a payload: its first byte when
@@ -415,8 +502,14 @@ fd_ed25519_amd_verify_txns( fd_ed25519_amd_t * e, ulong txn_cnt, uchar const * p
                             uint const * txn_sz, ulong payload_sz, schar * txn_err, uint * sig_base, schar * sig_err ) {
   if( !e || (txn_cnt && (!payload || !txn_off || !txn_sz || !txn_err)) ) return FD_ED25519_AMD_ERR_INVAL;
   if( sig_err && !sig_base ) return FD_ED25519_AMD_ERR_INVAL;
-  for( ulong t=0; t<txn_cnt; t++ )
-    if( txn_sz[t] > FD_TXN_AMD_MTU || (ulong)txn_off[t] + txn_sz[t] > payload_sz ) return FD_ED25519_AMD_ERR_INVAL;
+  /* every transaction in bounds and stageable in one chunk (its bytes in
+     blob_max, its signatures in batch_max): checked before anything
+     launches, so the chunk loop always makes progress */
+  for( ulong t=0; t<txn_cnt; t++ ) {
+    if( txn_sz[t] > FD_TXN_AMD_MTU || (ulong)txn_off[t] + txn_sz[t] > payload_sz || txn_sz[t] > e->blob_cap )
+      return FD_ED25519_AMD_ERR_INVAL;
+    if( fd_amd_txn_slots1( payload + txn_off[t], txn_sz[t] ) > e->cap ) return FD_ED25519_AMD_ERR_INVAL;
+  }
   if( hipSetDevice( e->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
   int rc;
   for( int k=0; k<2; k++ ) if( (rc = fd_amd_slot_alloc_aux( &e->slot[k], e->cap )) ) return rc;
@@ -429,7 +522,7 @@ fd_ed25519_amd_verify_txns( fd_ed25519_amd_t * e, ulong txn_cnt, uchar const * p
   ulong t = 0, gsig = 0; int k = 0;
   while( t < txn_cnt ) {
     slot_t * s = &e->slot[k];
-    if( (rc = fd_amd_slot_drain( s )) ) return rc;
+    if( (rc = fd_amd_slot_drain( s )) ) return engine_quiesce( e, rc );
     ulong c = 0, bsz = 0, ns = 0;
     while( t + c < txn_cnt && c < e->cap ) {
       uchar const * p = payload + txn_off[t+c];
@@ -440,10 +533,11 @@ fd_ed25519_amd_verify_txns( fd_ed25519_amd_t * e, ulong txn_cnt, uchar const * p
       bsz += sz; ns += k2; c++;
     }
     s->h_tbase[c] = (uint32_t)ns;
-    if( (rc = fd_amd_slot_launch_txn( s, c, ns, bsz, txn_err + t, sig_err ? sig_err + gsig : NULL, 0, NULL )) ) return rc;
+    if( (rc = fd_amd_slot_launch_txn( s, c, ns, bsz, txn_err + t, sig_err ? sig_err + gsig : NULL, 0, NULL )) )
+      return engine_quiesce( e, rc );
     t += c; gsig += ns; k ^= 1;
   }
-  for( int j=0; j<2; j++ ) if( (rc = fd_amd_slot_drain( &e->slot[j] )) ) return rc;
+  for( int j=0; j<2; j++ ) if( (rc = fd_amd_slot_drain( &e->slot[j] )) ) return engine_quiesce( e, rc );
   return FD_ED25519_AMD_OK;
 }
 
@@ -582,34 +676,55 @@ fd_ed25519_amd_debug_digits_dev( ulong n, void const * d_ws, ushort * d_dig, int
 /* ------------------------------------------------------------------ */
 /* drop-in reference API                                                */
 
+/* One engine per calling thread (the reference is reentrant with one
+   fd_sha512_t per thread, fd_frank_verify.c:121-123), freed by a
+   pthread-key destructor when the thread exits. */
+namespace {
+struct dropin_t { fd_ed25519_amd_t * eng; ulong blob; };
+pthread_key_t  dropin_key;
+pthread_once_t dropin_once = PTHREAD_ONCE_INIT;
+void dropin_free( void * p ) {
+  dropin_t * d = (dropin_t *)p;
+  if( d->eng ) fd_ed25519_amd_delete( d->eng );
+  free( d );
+}
+void dropin_key_init( void ) { (void)pthread_key_create( &dropin_key, dropin_free ); }
+}
+
 extern "C" int
 fd_ed25519_verify( void const * msg, ulong sz, void const * sig, void const * public_key, fd_sha512_t * sha ) {
   (void)sha;   /* scratch of the reference; hashing happens on the GPU */
-  /* one engine per calling thread (the reference is reentrant with one
-     fd_sha512_t per thread, fd_frank_verify.c:121-123); it grows when a
-     message exceeds its staging (the reference accepts any size) */
-  static thread_local fd_ed25519_amd_t * eng = NULL;
-  static thread_local ulong eng_blob = 0;
+  (void)pthread_once( &dropin_once, dropin_key_init );
+  dropin_t * d = (dropin_t *)pthread_getspecific( dropin_key );
+  if( !d ) {
+    d = (dropin_t *)calloc( 1, sizeof(dropin_t) );
+    if( !d || pthread_setspecific( dropin_key, d ) ) {
+      fprintf( stderr, "fd_ed25519_verify: out of memory\n" );
+      abort();
+    }
+  }
   if( sz > 0xFFFFFFFFUL - 4096UL ) {
     fprintf( stderr, "fd_ed25519_verify: message of %lu bytes exceeds the engine's 32-bit offsets\n", sz );
     abort();
   }
-  if( !eng || sz > eng_blob ) {
+  /* the engine grows when a message exceeds its staging (the reference
+     accepts any size) */
+  if( !d->eng || sz > d->blob ) {
     ulong want = 64UL*FD_ED25519_AMD_MSG_MAX;
     while( want < sz ) want <<= 1;
-    if( eng ) fd_ed25519_amd_delete( eng );
-    char const * d = getenv( "FD_ED25519_AMD_DEVICE" );
-    eng = fd_ed25519_amd_new( d ? atoi( d ) : 0, 64UL, want );
-    if( !eng ) {
+    if( d->eng ) { fd_ed25519_amd_delete( d->eng ); d->eng = NULL; }
+    char const * dv = getenv( "FD_ED25519_AMD_DEVICE" );
+    d->eng = fd_ed25519_amd_new( dv ? atoi( dv ) : 0, 64UL, want );
+    if( !d->eng ) {
       fprintf( stderr, "fd_ed25519_verify: no usable MI355X/HIP device; this library has no CPU path\n" );
       abort();
     }
-    eng_blob = want;
+    d->blob = want;
   }
   static uint8_t const zero = 0;
   uint32_t off = 0, s32 = (uint32_t)sz;
   schar err = 0;
-  int rc = fd_ed25519_amd_verify_soa( eng, 1UL, (uchar const *)public_key, (uchar const *)sig, &off, &s32,
+  int rc = fd_ed25519_amd_verify_soa( d->eng, 1UL, (uchar const *)public_key, (uchar const *)sig, &off, &s32,
                                       sz ? (uchar const *)msg : &zero, sz, &err );
   if( rc ) { fprintf( stderr, "fd_ed25519_verify: device error %d\n", rc ); abort(); }
   return (int)err;

@@ -53,15 +53,10 @@ struct fd_ed25519_amd {
 fd_ed25519_amd_t * fd_amd_engine_new( int device, ulong batch_max, ulong blob_max, int nslot );
 
 
-/* Stage-free launch of slot s: inputs already in its pinned buffers (n
-   signatures, blob_sz message bytes).  Verdicts land in s->h_err (and the
-   dedup tags in s->h_tag when want_tag) once s->done has fired; `out`
-   (may be NULL) is where slot_drain copies the verdicts. */
-int  fd_amd_slot_launch( slot_t * s, ulong n, ulong blob_sz, schar * out, int want_tag );
-/* Zero-copy tile chunk: h_off[i] = chunk, h_sz[i] = frag size of frag i in
-   the GPU-mapped data region d_dc (pub|sig|msg framing); tags wanted. */
-int  fd_amd_slot_launch_zc( slot_t * s, ulong n, uint8_t const * d_dc );
-/* Same, inputs staged in s->h_pack as [pub 32n | sig 64n | off 4n | sz 4n | blob]. */
+/* n bytes of device results -> the mapped host buffer h_dst (one of the
+   slot's h_err / h_terr / h_tag) by a kernel on the slot's stream. */
+int  fd_amd_slot_out( slot_t * s, void * h_dst, void const * d_src, ulong n );
+/* Chunk of n signatures staged in s->h_pack as [pub 32n | sig 64n | off 4n | sz 4n | blob]. */
 int  fd_amd_slot_launch_packed( slot_t * s, ulong n, ulong blob_sz, schar * out );
 /* 1 if the slot's chunk finished (or nothing is in flight), 0 if still
    running, negative on a HIP error.  Non-blocking. */

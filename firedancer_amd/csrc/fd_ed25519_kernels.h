@@ -49,11 +49,15 @@ int fd_amd_launch_txn_reduce( uint32_t txn_cnt, uint32_t const * d_fp, uint32_t 
 int fd_amd_launch_sign( uint32_t n, uint8_t const * d_prv, uint32_t const * d_off, uint32_t const * d_sz,
                         uint8_t const * d_blob, uint8_t * d_pub, uint8_t * d_sig, hipStream_t stream );
 
-/* Zero-copy tile staging (k_zgather): frag i at d_dc + 64*d_chunk[i]
-   (host memory mapped into the GPU), d_fsz[i] bytes pub|sig|msg -> SoA
-   planes, msg_off relative to d_dc. */
-int fd_amd_launch_zgather( uint32_t n, uint32_t const * d_chunk, uint32_t const * d_fsz, uint8_t const * d_dc,
-                           uint8_t * d_pub, uint8_t * d_sig, uint32_t * d_off, uint32_t * d_sz, hipStream_t stream );
+/* Streaming-tile staging (k_tile_gather).  d_meta = [ichunk n | ochunk n |
+   fsz n] (u32): frag i is copied from d_src + 64*ichunk[i] (mapped host data
+   region) into frame i of d_mir (stride bytes apart, device) and, when
+   d_out != NULL, to d_out + 64*ochunk[i] (mapped output dcache).  txn == 0
+   (pub|sig|msg): d_pub/d_sig planes + msg_off/msg_sz into d_mir; txn == 1:
+   payload offset/size into d_mir in d_off/d_sz. */
+int fd_amd_launch_tile_gather( uint32_t n, uint32_t const * d_meta, uint8_t const * d_src, uint8_t * d_out,
+                               uint8_t * d_mir, uint32_t stride, int txn, uint8_t * d_pub, uint8_t * d_sig,
+                               uint32_t * d_off, uint32_t * d_sz, hipStream_t stream );
 
 /* Dense slide digits of the last call on workspace d_ws (debug): u16
    [n][256] (low byte h digit, high byte s digit) rebuilt from the event
@@ -62,6 +66,9 @@ int fd_amd_launch_digits_dense( uint32_t n, void const * d_ws, uint16_t * d_dig,
 
 /* 1 when a batch of n takes the latency kernels (k_front + k_dsm4). */
 int fd_amd_uses_latency_path( uint32_t n, int dsm_mode );
+
+/* d_off[i] -= lo for every nonempty message (0 for empty ones). */
+int fd_amd_launch_rebase_off( uint32_t n, uint32_t * d_off, uint32_t const * d_sz, uint32_t lo, hipStream_t stream );
 
 /* n bytes device -> mapped host memory by a kernel (no DMA engine). */
 int fd_amd_launch_copy_out( void * d_dst_mapped, void const * d_src, size_t n, hipStream_t stream );

@@ -970,29 +970,51 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
 }
 
 /* ------------------------------------------------------------------ */
-/* k_zgather: zero-copy staging for the streaming tile.  The tango data
-   region is host memory registered with the GPU (hipHostRegister); frag i
-   lives at chunk[i]*64 in it, framed public_key | signature | message.  Copy
-   the 96 header bytes into the SoA planes and point msg_off at the message
-   inside the mapped region, which k_prep then reads over PCIe in place. */
-__global__ void __launch_bounds__(64)
-k_zgather( u32 n, u32 const * __restrict__ chunk, u32 const * __restrict__ fsz, u8 const * __restrict__ dc,
-           u8 * __restrict__ pub, u8 * __restrict__ sig, u32 * __restrict__ moff, u32 * __restrict__ msz ) {
-  u32 i = blockIdx.x * 64u + threadIdx.x;
+/* k_tile_gather: the streaming tile's staging.  Frag i (fsz[i] bytes at
+   chunk ichunk[i] of `src`, host memory mapped into the GPU: the input
+   dcache in zero-copy mode, the tile's own output dcache in copy mode) is
+   copied into frame i of the slot's device frame buffer `mir` (stride B
+   apart) and, when `out` != NULL (zero-copy mode), into chunk ochunk[i] of
+   the tile-owned output dcache, so the bytes the tile publishes are the
+   bytes it verified.  PUB_SIG_MSG frags also get their SoA planes (pub,
+   sig; the message stays in `mir`), TXN frags their payload offset/size in
+   `mir`.  One wave per frag (4 per block), 16 B per lane: the frames are
+   chunk-aligned, so every 16-B word is whole; the tail word past fsz stays
+   inside the frag's chunk pair. */
+__global__ void __launch_bounds__(256)
+k_tile_gather( u32 n, u32 const * __restrict__ meta, u8 const * __restrict__ src, u8 * __restrict__ out,
+               u8 * __restrict__ mir, u32 stride, int txn, u8 * __restrict__ pub, u8 * __restrict__ sig,
+               u32 * __restrict__ moff, u32 * __restrict__ msz ) {
+  u32 i = blockIdx.x * 4u + (threadIdx.x >> 6), l = threadIdx.x & 63u;
   if( i >= n ) return;
-  uint4 const * src = (uint4 const *)(dc + ((size_t)chunk[i] << 6));    /* chunks are 64-aligned */
-  uint4 a0 = src[0], a1 = src[1], s0 = src[2], s1 = src[3], s2 = src[4], s3 = src[5];
-  uint4 * P = (uint4 *)(pub + 32UL*i); P[0] = a0; P[1] = a1;
-  uint4 * S = (uint4 *)(sig + 64UL*i); S[0] = s0; S[1] = s1; S[2] = s2; S[3] = s3;
-  moff[i] = (chunk[i] << 6) + 96u;
-  msz[i]  = fsz[i] - 96u;
+  u32 ic = meta[i], oc = meta[n + i], sz = meta[2u*n + i];
+  uint4 const * s = (uint4 const *)(src + ((size_t)ic << 6));
+  uint4 * m = (uint4 *)(mir + (size_t)i * stride);
+  uint4 * o = out ? (uint4 *)(out + ((size_t)oc << 6)) : (uint4 *)0;
+  u32 nv = (sz + 15u) >> 4;
+  uint4 v0 = make_uint4( 0u, 0u, 0u, 0u );
+  for( u32 k = l; k < nv; k += 64u ) {
+    uint4 v = s[k];
+    if( k == l ) v0 = v;
+    m[k] = v;
+    if( o ) o[k] = v;
+  }
+  if( txn ) {
+    if( !l ) { moff[i] = i * stride; msz[i] = sz; }
+  } else {
+    if( l < 2u )      ((uint4 *)(pub + 32UL*i))[l]      = v0;     /* host checked fsz >= 96 */
+    else if( l < 6u ) ((uint4 *)(sig + 64UL*i))[l - 2u] = v0;
+    if( !l ) { moff[i] = i * stride + 96u; msz[i] = sz - 96u; }
+  }
 }
 
 int
-fd_amd_launch_zgather( uint32_t n, uint32_t const * d_chunk, uint32_t const * d_fsz, uint8_t const * d_dc,
-                       uint8_t * d_pub, uint8_t * d_sig, uint32_t * d_off, uint32_t * d_sz, hipStream_t stream ) {
+fd_amd_launch_tile_gather( uint32_t n, uint32_t const * d_meta, uint8_t const * d_src, uint8_t * d_out,
+                           uint8_t * d_mir, uint32_t stride, int txn, uint8_t * d_pub, uint8_t * d_sig,
+                           uint32_t * d_off, uint32_t * d_sz, hipStream_t stream ) {
   if( !n ) return 0;
-  hipLaunchKernelGGL( k_zgather, dim3((n + 63u)/64u), dim3(64), 0, stream, n, d_chunk, d_fsz, d_dc, d_pub, d_sig, d_off, d_sz );
+  hipLaunchKernelGGL( k_tile_gather, dim3((n + 3u)/4u), dim3(256), 0, stream, n, d_meta, d_src, d_out, d_mir, stride, txn,
+                      d_pub, d_sig, d_off, d_sz );
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1016,6 +1038,23 @@ int
 fd_amd_launch_digits_dense( uint32_t n, void const * d_ws, uint16_t * d_dig, hipStream_t stream ) {
   if( !n ) return 0;
   hipLaunchKernelGGL( k_digits_dense, dim3((n + 63u)/64u), dim3(64), 0, stream, n, (u8 const *)d_ws, fd_amd_ws_layout( n ), d_dig );
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+/* Registered-memory batches: message offsets arrive as the caller wrote
+   them (into its whole blob); the chunk's message window [lo, ...) was
+   copied to the start of the device blob, so rebase them (empty messages
+   point at 0, never outside the window). */
+__global__ void __launch_bounds__(256)
+k_rebase_off( u32 n, u32 * __restrict__ off, u32 const * __restrict__ sz, u32 lo ) {
+  u32 i = blockIdx.x * 256u + threadIdx.x;
+  if( i < n ) off[i] = sz[i] ? off[i] - lo : 0u;
+}
+
+int
+fd_amd_launch_rebase_off( uint32_t n, uint32_t * d_off, uint32_t const * d_sz, uint32_t lo, hipStream_t stream ) {
+  if( !n ) return 0;
+  hipLaunchKernelGGL( k_rebase_off, dim3((n + 255u)/256u), dim3(256), 0, stream, n, d_off, d_sz, lo );
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -205,8 +205,15 @@ k_txn_parse( u32 txn_cnt, u8 const * __restrict__ payload, u32 const * __restric
     for( u32 s=b; s<e; s++ ) skip[s] = (i8)TXN_ERR_PARSE;
     return;
   }
-  /* host reserved payload[0] slots; a parsed transaction has exactly that many */
-  for( u32 i=0u; i<nsig && b+i<e; i++ ) {
+  /* host reserved payload[0] slots; a parsed transaction has exactly that
+     many.  A caller-supplied tbase that reserved a different count (device
+     API) rejects the transaction instead of verifying a subset: fail closed */
+  if( e - b != nsig ) {
+    if( fp_out ) fp_out[t] = 0u;
+    for( u32 s=b; s<e; s++ ) skip[s] = (i8)TXN_ERR_PARSE;
+    return;
+  }
+  for( u32 i=0u; i<nsig; i++ ) {
     u32 s = b + i;
     copy_dw( (u32 *)(pub + 32UL*s), p + acct_off + 32u*i,  8u );
     copy_dw( (u32 *)(sig + 64UL*s), p + sig_off  + 64u*i, 16u );

@@ -12,14 +12,22 @@
  *   dedup  -- HA tag cache (tag = first 8 signature bytes), FD_TCACHE_INSERT
  *             semantics (src/tango/tcache/fd_tcache.h:372-403): a tag is a
  *             duplicate iff it is one of the last `depth` distinct tags
- *   stage  -- copy pub/sig/msg into the pinned staging of the free engine slot
+ *   stage  -- reserve a frame of the tile-owned output dcache; copy mode:
+ *             copy the frag into it, re-check the mcache line, release the
+ *             input frag; zero-copy: hand the GPU (chunk, size) only
  *   launch -- adaptive batching: launch when the batch is full, or when the
  *             GPU is idle (no batch in flight), or when the oldest staged
- *             frag waited batch_wait_ns; two slots, so one batch stages
- *             while the other verifies
+ *             frag waited batch_wait_ns; up to 4 batches in flight
  *   publish-- when the oldest batch completes, publish its passing frags in
- *             arrival order (fd_mcache_publish protocol) with the GPU's
- *             SHA-512-derived dedup tag as meta.sig; failures count SV_FILT
+ *             arrival order (fd_mcache_publish protocol) out of the output
+ *             dcache, with the GPU's SHA-512-derived dedup tag as meta.sig;
+ *             failures count SV_FILT; zero-copy releases the batch's input
+ *             frags only now
+ *
+ * The output data region follows the reference tile's ownership model: the
+ * tile publishes frags from a dcache it owns (fd_frank_verify_synth_load.c:
+ * 324,409-411) and takes output credit from its consumers' fseq
+ * (fd_frank_verify.c:85-92,167).
  */
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -96,7 +104,8 @@ struct tcache_t {
 };
 
 struct pending_t {            /* one staged / in-flight frag */
-  uint   chunk;
+  ulong  seq;                 /* input sequence number */
+  ulong  frame;               /* output frame reservation (monotonic; frame = frame % frame_cnt) */
   ushort sz, ctl;
   uint   tsorig;
 };
@@ -136,6 +145,21 @@ inline ulong now_ns( void ) {
 
 } /* namespace */
 
+#define FRAME_CHUNKS ((uint)(FD_VERIFY_AMD_FRAME_SZ >> FD_CHUNK_LG_SZ))
+#define FRAME_FREE   (~0UL)
+#define TXN_SIG_MAX_AT_MTU (19UL)   /* most signatures fd_amd_txn_slots1 reserves for a 1232-B payload */
+
+struct tile_slot_t {
+  uint32_t * h_meta;             /* pinned, mapped: [ichunk n | ochunk n | fsz n | tbase n+1] of the batch */
+  uint32_t * m_meta;             /* its device address (the kernels read it in place) */
+  uint8_t  * d_mir;              /* device frames of the batch, FD_VERIFY_AMD_FRAME_SZ apart */
+  std::vector<pending_t> pend;
+  std::vector<uint32_t>  ich, fsz, tb;
+  ulong seq_lo;                  /* first input seq of the batch (zero-copy release point) */
+  ulong frame_hi;                /* frame reservation counter after the batch's last frame */
+  ulong nsig;                    /* signature slots (TXN) */
+};
+
 struct fd_verify_amd_tile {
   fd_ed25519_amd_t * eng;
   ulong              batch_max;
@@ -146,13 +170,20 @@ struct fd_verify_amd_tile {
   uint8_t *          reg_base;  /* host data region mapped into the GPU (zero copy) */
   ulong              reg_sz;
   uint8_t *          reg_dev;
-  std::vector<pending_t> meta[FD_AMD_SLOT_MAX];
+  /* the tile-owned output dcache: frame_cnt frames, pinned and mapped */
+  uint8_t *          out_base;
+  uint8_t *          out_dev;
+  ulong              frame_cnt;
+  std::vector<ulong> frame_pub;  /* out seq of the frag a frame last carried (FRAME_FREE: none) */
+  ulong              frame_next, frame_retired;
+  tile_slot_t        ts[FD_AMD_SLOT_MAX];
 };
 
 extern "C" int
 fd_verify_amd_tile_register_dcache( fd_verify_amd_tile_t * t, void * base, ulong sz ) {
   if( !t || !base || !sz ) return FD_ED25519_AMD_ERR_INVAL;
   if( hipSetDevice( t->eng->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  if( t->reg_base ) { (void)hipHostUnregister( t->reg_base ); t->reg_base = NULL; t->reg_dev = NULL; t->reg_sz = 0; }
   uintptr_t lo = (uintptr_t)base & ~(uintptr_t)4095, hi = ((uintptr_t)base + sz + 4095) & ~(uintptr_t)4095;
   if( hipHostRegister( (void *)lo, hi - lo, hipHostRegisterMapped ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
   void * dev = NULL;
@@ -168,8 +199,20 @@ extern "C" int
 fd_verify_amd_tile_set_framing( fd_verify_amd_tile_t * t, int framing ) {
   if( !t || (framing != FD_VERIFY_AMD_FRAMING_PUB_SIG_MSG && framing != FD_VERIFY_AMD_FRAMING_TXN) )
     return FD_ED25519_AMD_ERR_INVAL;
+  /* every transaction must fit an empty batch, else the tile could never stage it */
+  if( framing == FD_VERIFY_AMD_FRAMING_TXN && t->batch_max < TXN_SIG_MAX_AT_MTU ) return FD_ED25519_AMD_ERR_INVAL;
   t->framing = framing;
   return FD_ED25519_AMD_OK;
+}
+
+extern "C" void *
+fd_verify_amd_tile_out_chunk0( fd_verify_amd_tile_t * t ) {
+  return t ? t->out_base : NULL;
+}
+
+extern "C" ulong
+fd_verify_amd_tile_out_data_sz( fd_verify_amd_tile_t * t ) {
+  return t ? t->frame_cnt * FD_VERIFY_AMD_FRAME_SZ : 0UL;
 }
 
 #define TILE_NSLOT (4)   /* batches in flight (FD_AMD_TILE_NSLOT overrides; 6 or 8 measured: higher
@@ -181,73 +224,159 @@ fd_verify_amd_tickcount( void ) {
   return (uint)now_ns();
 }
 
+extern "C" void
+fd_verify_amd_tile_delete( fd_verify_amd_tile_t * t ) {
+  if( !t ) return;
+  (void)hipSetDevice( t->eng->device );
+  fd_ed25519_amd_delete( t->eng );   /* synchronises every slot stream first */
+  if( t->reg_base ) (void)hipHostUnregister( t->reg_base );
+  for( int k=0; k<FD_AMD_SLOT_MAX; k++ ) {
+    if( t->ts[k].h_meta ) (void)hipHostFree( t->ts[k].h_meta );
+    if( t->ts[k].d_mir  ) (void)hipFree( t->ts[k].d_mir );
+  }
+  if( t->out_base ) (void)hipHostFree( t->out_base );
+  delete t;
+}
+
 extern "C" fd_verify_amd_tile_t *
-fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong tcache_depth ) {
-  if( !batch_max ) return NULL;
+fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong tcache_depth, ulong out_frame_cnt ) {
+  if( !batch_max || batch_max > (1UL<<20) ) return NULL;
   int nslot = TILE_NSLOT;
   if( char const * v = getenv( "FD_AMD_TILE_NSLOT" ) ) nslot = atoi( v );
   if( nslot < 2 || nslot > FD_AMD_SLOT_MAX ) return NULL;
-  fd_ed25519_amd_t * eng = fd_amd_engine_new( device, batch_max, batch_max * FD_ED25519_AMD_MSG_MAX, nslot );
+  if( !out_frame_cnt ) out_frame_cnt = 4096UL + (ulong)(nslot + 1) * batch_max;
+  if( out_frame_cnt > (0xFFFFFFFFUL / FRAME_CHUNKS) ) return NULL;   /* chunk indices are 32-bit */
+  /* the engine's own staging is unused by the tile (frags reach the GPU
+     through the output frames), so it is sized for a single message */
+  fd_ed25519_amd_t * eng = fd_amd_engine_new( device, batch_max, FD_ED25519_AMD_MSG_MAX, nslot );
   if( !eng ) return NULL;
-  for( int k=0; k<nslot; k++ )
-    if( fd_amd_slot_alloc_aux( &eng->slot[k], batch_max ) ) { fd_ed25519_amd_delete( eng ); return NULL; }
   fd_verify_amd_tile_t * t = new fd_verify_amd_tile_t();
   t->eng = eng; t->batch_max = batch_max; t->wait_ns = batch_wait_ns; t->nslot = nslot;
   t->framing = FD_VERIFY_AMD_FRAMING_PUB_SIG_MSG;
   t->tc.init( tcache_depth );
-  for( int k=0; k<nslot; k++ ) t->meta[k].resize( batch_max );
+  bool ok = true;
+  for( int k=0; k<nslot && ok; k++ ) {
+    tile_slot_t & s = t->ts[k];
+    ok = !fd_amd_slot_alloc_aux( &eng->slot[k], batch_max ) &&
+         hipHostMalloc( (void **)&s.h_meta, 4UL*(4UL*batch_max + 1UL), hipHostMallocMapped ) == hipSuccess &&
+         hipHostGetDevicePointer( (void **)&s.m_meta, s.h_meta, 0 ) == hipSuccess &&
+         hipMalloc( (void **)&s.d_mir, batch_max * FD_VERIFY_AMD_FRAME_SZ + 64UL ) == hipSuccess;
+    s.pend.resize( batch_max ); s.ich.resize( batch_max ); s.fsz.resize( batch_max ); s.tb.resize( batch_max + 1UL );
+  }
+  ok = ok && hipHostMalloc( (void **)&t->out_base, out_frame_cnt * FD_VERIFY_AMD_FRAME_SZ, hipHostMallocMapped ) == hipSuccess &&
+       hipHostGetDevicePointer( (void **)&t->out_dev, t->out_base, 0 ) == hipSuccess;
+  if( !ok ) { fd_verify_amd_tile_delete( t ); return NULL; }
+  t->frame_cnt = out_frame_cnt;
+  t->frame_pub.assign( out_frame_cnt, FRAME_FREE );
   return t;
 }
 
-extern "C" void
-fd_verify_amd_tile_delete( fd_verify_amd_tile_t * t ) {
-  if( !t ) return;
-  if( t->reg_base ) { (void)hipSetDevice( t->eng->device ); (void)hipHostUnregister( t->reg_base ); }
-  fd_ed25519_amd_delete( t->eng );
-  delete t;
+/* Launch the staged batch of tile slot k (n frags; nsig signature slots
+   for TXN framing).  src: the mapped region the GPU copies the frags from
+   (input dcache in zero-copy mode, the output dcache in copy mode); out:
+   the mapped output dcache when the GPU must fill the output frames. */
+static int
+tile_launch( fd_verify_amd_tile_t * t, int k, ulong n, bool txn, uint8_t const * src, uint8_t * out ) {
+  slot_t *      s  = &t->eng->slot[k];
+  tile_slot_t & ts = t->ts[k];
+  uint32_t * hm = ts.h_meta;
+  memcpy( hm, ts.ich.data(), 4UL*n );
+  for( ulong i=0; i<n; i++ ) hm[n + i] = (uint32_t)((ts.pend[i].frame % t->frame_cnt) * FRAME_CHUNKS);
+  memcpy( hm + 2UL*n, ts.fsz.data(), 4UL*n );
+  uint32_t const * m_tbase = ts.m_meta + 3UL*n;
+  if( txn ) memcpy( hm + 3UL*n, ts.tb.data(), 4UL*(n + 1UL) );
+  if( fd_amd_launch_tile_gather( (uint32_t)n, ts.m_meta, src, out, ts.d_mir, (uint32_t)FD_VERIFY_AMD_FRAME_SZ, txn ? 1 : 0,
+                                 s->d_pub, s->d_sig, txn ? s->d_toff : s->d_off, txn ? s->d_tsz : s->d_sz, s->stream ) )
+    return FD_ED25519_AMD_ERR_DEVICE;
+  /* tile batches are small next to the GPU, so the 4-lane latency kernels
+     are used even with 4 in flight.  Measured (profiles/r01_tile_policy_ab.txt):
+     switching batches of >= 4096/8192 to the 1-lane kernel while others were
+     in flight lowered the saturated rate at every batch_max and doubled
+     latency; the in-flight work (4 x batch_max) is too small for the 1-lane
+     kernel to fill the GPU. */
+  if( txn ) {
+    ulong nsig = ts.nsig;
+    if( fd_amd_launch_txn_parse( (uint32_t)n, ts.d_mir, s->d_toff, s->d_tsz, s->d_fp, NULL, 0, m_tbase,
+                                 s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_skip, s->stream ) )
+      return FD_ED25519_AMD_ERR_DEVICE;
+    if( nsig && fd_amd_launch_verify( (uint32_t)nsig, s->d_pub, s->d_sig, s->d_off, s->d_sz, ts.d_mir, s->d_err,
+                                      s->d_ws, s->stream, 0, NULL, s->d_skip, 0 ) )
+      return FD_ED25519_AMD_ERR_DEVICE;
+    if( fd_amd_launch_txn_reduce( (uint32_t)n, s->d_fp, m_tbase, s->d_err, s->d_terr, s->stream ) )
+      return FD_ED25519_AMD_ERR_DEVICE;
+    if( fd_amd_slot_out( s, s->h_terr, s->d_terr, n ) ) return FD_ED25519_AMD_ERR_DEVICE;
+    if( nsig ) {
+      ws_layout_t L = fd_amd_ws_layout( nsig );
+      if( fd_amd_slot_out( s, s->h_tag, (uint8_t *)s->d_ws + L.tag, 8UL*nsig ) ) return FD_ED25519_AMD_ERR_DEVICE;
+    }
+  } else {
+    if( fd_amd_launch_verify( (uint32_t)n, s->d_pub, s->d_sig, s->d_off, s->d_sz, ts.d_mir, s->d_err, s->d_ws,
+                              s->stream, 1, NULL, NULL, 0 ) )
+      return FD_ED25519_AMD_ERR_DEVICE;
+    if( fd_amd_slot_out( s, s->h_err, s->d_err, n ) ) return FD_ED25519_AMD_ERR_DEVICE;
+    ws_layout_t L = fd_amd_ws_layout( n );
+    if( fd_amd_slot_out( s, s->h_tag, (uint8_t *)s->d_ws + L.tag, 8UL*n ) ) return FD_ED25519_AMD_ERR_DEVICE;
+  }
+  if( hipEventRecord( s->done, s->stream ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  s->out = s->t_out = s->s_out = NULL;
+  s->n = n; s->t_n = n; s->busy = 1;
+  return FD_ED25519_AMD_OK;
 }
 
 extern "C" int
 fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ulong in_depth,
-                        void const * in_chunk0, ulong in_seq0, fd_frag_meta_t * out_mcache, ulong out_depth,
-                        ulong out_seq0, ulong const * out_fseq, ulong frag_cnt, int const * stop,
+                        void const * in_chunk0, ulong in_seq0, ulong * in_fseq, fd_frag_meta_t * out_mcache,
+                        ulong out_depth, ulong out_seq0, ulong const * out_fseq, ulong frag_cnt, int const * stop,
                         fd_verify_amd_diag_t * diag, uint * lat, ulong lat_max ) {
-  if( !t || !in_mcache || !in_depth || (in_depth & (in_depth-1UL)) || !out_mcache || !out_depth ||
+  if( !t || !in_mcache || !in_depth || (in_depth & (in_depth-1UL)) || !in_chunk0 || !out_mcache || !out_depth ||
       (out_depth & (out_depth-1UL)) || !diag || (!frag_cnt && !stop) ) return FD_ED25519_AMD_ERR_INVAL;
   fd_ed25519_amd_t * e = t->eng;
   if( hipSetDevice( e->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  bool txn = t->framing == FD_VERIFY_AMD_FRAMING_TXN;
+  if( txn && t->batch_max < TXN_SIG_MAX_AT_MTU ) return FD_ED25519_AMD_ERR_INVAL;
+
+  ulong const F = t->frame_cnt;
+  /* a new run starts a new output session: no frame is held for a consumer */
+  std::fill( t->frame_pub.begin(), t->frame_pub.end(), FRAME_FREE );
+  t->frame_next = t->frame_retired = 0UL;
 
   ulong in_seq = in_seq0, out_seq = out_seq0, lat_n = 0;
   int   K = t->nslot;
   int   stage = 0;                 /* slot being filled; slots are used round robin, so the */
   int   oldest = 0, nfly = 0;      /* in-flight ones are oldest, oldest+1, ... (mod K)      */
-  ulong staged = 0, blob_at = 0, stage_t0 = 0, slots = 0;
+  ulong staged = 0, slots = 0, stage_t0 = 0;
   int   rc;
   /* Flow-control state shared with other threads is exchanged in strides,
      not per frag (the reference's tiles publish fseq and refresh credits
-     in housekeeping, fd_fctl): diag->in_cnt is published every 256 frags
-     and at the end of each staging pass; out_fseq is re-read only when the
-     cached credit runs out. */
-  ulong in_cnt = diag->in_cnt, out_cr = 0;
+     in housekeeping, fd_fctl): diag->in_cnt and in_fseq are published per
+     staging pass; out_fseq is re-read only when a cached value runs out. */
+  ulong in_cnt = diag->in_cnt, out_cr = 0, cons = out_seq0, fseq_pub = ~0UL;
 
-  bool txn = t->framing == FD_VERIFY_AMD_FRAMING_TXN;
   /* zero copy: the input data region is mapped into the GPU; frags are
-     handed over as (chunk, size) and gathered on the device */
+     handed over as (chunk, size) and copied on the device */
   uint8_t const * zc_dev = NULL;
   if( t->reg_base && (uint8_t const *)in_chunk0 >= t->reg_base &&
       (uint8_t const *)in_chunk0 < t->reg_base + t->reg_sz &&
-      t->reg_sz - (ulong)((uint8_t const *)in_chunk0 - t->reg_base) <= (1UL << 32) )
+      t->reg_sz - (ulong)((uint8_t const *)in_chunk0 - t->reg_base) <= (1UL << 38) )
     zc_dev = t->reg_dev + ((uint8_t const *)in_chunk0 - t->reg_base);
+
   auto publish = [&]( int k ) -> int {
-    slot_t * s = &e->slot[k];
+    slot_t *      s  = &e->slot[k];
+    tile_slot_t & ts = t->ts[k];
     if( (rc = fd_amd_slot_drain( s )) ) return rc;
-    ulong cnt = txn ? s->t_n : s->n;
+    ulong cnt = s->n;
     for( ulong i=0; i<cnt; i++ ) {
-      pending_t const & m = t->meta[k][i];
+      pending_t const & m = ts.pend[i];
+      /* zero copy: the GPU read the frag some time before now; if its mcache
+         line has been lapped since, the producer may have rewritten it */
+      if( zc_dev && __atomic_load_n( &in_mcache[ m.seq & (in_depth-1UL) ].seq, __ATOMIC_ACQUIRE ) != m.seq ) {
+        diag->ovrn_cnt++;
+        continue;
+      }
       int bad = txn ? s->h_terr[i] : s->h_err[i];
       if( bad ) { diag->sv_filt_cnt++; diag->sv_filt_sz += m.sz; continue; }
       /* dedup tag: the verify's SHA-512 tag of the (first) signature */
-      ulong tag = txn ? s->h_tag[ s->h_tbase[i] ] : s->h_tag[i];
+      ulong tag = txn ? s->h_tag[ ts.tb[i] ] : s->h_tag[i];
       if( out_fseq && (long)(out_seq - out_cr) >= 0 ) {   /* credit check against the slowest consumer */
         out_cr = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) + out_depth;
         if( (long)(out_seq - out_cr) >= 0 ) {
@@ -255,11 +384,14 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
           do out_cr = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) + out_depth; while( (long)(out_seq - out_cr) >= 0 );
         }
       }
+      ulong f = m.frame % F;
+      t->frame_pub[f] = out_seq;
       uint tspub = fd_verify_amd_tickcount();
-      fd_mcache_publish( out_mcache, out_depth, out_seq, tag, m.chunk, m.sz, m.ctl, m.tsorig, tspub );
+      fd_mcache_publish( out_mcache, out_depth, out_seq, tag, f * FRAME_CHUNKS, m.sz, m.ctl, m.tsorig, tspub );
       if( lat && lat_n < lat_max ) lat[lat_n++] = tspub - m.tsorig;
       out_seq++; diag->out_cnt++; diag->out_sz += m.sz;
     }
+    t->frame_retired = ts.frame_hi;
     return FD_ED25519_AMD_OK;
   };
 
@@ -273,16 +405,21 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
       if( (rc = publish( oldest )) ) return rc;
       oldest = (oldest + 1) % K; nfly--;
     }
-    bool done_in = frag_cnt ? (in_cnt >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
+    /* producer credit: copy mode is done with a frag once it is copied;
+       zero copy only once the batch holding it has retired */
+    if( in_fseq ) {
+      ulong rel = !zc_dev ? in_seq : nfly ? t->ts[oldest].seq_lo : staged ? t->ts[stage].seq_lo : in_seq;
+      if( rel != fseq_pub ) { __atomic_store_n( in_fseq, rel, __ATOMIC_RELEASE ); fseq_pub = rel; }
+    }
+    bool done_in = frag_cnt ? (in_seq - in_seq0 >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
     if( done_in && !staged && !nfly ) break;
     if( nfly == K ) continue;      /* every slot in flight: the staging slot is busy */
 
     /* 2. stage input frags into the free slot */
-    slot_t * s = &e->slot[stage];
+    tile_slot_t & ts = t->ts[stage];
     bool idle_in = false, full = false;
     while( !done_in && staged < t->batch_max ) {
-      if( frag_cnt && in_cnt >= frag_cnt ) break;
-      if( !(in_cnt & 255UL) ) __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
+      if( frag_cnt && in_seq - in_seq0 >= frag_cnt ) break;
       fd_frag_meta_t const * m = in_mcache + (in_seq & (in_depth-1UL));
       ulong seq_found = __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE );
       long  d = (long)(seq_found - in_seq);
@@ -291,118 +428,121 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
       ulong chunk = m->chunk, sz = m->sz, ctl = m->ctl, tsorig = m->tsorig;
       __atomic_thread_fence( __ATOMIC_ACQUIRE );
       if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != in_seq ) { diag->ovrn_cnt++; in_seq++; continue; }
-      uchar const * p = (uchar const *)fd_chunk_to_laddr_const( in_chunk0, chunk );
-      in_seq++;
-      in_cnt++;
-      if( !txn ) {
-        if( sz < 96UL || sz - 96UL > FD_ED25519_AMD_MSG_MAX ) { diag->bad_frag_cnt++; continue; }
-        ulong ha_tag; memcpy( &ha_tag, p + 32, 8 );                      /* first 8 signature bytes */
-        if( t->tc.insert( ha_tag ) ) { diag->ha_filt_cnt++; diag->ha_filt_sz += sz; continue; }
-        if( zc_dev ) {                                                   /* zero copy: metadata only */
-          s->h_off[staged] = (uint32_t)chunk; s->h_sz[staged] = (uint32_t)sz;
-        } else {
-          ulong msz = sz - 96UL;                                         /* blob_cap = batch_max*MSG_MAX: fits */
-          memcpy( s->h_pub + 32UL*staged, p,      32 );
-          memcpy( s->h_sig + 64UL*staged, p + 32, 64 );
-          memcpy( s->h_blob + blob_at,    p + 96, msz );
-          s->h_off[staged] = (uint32_t)blob_at; s->h_sz[staged] = (uint32_t)msz;
-          blob_at += msz;
-        }
-      } else {
-        /* wire transaction (fd_txn.h layout): dedup on its first signature */
-        if( sz > FD_ED25519_AMD_MSG_MAX ) { diag->bad_frag_cnt++; continue; }
-        ulong k2 = fd_amd_txn_slots1( p, sz );
-        if( slots + k2 > t->batch_max ) {                              /* no room for its signatures: next batch */
-          in_seq--; in_cnt--;
-          full = true;
-          break;
-        }
-        if( k2 ) {
-          ulong ha_tag; memcpy( &ha_tag, p + 1, 8 );
-          if( t->tc.insert( ha_tag ) ) { diag->ha_filt_cnt++; diag->ha_filt_sz += sz; continue; }
-        }
-        if( zc_dev ) {                                                   /* zero copy: parsed in place */
-          s->h_toff[staged] = (uint32_t)(chunk << FD_CHUNK_LG_SZ);
-        } else {
-          memcpy( s->h_blob + blob_at, p, sz );
-          s->h_toff[staged] = (uint32_t)blob_at;
-          blob_at += sz;
-        }
-        s->h_tsz[staged] = (uint32_t)sz; s->h_tbase[staged] = (uint32_t)slots;
-        slots += k2;
+      if( txn ? (!sz || sz > FD_ED25519_AMD_MSG_MAX) : (sz < 96UL || sz - 96UL > FD_ED25519_AMD_MSG_MAX) ) {
+        diag->bad_frag_cnt++; in_seq++; in_cnt++; continue;
       }
-      t->meta[stage][staged] = pending_t{ (uint)chunk, (ushort)sz, (ushort)ctl, (uint)tsorig };
-      if( !staged ) stage_t0 = now_ns();
+      /* reserve the next output frame: not staged or in flight, and no
+         longer read by a consumer that honours flow control */
+      ulong fr = t->frame_next, f = fr % F;
+      if( fr - t->frame_retired >= F ) { full = true; break; }
+      if( out_fseq && t->frame_pub[f] != FRAME_FREE && (long)(t->frame_pub[f] - cons) >= 0 ) {
+        cons = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE );
+        if( (long)(t->frame_pub[f] - cons) >= 0 ) { diag->backp_cnt++; full = true; break; }
+      }
+      uchar const * p = (uchar const *)fd_chunk_to_laddr_const( in_chunk0, chunk );
+      if( !zc_dev ) {
+        /* copy mode: the frame is the tile's copy; a frag lapped while it
+           was copied is dropped (speculative read, then seq re-check) */
+        uint8_t * dst = t->out_base + f * FD_VERIFY_AMD_FRAME_SZ;
+        memcpy( dst, p, sz );
+        __atomic_thread_fence( __ATOMIC_ACQUIRE );
+        if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != in_seq ) { diag->ovrn_cnt++; in_seq++; continue; }
+        p = dst;
+      }
+      ulong k2 = 0;
+      if( txn ) {
+        /* wire transaction (fd_txn.h layout): dedup on its first signature */
+        k2 = fd_amd_txn_slots1( p, sz );
+        if( slots + k2 > t->batch_max ) { full = true; break; }        /* no room for its signatures: next batch */
+      }
+      in_seq++; in_cnt++;
+      ulong ha_tag = 0;
+      if( !txn )   memcpy( &ha_tag, p + 32, 8 );                        /* first 8 signature bytes */
+      else if( k2 ) memcpy( &ha_tag, p + 1, 8 );
+      if( (!txn || k2) && t->tc.insert( ha_tag ) ) { diag->ha_filt_cnt++; diag->ha_filt_sz += sz; continue; }
+      t->frame_pub[f] = FRAME_FREE;
+      t->frame_next++;
+      ts.ich[staged] = zc_dev ? (uint32_t)chunk : (uint32_t)(f * FRAME_CHUNKS);
+      ts.fsz[staged] = (uint32_t)sz;
+      ts.tb[staged]  = (uint32_t)slots;
+      slots += k2;
+      ts.pend[staged] = pending_t{ in_seq - 1UL, fr, (ushort)sz, (ushort)ctl, (uint)tsorig };
+      if( !staged ) { stage_t0 = now_ns(); ts.seq_lo = in_seq - 1UL; }
       staged++;
     }
     __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
-    done_in = frag_cnt ? (in_cnt >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
+    if( in_fseq && !zc_dev && in_seq != fseq_pub ) { __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE ); fseq_pub = in_seq; }
+    done_in = frag_cnt ? (in_seq - in_seq0 >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
 
     /* 3. adaptive launch (a free slot exists here): full batch, input
           momentarily drained (greedy: under light load batches stay small
           and latency low; under load every slot is busy and batches grow
-          toward batch_max), end of input, or the oldest staged frag waited
-          batch_wait_ns.  A nonzero batch_wait_ns turns the greedy rule off
-          while another batch is in flight. */
+          toward batch_max), end of input, no frame or signature room left,
+          or the oldest staged frag waited batch_wait_ns.  A nonzero
+          batch_wait_ns turns the greedy rule off while another batch is in
+          flight. */
     bool greedy = idle_in && (!t->wait_ns || !nfly);
     if( staged && ( staged == t->batch_max || full || greedy || done_in ||
                     (t->wait_ns && now_ns() - stage_t0 >= t->wait_ns) ) ) {
-      /* kernel path by batch size: tile batches are small next to the GPU,
-         so the 4-lane latency kernels are used even with 4 in flight.
-         Measured (profiles/r01_tile_policy_ab.txt): switching batches
-         of >= 4096/8192 to the 1-lane kernel while others were in flight
-         lowered the saturated rate at every batch_max and doubled latency;
-         the in-flight work (4 x batch_max) is too small for the 1-lane
-         kernel to fill the GPU. */
-      s->dsm_mode = 0;
-      if( txn ) {
-        s->h_tbase[staged] = (uint32_t)slots;
-        if( (rc = fd_amd_slot_launch_txn( s, staged, slots, blob_at, NULL, NULL, 1, zc_dev )) ) return rc;
-        diag->batch_sig_cnt += slots;
-      } else if( zc_dev ) {
-        if( (rc = fd_amd_slot_launch_zc( s, staged, zc_dev )) ) return rc;
-        diag->batch_sig_cnt += staged;
-      } else {
-        if( (rc = fd_amd_slot_launch( s, staged, blob_at, NULL, 1 )) ) return rc;
-        diag->batch_sig_cnt += staged;
-      }
+      ts.tb[staged] = (uint32_t)slots;
+      ts.nsig = slots;
+      ts.frame_hi = t->frame_next;
+      uint8_t const * src = zc_dev ? zc_dev : t->out_dev;
+      if( (rc = tile_launch( t, stage, staged, txn, src, zc_dev ? t->out_dev : NULL )) ) return rc;
+      diag->batch_sig_cnt += txn ? slots : staged;
       diag->batch_cnt++;
       nfly++;
-      stage = (stage + 1) % K; staged = 0; blob_at = 0; slots = 0;
+      stage = (stage + 1) % K; staged = 0; slots = 0;
     }
   }
+  __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
+  if( in_fseq ) __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE );
   return FD_ED25519_AMD_OK;
 }
 
 /* ------------------------------------------------------------------ */
-/* streaming benchmark: producer -> tile -> consumer                    */
+/* streaming benchmark and end-to-end check: producer -> tile -> consumer */
 
 extern "C" int
-fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, double rate, int zero_copy,
-                            ulong pool_n, uchar const * pub, uchar const * sig, uint const * msg_off,
-                            uint const * msg_sz, uchar const * blob, ulong frag_cnt, double * out ) {
-  if( !pool_n || !frag_cnt || !out ) return FD_ED25519_AMD_ERR_INVAL;
+fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, double rate, int flags,
+                            ulong dcache_frames, ulong pool_n, uchar const * pub, uchar const * sig,
+                            uint const * msg_off, uint const * msg_sz, uchar const * blob, schar const * expect_err,
+                            ulong const * expect_tag, ulong frag_cnt, double * out ) {
+  if( !pool_n || !frag_cnt || !out || frag_cnt > 0xFFFFFFFFUL ) return FD_ED25519_AMD_ERR_INVAL;
+  for( ulong k=0; k<pool_n; k++ ) if( msg_sz[k] > FD_ED25519_AMD_MSG_MAX ) return FD_ED25519_AMD_ERR_INVAL;
+  bool zero_copy = !!(flags & FD_VERIFY_AMD_BENCH_ZERO_COPY);
+  bool writes    = !!(flags & FD_VERIFY_AMD_BENCH_WRITE);
+  bool lap       = writes && (flags & FD_VERIFY_AMD_BENCH_LAP);
+  bool check     = expect_err && expect_tag;
   ulong depth = 1UL; while( depth < 8UL*batch_max + 1024UL ) depth <<= 1;   /* > batches in flight + staging */
-  ulong mtu = 96UL + FD_ED25519_AMD_MSG_MAX;
-  ulong chunk_mtu = ((mtu + 2UL*FD_CHUNK_SZ - 1UL) >> (1 + FD_CHUNK_LG_SZ)) << 1;
-  /* The data region holds every pool frame once (what a NIC would have
-     DMA'd): the producer publishes metadata only, so the bench measures the
-     tile, not a producer-side memcpy. */
-  ulong data_chunks = chunk_mtu * pool_n;
-  std::vector<fd_frag_meta_t> in_mc( depth ), out_mc( depth );
-  for( ulong i=0; i<depth; i++ ) { in_mc[i].seq = i - depth; out_mc[i].seq = i - depth; }   /* "never published" */
-  uchar * dcache = (uchar *)aligned_alloc( 4096, ((data_chunks * FD_CHUNK_SZ + 4095UL) & ~4095UL) );
+  ulong out_depth = 1UL; while( out_depth < 2UL*batch_max + 1024UL ) out_depth <<= 1;
+  ulong const frame = FD_VERIFY_AMD_FRAME_SZ, frame_c = FRAME_CHUNKS;
+  /* Data region: either every pool frame once (what a NIC would have
+     DMA'd; the producer publishes metadata only, so the bench measures the
+     tile, not a producer-side memcpy), or a wrapping region of D frames the
+     producer writes before publishing (D > depth: a frame is rewritten only
+     after the mcache line of its previous frag was lapped, the tango sizing
+     that makes the consumer's seq re-check sufficient). */
+  ulong D = writes ? (dcache_frames ? dcache_frames : depth + 64UL) : pool_n;
+  if( writes && D <= depth ) return FD_ED25519_AMD_ERR_INVAL;
+  ulong region = (D * frame + 4095UL) & ~4095UL;
+  std::vector<fd_frag_meta_t> in_mc( depth ), out_mc( out_depth );
+  for( ulong i=0; i<depth; i++ )     in_mc[i].seq  = i - depth;       /* "never published" */
+  for( ulong i=0; i<out_depth; i++ ) out_mc[i].seq = i - out_depth;
+  uchar * dcache = (uchar *)aligned_alloc( 4096, region );
   if( !dcache ) return FD_ED25519_AMD_ERR_INVAL;
-  for( ulong k=0; k<pool_n; k++ ) {
-    uchar * p = dcache + k * chunk_mtu * FD_CHUNK_SZ;
+  memset( dcache, 0, region );
+  auto put_frame = [&]( uchar * p, ulong k ) {
     memcpy( p, pub + 32UL*k, 32 ); memcpy( p + 32, sig + 64UL*k, 64 ); memcpy( p + 96, blob + msg_off[k], msg_sz[k] );
-  }
+  };
+  if( !writes ) for( ulong k=0; k<pool_n; k++ ) put_frame( dcache + k * frame, k );
 
-  fd_verify_amd_tile_t * tile = fd_verify_amd_tile_new( device, batch_max, batch_wait_ns, 0UL );
+  fd_verify_amd_tile_t * tile = fd_verify_amd_tile_new( device, batch_max, batch_wait_ns, 0UL, 0UL );
   if( !tile ) { free( dcache ); return FD_ED25519_AMD_ERR_DEVICE; }
-  if( zero_copy && fd_verify_amd_tile_register_dcache( tile, dcache, data_chunks * FD_CHUNK_SZ ) ) {
+  if( zero_copy && fd_verify_amd_tile_register_dcache( tile, dcache, region ) ) {
     fd_verify_amd_tile_delete( tile ); free( dcache ); return FD_ED25519_AMD_ERR_DEVICE;
   }
+  uchar const * out_chunk0 = (uchar const *)fd_verify_amd_tile_out_chunk0( tile );
 
   /* the three spinning threads (producer, tile, consumer) each get a CPU of
      their own from the process's allowed set, so the scheduler does not
@@ -421,48 +561,80 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
     (void)pthread_setaffinity_np( pthread_self(), sizeof one, &one );
   };
 
-  std::atomic<ulong> in_fseq( 0UL ), out_fseq( 0UL );   /* consumer progress (credits) */
+  ulong in_fseq = 0UL;                                   /* the tile's credit to the producer */
+  std::atomic<ulong> out_fseq( 0UL );                    /* consumer progress (the tile's output credit) */
   std::vector<uint> lat( frag_cnt );
   fd_verify_amd_diag_t diag; memset( &diag, 0, sizeof diag );
   int tile_rc = 0;
+  ulong mism = 0, checked = 0;
   ulong t0 = now_ns();
 
   std::thread prod( [&]() {
     pin_to( 1 );
     ulong p0 = now_ns(), cr = 0;   /* cr: first seq not covered by the cached credit */
+    ulong lim = writes ? std::min( depth, D ) : depth;
     for( ulong seq=0; seq<frag_cnt; seq++ ) {
       ulong due = rate > 0.0 ? p0 + (ulong)((double)seq * 1e9 / rate) : 0UL;   /* paced: open loop */
       if( due ) while( now_ns() < due ) { /* spin */ }
-      /* credit: do not lap the tile's consumption of the input mcache
-         (refreshed only when the cached credit runs out) */
-      while( seq >= cr ) cr = __atomic_load_n( &diag.in_cnt, __ATOMIC_ACQUIRE ) + depth - 16UL;
+      /* credit: neither the mcache line nor (when writing) the data frame
+         of a frag the tile still reads is reused; refreshed only when the
+         cached credit runs out */
+      if( !lap ) while( seq >= cr ) cr = __atomic_load_n( &in_fseq, __ATOMIC_ACQUIRE ) + lim;
       ulong k = seq % pool_n, sz = 96UL + msg_sz[k];
-      /* tsorig = the scheduled send time when paced, so producer stalls count as latency */
-      uint tso = due ? (uint)due : fd_verify_amd_tickcount();
-      fd_mcache_publish( in_mc.data(), depth, seq, 0UL, k * chunk_mtu, sz, 3UL, tso, 0UL );
+      ulong fr = writes ? seq % D : k;
+      if( writes ) put_frame( dcache + fr * frame, k );
+      /* tsorig = the scheduled send time when paced, so producer stalls
+         count as latency; the input seq when lapping (the check needs it) */
+      uint tso = lap ? (uint)seq : due ? (uint)due : fd_verify_amd_tickcount();
+      fd_mcache_publish( in_mc.data(), depth, seq, 0UL, fr * frame_c, sz, 3UL, tso, 0UL );
     }
   } );
   std::thread cons( [&]() {
     pin_to( 2 );
     ulong seq = 0, fseq = 0;   /* fseq: last value published to out_fseq (every 64 frags, or when idle) */
+    ulong exp_s = 0;           /* check: next input seq that should be published */
+    long  last = -1;
     for( ;; ) {
-      if( __atomic_load_n( &tile_rc, __ATOMIC_ACQUIRE ) == 1 ) {   /* tile finished: drain what is there */
-        fd_frag_meta_t const * m = &out_mc[ seq & (depth-1UL) ];
-        if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != seq ) break;
-      }
-      fd_frag_meta_t const * m = &out_mc[ seq & (depth-1UL) ];
+      fd_frag_meta_t const * m = &out_mc[ seq & (out_depth-1UL) ];
       if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) == seq ) {
+        if( check ) {
+          ulong tag = m->sig, chunk = m->chunk, sz = m->sz, s_in;
+          if( lap ) {
+            s_in = m->tsorig;
+            if( (long)s_in <= last ) mism++;
+          } else {
+            while( exp_s < frag_cnt && expect_err[exp_s % pool_n] ) exp_s++;
+            s_in = exp_s++;
+          }
+          last = (long)s_in;
+          ulong k = s_in % pool_n;
+          uchar const * q = out_chunk0 + (chunk << FD_CHUNK_LG_SZ);
+          bool ok = s_in < frag_cnt && !expect_err[k] && tag == expect_tag[k] && sz == 96UL + msg_sz[k] &&
+                    !memcmp( q, pub + 32UL*k, 32 ) && !memcmp( q + 32, sig + 64UL*k, 64 ) &&
+                    !memcmp( q + 96, blob + msg_off[k], msg_sz[k] );
+          mism += !ok; checked++;
+        }
         seq++;
         if( seq - fseq >= 64UL ) { fseq = seq; out_fseq.store( seq, std::memory_order_release ); }
-      } else if( fseq != seq ) { fseq = seq; out_fseq.store( seq, std::memory_order_release ); }
+        continue;
+      }
+      if( __atomic_load_n( &tile_rc, __ATOMIC_ACQUIRE ) == 1 &&          /* tile finished and nothing left */
+          __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != seq ) break;
+      if( fseq != seq ) { fseq = seq; out_fseq.store( seq, std::memory_order_release ); }
+    }
+    if( check && !lap ) {     /* frags that should have been published and were not */
+      ulong want = 0;
+      for( ulong s=0; s<frag_cnt; s++ ) want += !expect_err[s % pool_n];
+      if( want > checked ) mism += want - checked;
     }
   } );
   ulong const * ofs = (ulong const *)&out_fseq;
   pin_to( 0 );
-  int rc = fd_verify_amd_tile_run( tile, in_mc.data(), depth, dcache, 0UL, out_mc.data(), depth, 0UL, ofs,
+  int rc = fd_verify_amd_tile_run( tile, in_mc.data(), depth, dcache, 0UL, &in_fseq, out_mc.data(), out_depth, 0UL, ofs,
                                    frag_cnt, NULL, &diag, lat.data(), frag_cnt );
   ulong t1 = now_ns();
   __atomic_store_n( &tile_rc, 1, __ATOMIC_RELEASE );
+  if( rc ) __atomic_store_n( &in_fseq, ~0UL >> 1, __ATOMIC_RELEASE );   /* unblock the producer */
   prod.join(); cons.join();
   if( pin ) (void)pthread_setaffinity_np( pthread_self(), sizeof saved, &saved );
   fd_verify_amd_tile_delete( tile );
@@ -470,11 +642,11 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   if( rc ) return rc;
   ulong n = std::min( (ulong)diag.out_cnt, frag_cnt );
   std::sort( lat.begin(), lat.begin() + (long)n );
-  auto pct = [&]( double q ) -> double { return n ? (double)lat[ std::min( n-1UL, (ulong)(q * (double)n) ) ] : 0.0; };
+  auto pct = [&]( double q ) -> double { return n && !lap ? (double)lat[ std::min( n-1UL, (ulong)(q * (double)n) ) ] : 0.0; };
   out[0] = (double)diag.in_cnt / ((double)(t1 - t0) * 1e-9);
   out[1] = pct( 0.50 ); out[2] = pct( 0.99 ); out[3] = pct( 0.999 );
   out[4] = diag.batch_cnt ? (double)diag.batch_sig_cnt / (double)diag.batch_cnt : 0.0;
-  out[5] = (double)diag.out_cnt; out[6] = (double)diag.sv_filt_cnt;
-  (void)in_fseq;
+  out[5] = (double)diag.out_cnt; out[6] = (double)diag.sv_filt_cnt; out[7] = (double)diag.ovrn_cnt;
+  out[8] = (double)mism; out[9] = (double)checked;
   return FD_ED25519_AMD_OK;
 }

@@ -78,19 +78,44 @@ def lib():
     L.fd_ed25519_amd_sign_dev.restype = i
     L.fd_ed25519_amd_set_small_batch_max.argtypes = [ul]
     L.fd_ed25519_amd_set_small_batch_max.restype = None
-    L.fd_verify_amd_tile_new.argtypes = [i, ul, ul, ul]
+    L.fd_verify_amd_tile_new.argtypes = [i, ul, ul, ul, ul]
     L.fd_verify_amd_tile_new.restype = vp
+    L.fd_verify_amd_tile_out_chunk0.argtypes = [vp]
+    L.fd_verify_amd_tile_out_chunk0.restype = vp
+    L.fd_verify_amd_tile_out_data_sz.argtypes = [vp]
+    L.fd_verify_amd_tile_out_data_sz.restype = ul
+    L.fd_ed25519_amd_host_register.argtypes = [vp, ul]
+    L.fd_ed25519_amd_host_register.restype = i
+    L.fd_ed25519_amd_host_unregister.argtypes = [vp]
+    L.fd_ed25519_amd_host_unregister.restype = i
+    L.fd_ed25519_amd_verify_soa_registered.argtypes = [vp, ul, vp, vp, vp, vp, vp, ul, vp]
+    L.fd_ed25519_amd_verify_soa_registered.restype = i
+    L.fd_ed25519_amd_multi_new.argtypes = [vp, ul, ul, ul]
+    L.fd_ed25519_amd_multi_new.restype = vp
+    L.fd_ed25519_amd_multi_delete.argtypes = [vp]
+    L.fd_ed25519_amd_multi_delete.restype = None
+    L.fd_ed25519_amd_multi_ndev.argtypes = [vp]
+    L.fd_ed25519_amd_multi_ndev.restype = ul
+    L.fd_ed25519_amd_shard_range.argtypes = [ul, ul, ul, c_ulong_p, c_ulong_p]
+    L.fd_ed25519_amd_shard_range.restype = None
+    L.fd_ed25519_amd_multi_verify_soa.argtypes = [vp, ul, vp, vp, vp, vp, vp, ul, vp]
+    L.fd_ed25519_amd_multi_verify_soa.restype = i
+    L.fd_ed25519_amd_multi_verify_txns.argtypes = [vp, ul, vp, vp, vp, ul, vp, vp, vp]
+    L.fd_ed25519_amd_multi_verify_txns.restype = i
+    L.fd_ed25519_amd_txn_slots.argtypes = [ul, vp, vp, vp, vp]
+    L.fd_ed25519_amd_txn_slots.restype = ul
     L.fd_verify_amd_tile_register_dcache.argtypes = [vp, vp, ul]
     L.fd_verify_amd_tile_register_dcache.restype = i
     L.fd_verify_amd_tile_set_framing.argtypes = [vp, i]
     L.fd_verify_amd_tile_set_framing.restype = i
     L.fd_verify_amd_tile_delete.argtypes = [vp]
     L.fd_verify_amd_tile_delete.restype = None
-    L.fd_verify_amd_tile_run.argtypes = [vp, vp, ul, vp, ul, vp, ul, ul, vp, ul, vp, vp, vp, ul]
+    L.fd_verify_amd_tile_run.argtypes = [vp, vp, ul, vp, ul, vp, vp, ul, ul, vp, ul, vp, vp, vp, ul]
     L.fd_verify_amd_tile_run.restype = i
     L.fd_verify_amd_tickcount.argtypes = []
     L.fd_verify_amd_tickcount.restype = ui
-    L.fd_verify_amd_bench_stream.argtypes = [i, ul, ul, ctypes.c_double, i, ul, vp, vp, vp, vp, vp, ul, vp]
+    L.fd_verify_amd_bench_stream.argtypes = [i, ul, ul, ctypes.c_double, i, ul, ul, vp, vp, vp, vp, vp, vp, vp, ul,
+                                             vp]
     L.fd_verify_amd_bench_stream.restype = i
     _lib = L
     return L
@@ -195,6 +220,18 @@ class Engine:
             raise EngineError("fd_ed25519_amd_verify_soa rc=%d" % rc)
         return err
 
+    def verify_soa_registered(self, pub, sig, msg_off, msg_sz, blob, err=None):
+        """fd_ed25519_amd_verify_soa_registered: every plane must lie in memory
+        registered with host_register (see RegisteredBatch); no host copy."""
+        n = int(pub.shape[0])
+        if err is None:
+            err = np.zeros(n, np.int8)
+        rc = lib().fd_ed25519_amd_verify_soa_registered(self._h, n, _ptr(pub), _ptr(sig), _ptr(msg_off), _ptr(msg_sz),
+                                                        _ptr(blob), int(blob.size), _ptr(err))
+        if rc:
+            raise EngineError("fd_ed25519_amd_verify_soa_registered rc=%d" % rc)
+        return err
+
     def verify_batch(self, msgs, sigs, pubs):
         """Pointer-array form: lists of bytes-like."""
         n = len(msgs)
@@ -215,21 +252,101 @@ class Engine:
         GPU, verify every signature (multi-signer rule), one verdict per
         transaction in {0, -1, -2, -3, FD_TXN_AMD_ERR_PARSE}.  With
         want_sigs, also returns (sig_base, sig_err)."""
-        payload = np.ascontiguousarray(payload, np.uint8)
-        off = np.ascontiguousarray(txn_off, np.uint32)
-        sz = np.ascontiguousarray(txn_sz, np.uint32)
-        n = int(off.size)
-        terr = np.zeros(max(n, 1), np.int8)
-        base = np.zeros(n + 1, np.uint32) if want_sigs else None
-        serr = np.zeros(max(payload.size // 65 + 1, 1), np.int8) if want_sigs else None
-        rc = lib().fd_ed25519_amd_verify_txns(self._h, n, _ptr(payload), _ptr(off), _ptr(sz), int(payload.size),
-                                              _ptr(terr), _ptr(base) if want_sigs else None,
-                                              _ptr(serr) if want_sigs else None)
+        return _verify_txns(lib().fd_ed25519_amd_verify_txns, self._h, payload, txn_off, txn_sz, want_sigs)
+
+
+def txn_slots(payload, txn_off, txn_sz):
+    """fd_ed25519_amd_txn_slots: (tbase[txn_cnt+1], total signature slots)."""
+    payload = np.ascontiguousarray(payload, np.uint8)
+    off = np.ascontiguousarray(txn_off, np.uint32)
+    sz = np.ascontiguousarray(txn_sz, np.uint32)
+    base = np.zeros(off.size + 1, np.uint32)
+    tot = lib().fd_ed25519_amd_txn_slots(int(off.size), _ptr(payload), _ptr(off), _ptr(sz), _ptr(base))
+    return base, int(tot)
+
+
+def _verify_txns(fn, h, payload, txn_off, txn_sz, want_sigs):
+    payload = np.ascontiguousarray(payload, np.uint8)
+    off = np.ascontiguousarray(txn_off, np.uint32)
+    sz = np.ascontiguousarray(txn_sz, np.uint32)
+    n = int(off.size)
+    terr = np.zeros(max(n, 1), np.int8)
+    base = serr = None
+    if want_sigs:
+        # sig_err is sized by the engine's own slot rule (overlapping or
+        # repeated txn_off entries reserve slots more than once)
+        base, tot = txn_slots(payload, off, sz)
+        serr = np.zeros(max(tot, 1), np.int8)
+    rc = fn(h, n, _ptr(payload), _ptr(off), _ptr(sz), int(payload.size), _ptr(terr),
+            _ptr(base) if want_sigs else None, _ptr(serr) if want_sigs else None)
+    if rc:
+        raise EngineError("verify_txns rc=%d" % rc)
+    if want_sigs:
+        return terr[:n], base, serr[:int(base[-1])]
+    return terr[:n]
+
+
+def shard_range(n, ndev, r):
+    """fd_ed25519_amd_shard_range: engine r's contiguous shard [lo, hi) of n."""
+    lo, hi = ctypes.c_ulong(), ctypes.c_ulong()
+    lib().fd_ed25519_amd_shard_range(int(n), int(ndev), int(r), ctypes.byref(lo), ctypes.byref(hi))
+    return lo.value, hi.value
+
+
+class MultiEngine:
+    """fd_ed25519_amd_multi_t: one engine + one persistent host thread per
+    entry of `devices` (repeats allowed); a batch is split into contiguous
+    shards verified concurrently, no collective."""
+
+    def __init__(self, devices, batch_max=1 << 16, blob_max=None):
+        if blob_max is None:
+            blob_max = max(batch_max * 256, MSG_MAX)
+        dv = np.ascontiguousarray(devices, np.int32)
+        self._h = lib().fd_ed25519_amd_multi_new(_ptr(dv), int(dv.size), int(batch_max), int(blob_max))
+        if not self._h:
+            raise EngineError("fd_ed25519_amd_multi_new(%r) failed" % (list(devices),))
+        self.ndev = int(lib().fd_ed25519_amd_multi_ndev(self._h))
+
+    def close(self):
+        if self._h:
+            lib().fd_ed25519_amd_multi_delete(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def verify_soa(self, pub, sig, msg_off, msg_sz, blob):
+        pub = np.ascontiguousarray(pub, np.uint8)
+        sig = np.ascontiguousarray(sig, np.uint8)
+        off = np.ascontiguousarray(msg_off, np.uint32)
+        sz = np.ascontiguousarray(msg_sz, np.uint32)
+        blob = np.ascontiguousarray(blob, np.uint8)
+        n = int(pub.shape[0])
+        err = np.zeros(max(n, 1), np.int8)
+        rc = lib().fd_ed25519_amd_multi_verify_soa(self._h, n, _ptr(pub), _ptr(sig), _ptr(off), _ptr(sz), _ptr(blob),
+                                                   int(blob.size), _ptr(err))
         if rc:
-            raise EngineError("fd_ed25519_amd_verify_txns rc=%d" % rc)
-        if want_sigs:
-            return terr[:n], base, serr[:int(base[-1])]
-        return terr[:n]
+            raise EngineError("fd_ed25519_amd_multi_verify_soa rc=%d" % rc)
+        return err[:n]
+
+    def verify_txns(self, payload, txn_off, txn_sz, want_sigs=False):
+        return _verify_txns(lib().fd_ed25519_amd_multi_verify_txns, self._h, payload, txn_off, txn_sz, want_sigs)
+
+
+def host_register(arr):
+    """Pin a numpy array's memory for fd_ed25519_amd_verify_soa_registered."""
+    rc = lib().fd_ed25519_amd_host_register(_ptr(arr), int(arr.nbytes))
+    if rc:
+        raise EngineError("fd_ed25519_amd_host_register rc=%d" % rc)
+
+
+def host_unregister(arr):
+    rc = lib().fd_ed25519_amd_host_unregister(_ptr(arr))
+    if rc:
+        raise EngineError("fd_ed25519_amd_host_unregister rc=%d" % rc)
 
 
 # ---------------------------------------------------------------- device-resident path

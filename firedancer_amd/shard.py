@@ -9,21 +9,19 @@ Two ways to run N GPUs:
   * one process per GPU (bench.py under torch.distributed.run): each rank
     verifies shard_range(n, rank, world); gloo carries only the start/stop
     barriers and the max-over-ranks of the elapsed time;
-  * one process driving every local GPU (MultiDeviceVerifier): one host
-    thread per device, each feeding its own engine.
+  * one process driving every local GPU: the native multi-device engine
+    (fd_ed25519_amd_multi_*, ed25519.MultiEngine), one engine and one
+    persistent host thread per device.
 """
-import threading
-
 import numpy as np
 
 
 def shard_range(n, rank, world):
-    """Contiguous [lo, hi) of n units for `rank` of `world` (sizes differ by <= 1)."""
+    """Contiguous [lo, hi) of n units for `rank` of `world` (sizes differ by
+    <= 1): lo = n*rank//world, the split fd_ed25519_amd_shard_range uses."""
     if world < 1 or not (0 <= rank < world):
         raise ValueError("bad rank/world %r/%r" % (rank, world))
-    base, extra = divmod(int(n), int(world))
-    lo = rank * base + min(rank, extra)
-    return lo, lo + base + (1 if rank < extra else 0)
+    return int(n) * rank // world, int(n) * (rank + 1) // world
 
 
 def max_over_ranks(value):
@@ -50,37 +48,3 @@ def _slice_soa(pub, sig, off, sz, blob, lo, hi):
     start, end = int(o.min()), int((o + s).max())
     return (pub[lo:hi], sig[lo:hi], (o - start).astype(np.uint32), sz[lo:hi],
             np.ascontiguousarray(blob[start:max(end, start + 1)]))
-
-
-class MultiDeviceVerifier:
-    """Verify one SoA batch across `devices` (one engine + host thread each)."""
-
-    def __init__(self, devices, batch_max=1 << 18, blob_max=None):
-        from . import ed25519
-        self.engines = [ed25519.Engine(device=d, batch_max=batch_max, blob_max=blob_max) for d in devices]
-
-    def verify_soa(self, pub, sig, msg_off, msg_sz, blob):
-        n = len(pub)
-        err = np.zeros(n, np.int8)
-        excs = []
-
-        def work(k, eng):
-            try:
-                lo, hi = shard_range(n, k, len(self.engines))
-                if hi > lo:
-                    err[lo:hi] = eng.verify_soa(*_slice_soa(pub, sig, msg_off, msg_sz, blob, lo, hi))
-            except Exception as e:  # surfaced below
-                excs.append(e)
-
-        th = [threading.Thread(target=work, args=(k, e)) for k, e in enumerate(self.engines)]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        if excs:
-            raise excs[0]
-        return err
-
-    def close(self):
-        for e in self.engines:
-            e.close()

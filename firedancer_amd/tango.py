@@ -54,21 +54,29 @@ def tickcount():
 
 
 class VerifyTile:
-    """fd_verify_amd_tile_t: adaptive-batching GPU verify tile."""
+    """fd_verify_amd_tile_t: adaptive-batching GPU verify tile that publishes
+    out of its own output dcache."""
 
     FRAMING_PUB_SIG_MSG = 0
     FRAMING_TXN = 1
+    FRAME_SZ = 1408
 
-    def __init__(self, device=0, batch_max=4096, batch_wait_ns=0, tcache_depth=1 << 16, framing=0):
-        self._h = ed25519.lib().fd_verify_amd_tile_new(int(device), int(batch_max), int(batch_wait_ns),
-                                                      int(tcache_depth))
+    def __init__(self, device=0, batch_max=4096, batch_wait_ns=0, tcache_depth=1 << 16, framing=0, out_frame_cnt=0):
+        L = ed25519.lib()
+        self._h = L.fd_verify_amd_tile_new(int(device), int(batch_max), int(batch_wait_ns), int(tcache_depth),
+                                           int(out_frame_cnt))
         if not self._h:
             raise ed25519.EngineError("fd_verify_amd_tile_new failed (no HIP device?)")
-        if ed25519.lib().fd_verify_amd_tile_set_framing(self._h, int(framing)):
-            raise ed25519.EngineError("bad framing %r" % framing)
+        if L.fd_verify_amd_tile_set_framing(self._h, int(framing)):
+            self.close()
+            raise ed25519.EngineError("bad framing %r for batch_max %d" % (framing, batch_max))
+        base = L.fd_verify_amd_tile_out_chunk0(self._h)
+        nbytes = int(L.fd_verify_amd_tile_out_data_sz(self._h))
+        self.out_region = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(base))
 
     def close(self):
         if self._h:
+            self.out_region = None
             ed25519.lib().fd_verify_amd_tile_delete(self._h)
             self._h = None
 
@@ -77,6 +85,10 @@ class VerifyTile:
             self.close()
         except Exception:
             pass
+
+    def out_frame(self, chunk, sz):
+        """Bytes of a published frag (fd_chunk_to_laddr(out_chunk0, chunk))."""
+        return bytes(self.out_region[CHUNK_SZ * int(chunk):CHUNK_SZ * int(chunk) + int(sz)])
 
     def register_dcache(self, region):
         """Map the numpy data region into the GPU (zero-copy staging)."""
@@ -87,31 +99,45 @@ class VerifyTile:
             raise ed25519.EngineError("fd_verify_amd_tile_register_dcache rc=%d" % rc)
 
     def run(self, in_mcache, in_chunk0, in_seq0, out_mcache, out_seq0, frag_cnt, lat_max=0):
-        """Consume frag_cnt input frags; returns (diag dict, latency samples)."""
+        """Consume frag_cnt input frags; returns (diag dict, latency samples).
+        self.in_fseq holds the tile's final producer credit."""
         diag = (ctypes.c_ulong * len(DIAG_FIELDS))()
         lat = np.zeros(max(lat_max, 1), np.uint32)
+        fseq = ctypes.c_ulong(0)
         vp = ctypes.c_void_p
         rc = ed25519.lib().fd_verify_amd_tile_run(
             self._h, vp(in_mcache.ctypes.data), in_mcache.size, vp(in_chunk0.ctypes.data), int(in_seq0),
-            vp(out_mcache.ctypes.data), out_mcache.size, int(out_seq0), None, int(frag_cnt), None,
+            ctypes.byref(fseq), vp(out_mcache.ctypes.data), out_mcache.size, int(out_seq0), None, int(frag_cnt), None,
             ctypes.byref(diag), vp(lat.ctypes.data) if lat_max else None, int(lat_max))
         if rc:
             raise ed25519.EngineError("fd_verify_amd_tile_run rc=%d" % rc)
+        self.in_fseq = fseq.value
         d = dict(zip(DIAG_FIELDS, list(diag)))
         return d, lat[:min(lat_max, d["out_cnt"])]
 
 
+BENCH_ZERO_COPY, BENCH_WRITE, BENCH_LAP = 1, 2, 4
+
+
 def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, blob, frag_cnt, rate=0.0,
-                 zero_copy=False):
+                 zero_copy=False, writes=False, lap=False, dcache_frames=0, expect_err=None, expect_tag=None):
     """fd_verify_amd_bench_stream: producer (rate frags/s, 0 = saturate) -> tile -> consumer; returns
-    dict(frags_per_s, p50_ns, p99_ns, p999_ns, mean_batch, published, sv_filt)."""
-    out = (ctypes.c_double * 7)()
+    dict(frags_per_s, p50_ns, p99_ns, p999_ns, mean_batch, published, sv_filt, ovrn, mismatches, checked).
+    With expect_err/expect_tag (per pool entry) the consumer checks every published frag."""
+    out = (ctypes.c_double * 10)()
     p = [np.ascontiguousarray(a) for a in (pub, sig, msg_off, msg_sz, blob)]
+    ee = np.ascontiguousarray(expect_err, np.int8) if expect_err is not None else None
+    et = np.ascontiguousarray(expect_tag, np.uint64) if expect_tag is not None else None
+    flags = (BENCH_ZERO_COPY if zero_copy else 0) | (BENCH_WRITE if writes else 0) | (BENCH_LAP if lap else 0)
     vp = ctypes.c_void_p
-    rc = ed25519.lib().fd_verify_amd_bench_stream(int(device), int(batch_max), int(batch_wait_ns), float(rate),
-                                                  int(bool(zero_copy)), p[0].shape[0],
-                                                  *[vp(a.ctypes.data) for a in p], int(frag_cnt), out)
+    rc = ed25519.lib().fd_verify_amd_bench_stream(int(device), int(batch_max), int(batch_wait_ns), float(rate), flags,
+                                                  int(dcache_frames), p[0].shape[0],
+                                                  *[vp(a.ctypes.data) for a in p],
+                                                  vp(ee.ctypes.data) if ee is not None else None,
+                                                  vp(et.ctypes.data) if et is not None else None,
+                                                  int(frag_cnt), out)
     if rc:
         raise ed25519.EngineError("fd_verify_amd_bench_stream rc=%d" % rc)
-    keys = ("frags_per_s", "p50_ns", "p99_ns", "p999_ns", "mean_batch", "published", "sv_filt")
+    keys = ("frags_per_s", "p50_ns", "p99_ns", "p999_ns", "mean_batch", "published", "sv_filt", "ovrn", "mismatches",
+            "checked")
     return dict(zip(keys, list(out)))

@@ -144,6 +144,72 @@ fd_ed25519_amd_verify_soa( fd_ed25519_amd_t * eng,
                            ulong              blob_sz,
                            schar *            err );
 
+/* Zero-copy host batch.  fd_ed25519_amd_host_register pins [base,
+   base+sz) of caller memory once (hipHostRegister, portable to every
+   device; FD_ED25519_AMD_ERR_DEVICE if the runtime refuses).  When pub,
+   sig, msg_off, msg_sz and blob all lie in registered memory,
+   fd_ed25519_amd_verify_soa_registered moves each chunk's planes and its
+   message window from the caller's memory to the device by DMA, with no
+   host-side copy (fd_ed25519_amd_verify_soa copies into pinned staging
+   first).  Same arguments, verdicts and errors as
+   fd_ed25519_amd_verify_soa; FD_ED25519_AMD_ERR_INVAL if a plane is not
+   registered.  A chunk whose messages are scattered over much more than
+   their total size is gathered through the staging instead. */
+int
+fd_ed25519_amd_host_register( void * base, ulong sz );
+
+int
+fd_ed25519_amd_host_unregister( void * base );
+
+int
+fd_ed25519_amd_verify_soa_registered( fd_ed25519_amd_t * eng,
+                                      ulong              n,
+                                      uchar const *      pub,
+                                      uchar const *      sig,
+                                      uint const *       msg_off,
+                                      uint const *       msg_sz,
+                                      uchar const *      blob,
+                                      ulong              blob_sz,
+                                      schar *            err );
+
+/* Multi-device engine (SURVEY s8 e: signatures are independent, so a batch
+   shards with no exchange step).  One engine and one persistent host thread
+   per entry of devices[0..ndev) (a device may be listed more than once:
+   several engines share it); a batch is split into contiguous shards, one
+   per engine, verified concurrently, and the call returns when every shard
+   is done.  No collective, no peer traffic: each shard's inputs go host ->
+   its device, its verdicts device -> host.  The reference scales the same
+   way, as N independent verify tiles each with its own input
+   (src/app/frank/fd_frank_init:67-80).  batch_max / blob_max are per
+   engine.  NULL on failure (any device unusable). */
+typedef struct fd_ed25519_amd_multi fd_ed25519_amd_multi_t;
+
+fd_ed25519_amd_multi_t *
+fd_ed25519_amd_multi_new( int const * devices, ulong ndev, ulong batch_max, ulong blob_max );
+
+void
+fd_ed25519_amd_multi_delete( fd_ed25519_amd_multi_t * multi );
+
+ulong
+fd_ed25519_amd_multi_ndev( fd_ed25519_amd_multi_t const * multi );
+
+/* Shard [lo, hi) of n items that engine r of ndev verifies: lo = n*r/ndev. */
+void
+fd_ed25519_amd_shard_range( ulong n, ulong ndev, ulong r, ulong * lo, ulong * hi );
+
+/* fd_ed25519_amd_verify_soa over the engines (same arguments and
+   verdicts; err[i] for every i).  Returns the first engine error, if any. */
+int
+fd_ed25519_amd_multi_verify_soa( fd_ed25519_amd_multi_t * multi,
+                                 ulong                    n,
+                                 uchar const *            pub,
+                                 uchar const *            sig,
+                                 uint const *             msg_off,
+                                 uint const *             msg_sz,
+                                 uchar const *            blob,
+                                 ulong                    blob_sz,
+                                 schar *                  err );
+
 /* Device-resident batch: every pointer is HIP device memory, already
    resident (the layout of fd_ed25519_amd_verify_soa).  Enqueues the
    verify kernels on `stream` (hipStream_t, NULL = default stream) and

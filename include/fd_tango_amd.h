@@ -88,14 +88,14 @@ fd_dcache_compact_next( ulong chunk, ulong sz, ulong chunk0, ulong wmark ) {
 
 /* diagnostics (fd_frank.h:23-28 names, plus engine-side counts) */
 typedef struct {
-  ulong in_cnt;        /* input frags consumed */
+  ulong in_cnt;        /* input frags read (staged, filtered or rejected) */
   ulong ha_filt_cnt;   /* dropped as HA duplicates before verify */
   ulong ha_filt_sz;
   ulong sv_filt_cnt;   /* dropped by signature verification */
   ulong sv_filt_sz;
   ulong out_cnt;       /* frags published */
   ulong out_sz;
-  ulong ovrn_cnt;      /* input frags lost to producer overrun */
+  ulong ovrn_cnt;      /* input frags lost to producer overrun (skipped, or lapped before the tile was done) */
   ulong backp_cnt;     /* times the output was backpressured */
   ulong batch_cnt;     /* GPU batches launched */
   ulong batch_sig_cnt; /* signatures in those batches */
@@ -111,12 +111,34 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    batches grow toward batch_max).  batch_wait_ns != 0 replaces "drained"
    by "the oldest staged frag waited batch_wait_ns" while another batch is
    in flight (fewer, larger batches).  tcache_depth: HA dedup window (tags
-   remembered, 0 disables).  NULL on failure. */
+   remembered, 0 disables).
+
+   Output data region.  Like the reference verify tile, which publishes
+   frags out of a dcache it owns (fd_frank_verify_synth_load.c:324,409-411),
+   the tile owns its output dcache: out_frame_cnt frames of
+   FD_VERIFY_AMD_FRAME_SZ bytes (0: out_depth_hint + 5*batch_max, the
+   fd_dcache_req_data_sz rule with burst = the frags the tile holds staged
+   or in flight; out_depth_hint = 4096).  Every published frag's chunk is
+   relative to fd_verify_amd_tile_out_chunk0 and its bytes are the bytes
+   that were verified.  A frame is reused only once the consumer's out_fseq
+   has passed the frag it last carried (backpressure otherwise), so the
+   output never changes under a consumer that honours flow control.
+   NULL on failure. */
+#define FD_VERIFY_AMD_FRAME_SZ (1408UL)   /* 22 chunks >= 96 + FD_ED25519_AMD_MSG_MAX */
+
 fd_verify_amd_tile_t *
-fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong tcache_depth );
+fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong tcache_depth, ulong out_frame_cnt );
 
 void
 fd_verify_amd_tile_delete( fd_verify_amd_tile_t * tile );
+
+/* Local address of chunk 0 of the tile's output data region (published
+   chunk c lives at fd_chunk_to_laddr( out_chunk0, c )), and its size. */
+void *
+fd_verify_amd_tile_out_chunk0( fd_verify_amd_tile_t * tile );
+
+ulong
+fd_verify_amd_tile_out_data_sz( fd_verify_amd_tile_t * tile );
 
 /* Frag framing.  PUB_SIG_MSG (default): public_key(32) | signature(64) |
    message, one signature per frag (fd_frank_verify_synth_load.c:340-347).
@@ -125,36 +147,51 @@ fd_verify_amd_tile_delete( fd_verify_amd_tile_t * tile );
    against its account address (multi-signer) and publishes the transaction
    iff it parses and all its signatures pass; HA dedup uses its first
    signature, the published tag is that signature's SHA-512 tag.  A frag
-   that fails to parse counts as SV_FILT. */
-/* Zero-copy staging: map the host data region [base, base+sz) holding
-   the input frags into the GPU (hipHostRegister).  When a run's in_chunk0
-   lies inside it, the tile hands the GPU only (chunk, size) per frag (no
-   host memcpy): PUB_SIG_MSG frags are gathered by a kernel that reads the
-   96 header bytes, and k_prep reads the message over PCIe in place; TXN
-   frags are parsed and hashed in place. */
-int
-fd_verify_amd_tile_register_dcache( fd_verify_amd_tile_t * tile, void * base, ulong sz );
-
+   that fails to parse counts as SV_FILT.  TXN needs batch_max >= 19 (the
+   most signatures a 1232-B transaction can carry), else ERR_INVAL. */
 #define FD_VERIFY_AMD_FRAMING_PUB_SIG_MSG (0)
 #define FD_VERIFY_AMD_FRAMING_TXN         (1)
 int
 fd_verify_amd_tile_set_framing( fd_verify_amd_tile_t * tile, int framing );
 
-/* Run the tile until `frag_cnt` input frags were consumed (0: until
-   *stop != 0) and every accepted frag is published.  Input: in_mcache
-   (depth in_depth, power of 2), in_chunk0 = local address of chunk 0 of
-   the data region (fd_chunk_to_laddr), first sequence number in_seq0.
-   Output: out_mcache (depth out_depth), first sequence out_seq0; out_fseq
-   (NULL = no flow control) is the slowest consumer's next expected
-   sequence number.  Latency samples (tspub - tsorig, in the caller's
-   timestamp units) of up to lat_max published frags go to lat (NULL to
-   skip).  Returns FD_ED25519_AMD_OK or a negative FD_ED25519_AMD_ERR_*. */
+/* Input staging.
+   Copy mode (default): the tile copies each input frag into its own output
+   frame, re-checks the frag's mcache line afterwards (a frag lapped during
+   the copy is counted as overrun and dropped), and releases the frag to
+   the producer right away (in_fseq advances at staging).  The GPU reads the
+   frames from the mapped output region.
+   Zero-copy mode: fd_verify_amd_tile_register_dcache maps the host data
+   region [base, base+sz) holding the input frags into the GPU
+   (hipHostRegister).  When a run's in_chunk0 lies inside it, the tile hands
+   the GPU only (chunk, size) per frag; the GPU copies each frag from the
+   input region into the device and into the tile's output frame.  The
+   input frags of a batch are released (in_fseq) only when that batch has
+   retired, and a frag whose mcache line was lapped by then is dropped as
+   overrun instead of published. */
+int
+fd_verify_amd_tile_register_dcache( fd_verify_amd_tile_t * tile, void * base, ulong sz );
+
+/* Run the tile until `frag_cnt` input sequence numbers were consumed (0:
+   until *stop != 0) and every accepted frag is published.  Input:
+   in_mcache (depth in_depth, power of 2), in_chunk0 = local address of
+   chunk 0 of the input data region (fd_chunk_to_laddr), first sequence
+   number in_seq0.  in_fseq (NULL = none) receives the tile's flow-control
+   sequence for the producer (the reference's fseq, fd_fseq_update): every
+   input frag below it is no longer read by the tile, so the producer may
+   reuse its mcache line and its data.  Output: out_mcache (depth
+   out_depth), first sequence out_seq0, frags in the tile's output data
+   region; out_fseq (NULL = no flow control) is the slowest consumer's next
+   expected sequence number.  Latency samples (tspub - tsorig, in the
+   caller's timestamp units) of up to lat_max published frags go to lat
+   (NULL to skip).  Returns FD_ED25519_AMD_OK or a negative
+   FD_ED25519_AMD_ERR_*. */
 int
 fd_verify_amd_tile_run( fd_verify_amd_tile_t *  tile,
                         fd_frag_meta_t const *  in_mcache,
                         ulong                   in_depth,
                         void const *            in_chunk0,
                         ulong                   in_seq0,
+                        ulong *                 in_fseq,
                         fd_frag_meta_t *        out_mcache,
                         ulong                   out_depth,
                         ulong                   out_seq0,
@@ -173,29 +210,58 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t *  tile,
 uint
 fd_verify_amd_tickcount( void );
 
-/* Streaming benchmark (config 5): a producer thread publishes frags
-   public_key | signature | message cyclically from the given pool (SoA
-   layout of fd_ed25519_amd_verify_soa) into a private mcache/dcache --
-   at `rate` frags/s (open loop; tsorig = scheduled send time) or, with
-   rate 0, as fast as the tile accepts (credit-based flow control) -- the
-   tile runs on `device` with 4 batches in flight (zero_copy: the data
-   region is mapped into the GPU, fd_verify_amd_tile_register_dcache), and
-   a consumer drains the output.  Runs until frag_cnt frags were published.  out[0] = frags/s through the tile,
-   out[1..3] = p50 / p99 / p999 latency in ns (producer publish -> tile
-   publish), out[4] = mean GPU batch size, out[5] = frags published,
-   out[6] = frags dropped by verification.  Returns 0 or an error code. */
+/* Streaming benchmark and end-to-end check (config 5): a producer thread
+   publishes frags public_key | signature | message cyclically from the
+   given pool (SoA layout of fd_ed25519_amd_verify_soa; frag s carries pool
+   entry s % pool_n) into a private mcache/dcache -- at `rate` frags/s (open
+   loop; tsorig = scheduled send time) or, with rate 0, as fast as the tile
+   accepts (credit-based flow control on the tile's in_fseq) -- the tile
+   runs on `device` with 4 batches in flight, and a consumer drains the
+   output.  Runs until frag_cnt input frags were consumed.
+
+   flags: FD_VERIFY_AMD_BENCH_ZERO_COPY maps the input data region into the
+   GPU (fd_verify_amd_tile_register_dcache).  FD_VERIFY_AMD_BENCH_WRITE:
+   the producer writes every frame into a wrapping data region of
+   dcache_frames MTU frames (0: in_depth + 64) before publishing it, as a
+   NIC would (otherwise every pool frame is pre-placed once and only
+   metadata is published).  FD_VERIFY_AMD_BENCH_LAP: the producer ignores
+   the tile's credit (only with WRITE; overrun test).
+
+   expect_err / expect_tag (pool_n each, NULL = no check): the consumer
+   checks every published frag against them -- the frag's verdict must be
+   0, its tag (meta sig) must equal expect_tag, its bytes in the tile's
+   output region must equal the pool frame, and publication must follow
+   input order; in check mode tsorig = the input sequence number (not a
+   time), so latency is not measured.  The producer input sequence is
+   deterministic, so with no overrun the published set is exactly the pool
+   entries with expect_err == 0 in input order.
+
+   out[0] = frags/s through the tile, out[1..3] = p50 / p99 / p999 latency
+   in ns (producer publish -> tile publish), out[4] = mean GPU batch size,
+   out[5] = frags published, out[6] = frags dropped by verification
+   (SV_FILT), out[7] = overrun frags, out[8] = check mismatches (published
+   frags that fail a check, plus frags that should have been published and
+   were not, overrun ones excepted), out[9] = frags checked.  Returns 0 or
+   an error code. */
+#define FD_VERIFY_AMD_BENCH_ZERO_COPY (1)
+#define FD_VERIFY_AMD_BENCH_WRITE     (2)
+#define FD_VERIFY_AMD_BENCH_LAP       (4)
+
 int
 fd_verify_amd_bench_stream( int           device,
                             ulong         batch_max,
                             ulong         batch_wait_ns,
                             double        rate,
-                            int           zero_copy,
+                            int           flags,
+                            ulong         dcache_frames,
                             ulong         pool_n,
                             uchar const * pub,
                             uchar const * sig,
                             uint const *  msg_off,
                             uint const *  msg_sz,
                             uchar const * blob,
+                            schar const * expect_err,
+                            ulong const * expect_tag,
                             ulong         frag_cnt,
                             double *      out );
 

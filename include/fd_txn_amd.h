@@ -130,11 +130,13 @@ fd_txn_amd_parse_dev( ulong         txn_cnt,
    transaction.  txn_err[t] in {0, -1, -2, -3, FD_TXN_AMD_ERR_PARSE}.
    Optional outputs (NULL to skip): sig_base[t] = index of transaction t's
    first signature in sig_err (sig_base[txn_cnt] = total signatures) and
-   sig_err[...] = per-signature fd_ed25519_verify codes (capacity:
-   payload_sz/96 + 1 entries always suffices).  Every payload must be at
-   most FD_TXN_AMD_MTU bytes (the wire limit; FD_ED25519_AMD_ERR_INVAL
-   otherwise).  Returns FD_ED25519_AMD_OK or a negative
-   FD_ED25519_AMD_ERR_*. */
+   sig_err[...] = per-signature fd_ed25519_verify codes (capacity: the
+   total that fd_ed25519_amd_txn_slots returns for the same batch).  Every
+   payload must be at most FD_TXN_AMD_MTU bytes (the wire limit), fit the
+   engine's blob_max, and reserve at most batch_max signature slots
+   (FD_ED25519_AMD_ERR_INVAL otherwise, checked before anything is
+   launched; batch_max >= 19 admits every payload).  Returns
+   FD_ED25519_AMD_OK or a negative FD_ED25519_AMD_ERR_*. */
 #define FD_TXN_AMD_MTU (1232UL)
 int
 fd_ed25519_amd_verify_txns( fd_ed25519_amd_t * eng,
@@ -146,6 +148,21 @@ fd_ed25519_amd_verify_txns( fd_ed25519_amd_t * eng,
                             schar *            txn_err,
                             uint *             sig_base,
                             schar *            sig_err );
+
+/* Multi-device form (fd_ed25519_amd_multi_new): the transactions are split
+   into contiguous shards, one per device, verified concurrently, each by
+   its own engine and host thread; outputs as fd_ed25519_amd_verify_txns,
+   sig_base numbered over the whole batch. */
+int
+fd_ed25519_amd_multi_verify_txns( fd_ed25519_amd_multi_t * multi,
+                                  ulong                    txn_cnt,
+                                  uchar const *            payload,
+                                  uint const *             txn_off,
+                                  uint const *             txn_sz,
+                                  ulong                    payload_sz,
+                                  schar *                  txn_err,
+                                  uint *                   sig_base,
+                                  schar *                  sig_err );
 
 /* Device-resident form (inputs already in HBM, caller's stream, no sync).
    Signature slots follow the same rule as fd_ed25519_amd_verify_txns:

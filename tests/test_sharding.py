@@ -25,6 +25,24 @@ def test_shard_range_partition():
             assert max(sizes) - min(sizes) <= 1
 
 
+def test_shard_range_matches_native():
+    """The Python split (bench ranks) and fd_ed25519_amd_shard_range (the
+    native multi-device engine) give the same shards."""
+    from firedancer_amd import ed25519
+    for n in (0, 1, 7, 1000, (1 << 24) + 5):
+        for world in (1, 2, 3, 8):
+            for r in range(world):
+                assert ed25519.shard_range(n, world, r) == shard_range(n, r, world)
+
+
+def test_multi_engine_refuses_without_device():
+    from firedancer_amd import ed25519, hip
+    if hip.device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(ed25519.EngineError):
+        ed25519.MultiEngine([0, 0])
+
+
 def test_slice_soa_rebases_messages(golden):
     lo, hi = 100, 180
     pub, sig, off, sz, blob = _slice_soa(golden.pub, golden.sig, golden.msg_off, golden.msg_sz, golden.blob, lo, hi)

@@ -1,10 +1,15 @@
 """Streaming verify tile (include/fd_tango_amd.h) on the GPU: frags
 public_key | signature | message from an input mcache/dcache, HA dedup,
 adaptive GPU batches, in-order publication of the passing frags with the
-SHA-512-derived dedup tag.  Expected behaviour is modelled frag by frag in
-Python: tcache window semantics of FD_TCACHE_INSERT
-(src/tango/tcache/fd_tcache.h:372-403), verdicts from the committed golden
-fixtures / the CPU oracle, tag = first 8 bytes of SHA-512(R||A||M)."""
+SHA-512-derived dedup tag, out of the tile's own output dcache.  Expected
+behaviour is modelled frag by frag in Python: tcache window semantics of
+FD_TCACHE_INSERT (src/tango/tcache/fd_tcache.h:372-403), verdicts from the
+committed golden fixtures / the CPU oracle, tag = first 8 bytes of
+SHA-512(R||A||M).  The producer-facing contract (a frag is released by
+in_fseq only once the tile no longer reads it; a frag lapped before the
+tile is done is dropped, never published) is checked with producers that
+rewrite a small wrapping data region, with and without honouring the
+credit (fd_verify_amd_bench_stream check mode)."""
 import collections
 import hashlib
 
@@ -78,22 +83,25 @@ def test_tile_publishes_passing_frags_in_order(golden, batch_max, tc_depth, zero
     mc_out = tango.mcache_new(2048)
     tile = tango.VerifyTile(0, batch_max=batch_max, tcache_depth=tc_depth)
     if zero_copy:
-        tile.register_dcache(dc)        # frags gathered on the GPU from the mapped data region
+        tile.register_dcache(dc)        # frags copied on the GPU from the mapped data region
     try:
         diag, lat = tile.run(mc_in, dc, 0, mc_out, 0, n, lat_max=n)
+        exp, ha, sv = _model(pub, sig, msgs, order, verdict, tc_depth)
+        assert diag["in_cnt"] == n and diag["ha_filt_cnt"] == ha and diag["sv_filt_cnt"] == sv
+        assert diag["out_cnt"] == len(exp) and diag["ovrn_cnt"] == 0 and diag["bad_frag_cnt"] == 0
+        assert tile.in_fseq == n                      # every input frag released
+        for o, (seq_in, tag) in enumerate(exp):
+            line = mc_out[o]
+            k = order[seq_in]
+            assert int(line["seq"]) == o
+            assert int(line["sig"]) == tag
+            assert (int(line["sz"]), int(line["ctl"]), int(line["tsorig"])) == (sizes[seq_in], 3, ts[seq_in])
+            # published out of the tile's own dcache: the verified bytes
+            assert tile.out_frame(line["chunk"], line["sz"]) == bytes(pub[k]) + bytes(sig[k]) + msgs[k]
+        assert diag["batch_cnt"] >= 1 and diag["batch_sig_cnt"] == n - ha
+        assert lat.size == len(exp)
     finally:
         tile.close()
-    exp, ha, sv = _model(pub, sig, msgs, order, verdict, tc_depth)
-    assert diag["in_cnt"] == n and diag["ha_filt_cnt"] == ha and diag["sv_filt_cnt"] == sv
-    assert diag["out_cnt"] == len(exp) and diag["ovrn_cnt"] == 0 and diag["bad_frag_cnt"] == 0
-    for o, (seq_in, tag) in enumerate(exp):
-        line = mc_out[o]
-        assert int(line["seq"]) == o
-        assert int(line["sig"]) == tag
-        assert (int(line["chunk"]), int(line["sz"]), int(line["ctl"]), int(line["tsorig"])) == \
-            (chunks[seq_in], sizes[seq_in], 3, ts[seq_in])
-    assert diag["batch_cnt"] >= 1 and diag["batch_sig_cnt"] == n - ha
-    assert lat.size == len(exp)
 
 
 def test_tile_fresh_signatures_vs_oracle():
@@ -140,6 +148,73 @@ def test_stream_bench_smoke():
     assert r["published"] == 20000 and r["sv_filt"] == 0
 
 
+def _stream_pool(seed, count, szhi=1232):
+    """Fresh signatures, 10 % of them corrupted (bit flips in sig, msg or
+    pub), with the oracle's verdicts and the expected dedup tags."""
+    from firedancer_amd import ed25519
+    prv, blob, off, sz, fk, fp = _oracle.stream_inputs(seed, count, 0, szhi, True)
+    pub, sig = ed25519.sign_batch_gpu(prv, blob, off, sz)
+    for i in np.nonzero(fk)[0]:
+        byte, bit = divmod(int(fp[i]), 8)
+        tgt = sig[i] if fk[i] == 1 else (blob[off[i]:] if fk[i] == 2 else pub[i])
+        tgt[byte] ^= 1 << bit
+    err = _oracle.verify_batch(_golden.Batch(pub, sig, off, sz, blob))
+    tag = np.array([int.from_bytes(hashlib.sha512(bytes(sig[i][:32]) + bytes(pub[i]) +
+                                                  bytes(blob[off[i]:off[i] + sz[i]])).digest()[:8], "little")
+                    for i in range(count)], np.uint64)
+    assert 0.05 < (err != 0).mean() < 0.15
+    return pub, sig, off, sz, blob, err, tag
+
+
+@pytest.mark.parametrize("zero_copy", [False, True])
+def test_tile_producer_rewrites_wrapping_dcache(zero_copy):
+    """A producer that writes every frame into a small wrapping data region
+    (in_depth + 64 frames) as fast as the tile's in_fseq credit allows,
+    with 4 batches of 256 in flight: every published frag's verdict, tag,
+    bytes (in the tile's output dcache) and order equal the oracle's, none
+    is missing, none overran."""
+    from firedancer_amd import tango
+    pub, sig, off, sz, blob, err, tag = _stream_pool(777 + zero_copy, 3000)
+    nf = 60000
+    r = tango.bench_stream(0, 256, 0, pub, sig, off, sz, blob, nf, zero_copy=zero_copy, writes=True,
+                           expect_err=err, expect_tag=tag)
+    want = int((err[np.arange(nf) % err.size] == 0).sum())
+    assert r["mismatches"] == 0 and r["ovrn"] == 0
+    assert r["checked"] == r["published"] == want and r["sv_filt"] == nf - want
+
+
+@pytest.mark.parametrize("zero_copy", [False, True])
+def test_tile_lapping_producer_never_publishes_rewritten_frags(zero_copy):
+    """A producer that ignores the tile's credit and laps it: frags it
+    rewrote before the tile was done are dropped as overrun; every frag
+    that is published still carries exactly the bytes that were verified,
+    with the oracle's verdict and tag, in input order."""
+    from firedancer_amd import tango
+    pub, sig, off, sz, blob, err, tag = _stream_pool(999 + zero_copy, 2000, 400)
+    r = tango.bench_stream(0, 1024, 0, pub, sig, off, sz, blob, 400000, zero_copy=zero_copy, writes=True, lap=True,
+                           expect_err=err, expect_tag=tag)
+    assert r["mismatches"] == 0 and r["checked"] == r["published"] > 0
+    assert r["published"] + r["sv_filt"] + r["ovrn"] <= 400000
+
+
+@pytest.mark.parametrize("batch_max", [4096, 16384])
+@pytest.mark.parametrize("zero_copy", [False, True])
+def test_tile_large_batches_vs_oracle(batch_max, zero_copy):
+    """Config 5 at its large batch caps: saturated stream of fresh
+    signatures with 10 % corrupted frags through 4 in-flight batches of up
+    to batch_max; the published stream equals the oracle's accepted set, in
+    order, with the right tags and bytes."""
+    from firedancer_amd import tango
+    pub, sig, off, sz, blob, err, tag = _stream_pool(4096 + batch_max + zero_copy, 8192, 400)
+    nf = 8 * batch_max + 12345
+    r = tango.bench_stream(0, batch_max, 0, pub, sig, off, sz, blob, nf, zero_copy=zero_copy, expect_err=err,
+                           expect_tag=tag)
+    want = int((err[np.arange(nf) % err.size] == 0).sum())
+    assert r["mismatches"] == 0 and r["ovrn"] == 0
+    assert r["checked"] == r["published"] == want and r["sv_filt"] == nf - want
+    assert r["mean_batch"] > batch_max / 8
+
+
 @pytest.mark.parametrize("zero_copy", [False, True])
 def test_tile_txn_framing_vs_oracle(zero_copy):
     """Frags carrying wire transactions (multi-signer, legacy + v0, some
@@ -175,9 +250,10 @@ def test_tile_txn_framing_vs_oracle(zero_copy):
     eterr, _, _ = _oracle.txn_verify_batch(blob, off, sz)
     tile = tango.VerifyTile(0, batch_max=64, tcache_depth=4096, framing=tango.VerifyTile.FRAMING_TXN)
     if zero_copy:
-        tile.register_dcache(dcache)    # transactions parsed in place from the mapped data region
+        tile.register_dcache(dcache)    # transactions copied on the GPU from the mapped data region
     try:
         diag, _ = tile.run(mc_in, dcache, 0, mc_out, 0, len(order))
+        frames = [tile.out_frame(mc_out[o]["chunk"], mc_out[o]["sz"]) for o in range(int(diag["out_cnt"]))]
     finally:
         tile.close()
     seen, exp = set(), []
@@ -199,5 +275,15 @@ def test_tile_txn_framing_vs_oracle(zero_copy):
         exp.append((seq, int.from_bytes(h[:8], "little")))
     assert diag["ha_filt_cnt"] == ha == 3 and diag["sv_filt_cnt"] == sv and diag["out_cnt"] == len(exp)
     for o, (seq_in, tag) in enumerate(exp):
-        assert int(mc_out[o]["chunk"]) == chunks[seq_in] and int(mc_out[o]["tsorig"]) == seq_in
+        assert frames[o] == pays[order[seq_in]] and int(mc_out[o]["tsorig"]) == seq_in
         assert int(mc_out[o]["sig"]) == tag
+
+
+def test_tile_txn_framing_needs_room_for_a_full_transaction():
+    """TXN framing with batch_max < 19 could never stage a 19-signer
+    transaction: refused up front instead of spinning."""
+    from firedancer_amd import ed25519, tango
+    with pytest.raises(ed25519.EngineError):
+        tango.VerifyTile(0, batch_max=8, framing=tango.VerifyTile.FRAMING_TXN)
+    t = tango.VerifyTile(0, batch_max=19, framing=tango.VerifyTile.FRAMING_TXN)
+    t.close()

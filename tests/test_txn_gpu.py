@@ -167,20 +167,20 @@ def test_synth_txn_workload_and_device_path(engine):
 
 
 def test_config4_shard_full_size_properties():
-    """configs[3] at the size of one GPU's shard of 2^24 signatures over 4
-    GPUs: 2^22 signatures in multi-signer transactions (64..1232-B
+    """configs[3] at the size of one GPU's shard of 2^24 signatures over 2
+    GPUs: 2^23 signatures in multi-signer transactions (64..1232-B
     messages).  Every signature is valid: each rejected transaction must
     hold a limb-compare false reject, confirmed by the oracle."""
     from firedancer_amd import hip, workload
-    payload, toff, tsz, tbase = workload.txn_batch(1 << 22, 424242)
+    payload, toff, tsz, tbase = workload.txn_batch(1 << 23, 424242)
     dev = workload.TxnDevice(payload, toff, tsz, tbase)
     st = hip.Stream()
     dev.run(st.handle)
     st.synchronize()
     terr, serr = dev.verdicts()
-    assert dev.slot_cnt >= (1 << 22) * 0.99
+    assert dev.slot_cnt >= (1 << 23) * 0.99
     bad = np.nonzero(terr)[0]
-    assert bad.size <= 20, bad.size
+    assert bad.size <= 40, bad.size
     if bad.size:
         eterr, _, _ = _oracle.txn_verify_batch(payload, toff[bad], tsz[bad])
         assert np.array_equal(eterr, terr[bad]) and (eterr == -3).all()
