@@ -2,53 +2,69 @@
 """bench.py -- ed25519 verifies/sec on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n SIGS] [--msg-sz B]
+    python bench.py --workload txn [--total-sigs 16777216]
 
-A "step" is one pass of the verify pipeline (k_prep -> k_decomp -> k_dsm)
-over one batch of n synthetic signatures (BASELINE.json configs[1]:
-2^20 single-signer signatures, 200-byte Solana-txn-sized messages, fresh
-random keypairs), with the inputs already resident in HBM when the timed
-region starts.  For N > 1 (launched by torch.distributed.run) every rank
-verifies its own shard of n signatures on its own GPU -- signatures are
-independent, so there is no data-path collective (weak scaling); gloo is
-used only for the start/stop barriers and the max-over-ranks of the time.
+Default (configs[1]): a "step" is one pass of the verify pipeline (k_prep ->
+k_decomp -> k_dsm) over one batch of n synthetic signatures (2^20
+single-signer signatures, 200-byte Solana-txn-sized messages, fresh random
+keypairs), with the inputs already resident in HBM when the timed region
+starts.  For N > 1 (launched by torch.distributed.run) every rank verifies
+its own batch of n signatures on its own GPU -- signatures are independent,
+so there is no data-path collective (weak scaling); gloo is used only for
+the start/stop barriers and the max-over-ranks of the time.
+
+--workload txn (configs[3]): 2^24 signatures in multi-signer transactions
+(1..12 signers, 64..1232-B messages, legacy + v0), split across the ranks
+by contiguous shards (strong scaling: the total is fixed); a step parses,
+verifies and reduces every transaction of the rank's shard on its GPU.
 
 Rank 0 prints ONE JSON line: value = signatures verified by all ranks / max
 elapsed, plus "roofline" (k_dsm vs the measured integer-multiply issue
 peak), "cpu_baseline" (the reference's own fd_ed25519_verify compiled from
-its sources, oracle/_ref, timed on this host on a bounded sample of the same
-workload) and the end-to-end p50/p99 latency of a 4096-signature host batch.
+its sources, oracle/_ref, timed on every host core of this box on a
+bounded sample of the same workload), the end-to-end p50/p99 latency of a
+4096-signature host batch, the drop-in single-call latency, the
+PCIe-inclusive host paths and the streaming tile sweep (config 5).
 """
 import argparse
+import hashlib
 import json
+import math
 import os
 import sys
 import time
 
 import numpy as np
 
-# The streaming tile keeps 4 GPU batches in flight on 4 HIP streams; with
-# HIP's default of 4 hardware queues per process only 2 of them run
-# concurrently (measured in round 1 with a concurrency probe), so give the process 8
-# (read at HIP runtime init, before any device call; well under the pool's
-# limit of 32).
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# The streaming tile keeps 4 GPU batches in flight on 4 HIP streams, and
+# only streams on distinct hardware queues run concurrently.  HIP maps
+# streams onto at most GPU_MAX_HW_QUEUES queues per process; with the
+# default 4, or with 8 once the bench's earlier engines have created and
+# destroyed their streams, the tile's 4 streams landed on 2 queues (kernel
+# trace: Queue_Id 3/4 only; 0.92 M frags/s at batch 256 vs 1.63 M with 16,
+# profiles/r02_tile_queues.txt).  16 (read at HIP runtime init, before any
+# device call) keeps them apart; the pool's limit is 32.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+METRIC = "ed25519 verifies/sec (node, 1/2/4/8 GPUs); p50 latency @4096-sig batch"
+DTYPE = "int32x32->int64 (field limbs), u64 (SHA-512)"
 # k_dsm algorithmic work (SURVEY.md App. C): one field mul = 109 signed
 # 32x32->64 multiply-accumulates (100 products + 9 x19 pre-multiplies), one
 # square = 60.  Per signature, over the ref10 op flow's useful lanes:
 #   N_sq  = 4 (2A) + 4 I                      (I = loop iterations)
 #   N_mul = 68 (Ai table) + 3 I + 8 n_h + 7 n_s + 2 (final compare)
 MAC_MUL, MAC_SQ = 109, 60
-# Decompression (k_decomp), per point: 255 squares + ~19.5 muls.
-DECOMP_MAC_PER_SIG = 2 * (255 * MAC_SQ + 19.5 * MAC_MUL)
 # Peak: gfx950 issues v_mad_i64_i32 at half rate = 64 lane-ops/clk/CU
 # (tools/ubench_valu: 55.3/clk/CU sustained with 16 chains), 256 CUs,
 # 2.4 GHz max clock (MI355X_MICROARCH.md chip table).
 PEAK_TMAC = 64 * 256 * 2.4e9 / 1e12
+# the reference's single-thread fd_ed25519_verify at 200-B messages on the
+# build container (SURVEY.md s8 a1)
+REF_US_PER_CALL_SURVEY = 53.0
 
 
 def parse():
@@ -58,10 +74,12 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sigs", "--n", dest="n", type=int, default=1 << 20, help="signatures per GPU per step")
     ap.add_argument("--msg-sz", type=int, default=200)
+    ap.add_argument("--total-sigs", type=int, default=1 << 24,
+                    help="txn workload: signatures over all ranks (strong scaling)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="repeat passes over the CPU sample until this much wall time is spent")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every core this process may use")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-stream", action="store_true", help="skip the streaming-tile sweep (config 5)")
@@ -69,6 +87,120 @@ def parse():
                     help="sigs: configs[1] (default bench line); txn: configs[3] multi-signer transactions")
     ap.add_argument("--stream-frags", type=int, default=1 << 20, help="frags per streaming-tile run")
     return ap.parse_args()
+
+
+# ---------------------------------------------------------------- host facts
+
+def host_cores():
+    """Cores this process may use: the affinity set, capped by a cgroup CPU
+    quota and by the host share the pool grants a one-GPU box
+    (OMP_NUM_THREADS, set to it there) -- the machine itself may show many
+    more CPUs than the box owns."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(math.ceil(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    share = None
+    try:
+        share = int(os.environ["OMP_NUM_THREADS"])
+    except (KeyError, ValueError):
+        pass
+    cap = min(x for x in (aff, quota, share) if x)
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return cap, aff, {"cgroup_quota": quota, "omp_num_threads": share, "machine_cpus": os.cpu_count()}, model
+
+
+def ref_batch_lib():
+    """The reference's own verify (oracle/_ref, compiled from its sources in
+    the build container).  The CPU baseline is the reference itself: no
+    silent fallback to the port."""
+    import ctypes
+    path = os.path.join(ROOT, "oracle", "_ref", "libfdref_batch.so")
+    if not os.path.exists(path):
+        raise SystemExit("bench.py: %s missing -- build it with __graft_entry__.build() in a container that has "
+                         "/root/reference (or pass --no-cpu)" % path)
+    L = ctypes.CDLL(path)
+    vp = ctypes.c_void_p
+    L.ref_ed25519_verify_batch.argtypes = [ctypes.c_uint64, vp, vp, vp, vp, vp, vp, ctypes.c_int]
+    L.ref_txn_verify_batch.argtypes = [ctypes.c_uint64, vp, vp, vp, vp, ctypes.c_int]
+    return L
+
+
+def _vp(a):
+    import ctypes
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def timed_passes(call, seconds):
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        call()
+        passes += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            return passes, dt
+
+
+def cpu_baseline(pub, sig, off, sz, blob, sample, threads, gpu_err, seconds):
+    """The reference's fd_ed25519_verify (oracle/_ref) on every host core,
+    then on one core.  Bounded sample: passes over the first `sample`
+    signatures of the bench batch until `seconds` of wall time are spent."""
+    L = ref_batch_lib()
+    cores, aff, quota, model = host_cores()
+    nt = threads or cores
+    n = min(sample, pub.shape[0])
+    err = np.zeros(n, np.int8)
+    args = [n, _vp(pub), _vp(sig), _vp(off), _vp(sz), _vp(blob), _vp(err)]
+    passes, dt = timed_passes(lambda: L.ref_ed25519_verify_batch(*args, nt), seconds)
+    n1 = min(n, 1 << 15)
+    args1 = [n1] + args[1:]
+    p1, dt1 = timed_passes(lambda: L.ref_ed25519_verify_batch(*args1, 1), min(3.0, seconds))
+    per_core = p1 * n1 / dt1
+    return {"value": passes * n / dt, "unit": "verifies/s", "cores": nt, "kind": "reference",
+            "sample": "%d passes over %d of the bench batch's %d-B signatures on %d threads, %.1f s wall; "
+                      "single-thread: %d passes over %d" % (passes, n, int(sz[0]), nt, dt, p1, n1),
+            "per_core_verifies_per_s": per_core, "us_per_call_1_thread": 1e6 / per_core,
+            "host": {"cpu_model": model, "usable_cores": cores, "affinity_cpus": aff, "limits": quota},
+            "verdicts_equal_gpu": bool(np.array_equal(err, gpu_err[:n]))}
+
+
+# ---------------------------------------------------------------- workloads
+
+def make_workload(n, msg_sz, seed):
+    """configs[1]: n fresh keypairs, random msg_sz-byte messages, signed on
+    the GPU (k_sign, byte-identical to the host / reference signer)."""
+    from firedancer_amd import workload
+    return workload.sig_batch(n, msg_sz, seed)
+
+
+def dsm_roofline(st, kernel_ms, n, kernel="k_dsm", note=None):
+    """Algorithmic k_dsm multiply-accumulates (from the kernel's own work
+    statistics) per launch / kernel time, against the integer-multiply peak."""
+    st = st.astype(np.float64)
+    I, nh, ns = st[0].sum(), st[1].sum(), st[2].sum()
+    live = float((st[0] > 0).sum())
+    mac = MAC_MUL * (68 * live + 3 * I + 8 * nh + 7 * ns + 2 * live) + MAC_SQ * (4 * live + 4 * I)
+    achieved = mac / (kernel_ms * 1e-3) / 1e12
+    r = {"bound": "valu-imad64", "kernel": kernel, "achieved": achieved, "peak": PEAK_TMAC, "unit": "TMAC/s",
+         "frac": achieved / PEAK_TMAC, "traffic": pmc_traffic("k_dsm", n),
+         "traffic_note": "HBM bytes per launch from the committed PMC pass (profiles/r01_pmc_latest.json: "
+                         "2*FETCH_SIZE+WRITE_SIZE KB, gfx950 correction), scaled to this batch",
+         "mac_per_sig": mac / max(live, 1.0)}
+    if note:
+        r["note"] = note
+    return r
 
 
 def pmc_traffic(kernel, n):
@@ -84,21 +216,27 @@ def pmc_traffic(kernel, n):
         return None
 
 
-def make_workload(n, msg_sz, seed):
-    """configs[1]: n fresh keypairs, random msg_sz-byte messages, signed on
-    the GPU (k_sign, byte-identical to the host / reference signer)."""
-    from firedancer_amd import workload
-    return workload.sig_batch(n, msg_sz, seed)
+def gather_sum(dist, values):
+    if not dist:
+        return values
+    import torch
+    t = torch.tensor(values, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.tolist()
 
 
-def run_txn(args, rank, world, local, dist):
+# ---------------------------------------------------------------- configs[3]
+
+def run_txn(args, rank, world, dist):
     """configs[3]: GPU-signed multi-signer transactions (1..12 signers,
-    64..1232-B messages, legacy + v0), device resident, parsed + verified +
-    reduced per transaction on the GPU; weak scaling (each rank its own
-    shard of args.n signatures)."""
-    from firedancer_amd import hip, workload
+    64..1232-B messages, legacy + v0), device resident; args.total_sigs
+    signatures split across the ranks (strong scaling), each rank parsing,
+    verifying and reducing its shard on its GPU."""
+    from firedancer_amd import ed25519, hip, workload
+    from firedancer_amd.shard import max_over_ranks, shard_range
+    lo, hi = shard_range(args.total_sigs, rank, world)
     t0 = time.perf_counter()
-    payload, toff, tsz, tbase = workload.txn_batch(args.n, 5000 + rank)
+    payload, toff, tsz, tbase = workload.txn_batch(hi - lo, 5000 + rank)
     gen_s = time.perf_counter() - t0
     dev = workload.TxnDevice(payload, toff, tsz, tbase)
     stream = hip.Stream()
@@ -117,66 +255,119 @@ def run_txn(args, rank, world, local, dist):
     stream.synchronize()
     elapsed = time.perf_counter() - t0
     gpu_ms = e0.elapsed_ms(e1) / args.steps
-    if dist:
-        from firedancer_amd.shard import max_over_ranks
-        elapsed = max_over_ranks(elapsed)
-        dist.barrier()
+    elapsed = max_over_ranks(elapsed)
     terr, _ = dev.verdicts()
+    d_stats = hip.DeviceBuffer(4 * 3 * max(dev.slot_cnt, 1))
+    ed25519.work_stats_dev(dev.slot_cnt, dev.d_ws.ptr, d_stats.ptr, stream.handle)
+    stream.synchronize()
+    st = d_stats.to_array(np.uint32, 3 * dev.slot_cnt).reshape(3, dev.slot_cnt)
+    rej = np.nonzero(terr)[0]
+    slots, txns, nrej = gather_sum(dist, [float(dev.slot_cnt), float(dev.txn_cnt), float(rej.size)])
+    if dist:
+        dist.barrier()
     if rank != 0:
         return
-    slots = dev.slot_cnt * args.steps * world
     out = {
-        "metric": "ed25519 verifies/sec (node, 1/2/4/8 GPUs); p50 latency @4096-sig batch",
-        "value": slots / elapsed, "unit": "verifies/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "int32x32->int64 (field limbs), u64 (SHA-512)",
+        "metric": METRIC, "value": slots * args.steps / elapsed, "unit": "verifies/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": DTYPE,
         "data": "synthetic: GPU-signed multi-signer transactions, resident in HBM",
-        "config": {"workload": "configs[3]: multi-signer txns (1..12 signers, 64..1232-B messages, legacy+v0), "
-                               "%d signatures per GPU" % dev.slot_cnt,
-                   "txns_per_gpu": dev.txn_cnt, "sigs_per_gpu": dev.slot_cnt, "parallelism": "shard%d" % world},
-        "txns_per_s": dev.txn_cnt * args.steps * world / elapsed,
-        "gpu_ms_per_step": gpu_ms,
-        "verdicts": {"ok": int((terr == 0).sum()), "rejected": int((terr != 0).sum())},
-        "mean_payload_sz": float(tsz.mean()), "workload_gen_s": gen_s,
+        "config": {"workload": "configs[3]: %d signatures in multi-signer txns (1..12 signers, 64..1232-B messages, "
+                               "legacy+v0), contiguous shards over %d GPU(s)" % (int(slots), world),
+                   "total_sigs": int(slots), "total_txns": int(txns), "sigs_rank0": dev.slot_cnt,
+                   "parallelism": "shard%d" % world},
+        "txns_per_s": txns * args.steps / elapsed,
+        "gpu_ms_per_step_rank0": gpu_ms,
+        "roofline": dsm_roofline(st, gpu_ms, dev.slot_cnt, kernel="txn pass (parse+k_prep+k_decomp+k_dsm+reduce)",
+                                 note="whole-pass GPU time in the denominator: a lower bound on k_dsm's fraction"),
+        "verdicts": {"ok_txns": int(txns - nrej), "rejected_txns": int(nrej)},
+        "mean_payload_sz": float(tsz.mean()), "workload_gen_s_rank0": gen_s,
     }
+    if world == 1 and not args.no_cpu:
+        # CPU baseline: the reference's fd_txn_parse + fd_ed25519_verify on
+        # every core over a bounded sample of the same transactions; and the
+        # re-check of every rejected transaction by the reference itself
+        L = ref_batch_lib()
+        cores, aff, quota, model = host_cores()
+        nt = args.cpu_threads or cores
+        k = min(toff.size, 1 << 17)
+        err = np.zeros(k, np.int8)
+        passes, dt = timed_passes(lambda: L.ref_txn_verify_batch(k, _vp(payload), _vp(toff), _vp(tsz), _vp(err), nt),
+                                  args.cpu_seconds)
+        sig_k = int(tbase[k])
+        out["cpu_baseline"] = {"value": passes * sig_k / dt, "unit": "verifies/s", "cores": nt, "kind": "reference",
+                               "sample": "%d passes over the first %d transactions (%d signatures) on %d threads, "
+                                         "%.1f s wall" % (passes, k, sig_k, nt, dt),
+                               "host": {"cpu_model": model, "usable_cores": cores, "affinity_cpus": aff,
+                                        "limits": quota},
+                               "verdicts_equal_gpu": bool(np.array_equal(err, terr[:k]))}
+        if rej.size:
+            r_off = np.ascontiguousarray(toff[rej])
+            r_sz = np.ascontiguousarray(tsz[rej])
+            r_err = np.zeros(rej.size, np.int8)
+            L.ref_txn_verify_batch(rej.size, _vp(payload), _vp(r_off), _vp(r_sz), _vp(r_err), nt)
+            out["verdicts"]["rejected_rechecked_by_reference"] = bool(np.array_equal(r_err, terr[rej]))
+            out["verdicts"]["rejected_codes"] = sorted(set(int(c) for c in terr[rej]))
     print(json.dumps(out))
 
 
-def cpu_baseline(pub, sig, off, sz, blob, sample, threads, gpu_err, seconds):
-    """The reference's fd_ed25519_verify (oracle/_ref, compiled from its own
-    sources) on `threads` host threads; falls back to the clean-room port.
-    Bounded sample: passes over the first `sample` signatures of the bench
-    batch until `seconds` of wall time are spent (about 10 s by default)."""
-    import ctypes
-    n = min(sample, pub.shape[0])
-    err = np.zeros(n, np.int8)
-    vp = ctypes.c_void_p
-    args = [ctypes.c_uint64(n), pub.ctypes.data_as(vp), sig.ctypes.data_as(vp), off.ctypes.data_as(vp),
-            sz.ctypes.data_as(vp), blob.ctypes.data_as(vp), err.ctypes.data_as(vp)]
-    refso = os.path.join(ROOT, "oracle", "_ref", "libfdref_batch.so")
-    if os.path.exists(refso):
-        L = ctypes.CDLL(refso)
-        fn, kind = L.ref_ed25519_verify_batch, "reference"
-        fn.argtypes = [ctypes.c_uint64, vp, vp, vp, vp, vp, vp, ctypes.c_int]
-        call = lambda: fn(*args, threads)  # noqa: E731
-    else:
-        L = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
-        fn, kind = L.oracle_ed25519_verify_batch, "port"
-        fn.argtypes = [ctypes.c_uint64, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int]
-        call = lambda: fn(*args, None, threads)  # noqa: E731
-    t0 = time.perf_counter()
-    passes = 0
-    while True:
-        call()
-        passes += 1
-        dt = time.perf_counter() - t0
-        if dt >= seconds:
-            break
-    return {"value": passes * n / dt, "unit": "verifies/s", "cores": threads, "kind": kind,
-            "sample": "%d passes over %d of the bench batch's %d-B signatures, %d threads, %.1f s wall"
-                      % (passes, n, int(sz[0]), threads, dt),
-            "verdicts_equal_gpu": bool(np.array_equal(err, gpu_err[:n]))}
+# ---------------------------------------------------------------- configs[4]
 
+def stream_rows(local, pub, sig, off, sz, blob, args):
+    """config 5: tango mcache/dcache feed -> verify tile -> consumer, per
+    batch cap, copy and zero-copy staging.  The pool carries 10 % corrupted
+    frags (one message bit each: full verify cost, verdict -3); the
+    consumer checks every published frag against the batch engine's
+    verdicts and the SHA-512 tags (verdict, tag and order of every frag;
+    the bytes in the tile's output dcache of every 16th)."""
+    from firedancer_amd import ed25519, tango
+    m = min(pub.shape[0], 1 << 16)
+    p_pub, p_sig, p_sz = pub[:m], sig[:m], sz[:m]
+    p_off = (off[:m] - off[0]).astype(np.uint32)
+    p_blob = blob[off[0]:off[0] + int(p_off[-1]) + int(p_sz[-1])].copy()
+    rng = np.random.default_rng(55)
+    bad = rng.choice(m, m // 10, replace=False)
+    for i in bad:
+        p_blob[p_off[i] + int(rng.integers(0, max(int(p_sz[i]), 1)))] ^= 1 << int(rng.integers(0, 8))
+    eng = ed25519.Engine(device=local, batch_max=m, blob_max=p_blob.size + 64)
+    p_err = eng.verify_soa(p_pub, p_sig, p_off, p_sz, p_blob)
+    eng.close()
+    p_tag = np.array([int.from_bytes(hashlib.sha512(bytes(p_sig[i][:32]) + bytes(p_pub[i]) +
+                                                    bytes(p_blob[p_off[i]:p_off[i] + p_sz[i]])).digest()[:8],
+                                     "little") for i in range(m)], np.uint64)
+    rows = []
+    for bmax in (256, 1024, 4096, 16384):
+        row = {"batch_max": bmax}
+        for zc in (False, True):
+            key = "zero_copy" if zc else "copy"
+            kw = dict(zero_copy=zc, expect_err=p_err, expect_tag=p_tag, sample_bytes=True)
+            sat = tango.bench_stream(local, bmax, 0, p_pub, p_sig, p_off, p_sz, p_blob, args.stream_frags, **kw)
+            rr = {"saturated_frags_per_s": sat["frags_per_s"], "saturated_mean_batch": sat["mean_batch"],
+                  "published": int(sat["published"]), "sv_filt": int(sat["sv_filt"]), "ovrn": int(sat["ovrn"]),
+                  "check_mismatches": int(sat["mismatches"]), "checked": int(sat["checked"])}
+            for load in (0.5, 0.8):
+                rate = load * sat["frags_per_s"]
+                nf = int(min(args.stream_frags, max(20000, rate * 1.0)))
+                r = tango.bench_stream(local, bmax, 0, p_pub, p_sig, p_off, p_sz, p_blob, nf, rate=rate, **kw)
+                rr["at_%d%%" % int(load * 100)] = {"offered_frags_per_s": rate, "frags_per_s": r["frags_per_s"],
+                                                    "p50_us": r["p50_ns"] / 1e3, "p99_us": r["p99_ns"] / 1e3,
+                                                    "mean_batch": r["mean_batch"], "sv_filt": int(r["sv_filt"]),
+                                                    "check_mismatches": int(r["mismatches"])}
+            row[key] = rr
+        rows.append(row)
+    return {"path": "producer (metadata only; frames pre-placed in the data region as a NIC would) -> in "
+                    "mcache/dcache -> verify tile (adaptive GPU batches, 4 in flight; copy: frag copied into the "
+                    "tile's output dcache and released; zero_copy: GPU copies from the mapped input region, input "
+                    "released when its batch retires) -> out mcache + tile-owned out dcache -> consumer (checks "
+                    "verdict, tag and order of every frag, bytes of every 16th); latency = scheduled send to tile publish",
+            "pool": "%d signatures of %d B, %d with one message bit flipped" % (m, int(p_sz[0]), bad.size),
+            "frags_per_run": args.stream_frags,
+            "all_checks_pass": all(r[k]["check_mismatches"] == 0 and r[k]["at_50%"]["check_mismatches"] == 0 and
+                                   r[k]["at_80%"]["check_mismatches"] == 0 for r in rows for k in ("copy", "zero_copy")),
+            "rows": rows}
+
+
+# ---------------------------------------------------------------- configs[1]
 
 def main():
     args = parse()
@@ -198,7 +389,7 @@ def main():
     hip.set_device(local)
 
     if args.workload == "txn":
-        return run_txn(args, rank, world, local, dist)
+        return run_txn(args, rank, world, dist)
 
     n = args.n
     t0 = time.perf_counter()
@@ -228,10 +419,8 @@ def main():
     stream.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        from firedancer_amd.shard import max_over_ranks
+        elapsed = max_over_ranks(elapsed)
         dist.barrier()
 
     stage_ms = np.zeros(3)
@@ -243,18 +432,13 @@ def main():
     err = d_err.to_array(np.int8, n)
     ed25519.work_stats_dev(n, d_ws.ptr, d_stats.ptr, stream.handle)
     stream.synchronize()
-    st = d_stats.to_array(np.uint32, 3 * n).reshape(3, n).astype(np.float64)
-    I, nh, ns = st[0].sum(), st[1].sum(), st[2].sum()
-    live = float((st[0] > 0).sum())
-    dsm_mac = MAC_MUL * (68 * live + 3 * I + 8 * nh + 7 * ns + 2 * live) + MAC_SQ * (4 * live + 4 * I)
-    achieved = dsm_mac / (stage_ms[2] * 1e-3) / 1e12
-    traffic = pmc_traffic("k_dsm", n)
+    st = d_stats.to_array(np.uint32, 3 * n).reshape(3, n)
 
     if rank != 0:
         return
     total = n * args.steps * world
     out = {
-        "metric": "ed25519 verifies/sec (node, 1/2/4/8 GPUs); p50 latency @4096-sig batch",
+        "metric": METRIC,
         "value": total / elapsed,
         "unit": "verifies/s",
         "n_gpus": world,
@@ -264,17 +448,13 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int32x32->int64 (field limbs), u64 (SHA-512)",
+        "dtype": DTYPE,
         "data": "synthetic: fresh random keypairs and messages, signed on the GPU (k_sign), inputs resident in HBM",
         "config": {"workload": "configs[1]: 1xMI355X batch of 2^20 single-signer sigs, 200-byte messages",
                    "sigs_per_gpu_per_step": n, "msg_sz": args.msg_sz, "parallelism": "shard%d" % world},
         "stage_ms": {"k_prep": stage_ms[0], "k_decomp": stage_ms[1], "k_dsm": stage_ms[2]},
         "verdicts": {"ok": int((err == 0).sum()), "rejected": int((err != 0).sum())},
-        "roofline": {"bound": "valu-imad64", "kernel": "k_dsm", "achieved": achieved, "peak": PEAK_TMAC,
-                     "unit": "TMAC/s", "frac": achieved / PEAK_TMAC, "traffic": traffic,
-                     "traffic_note": "HBM bytes per launch from the committed PMC pass (profiles/r01_pmc_latest.json: "
-                                     "2*FETCH_SIZE+WRITE_SIZE KB, gfx950 correction), scaled to this batch",
-                     "mac_per_sig": dsm_mac / max(live, 1.0)},
+        "roofline": dsm_roofline(st, stage_ms[2], n),
         "workload_gen_s": gen_s,
     }
     if not args.no_latency:
@@ -292,10 +472,24 @@ def main():
         lat = np.array(lat[3:])
         out["latency_ms_4096"] = {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
                                   "path": "host SoA -> pinned staging -> H2D -> 3 kernels -> D2H"}
-    if not args.no_latency:
-        # PCIe-inclusive rate: the same 2^20 batch handed over as host SoA
-        # buffers (pinned double-buffered staging, chunks of 2^17), priced
-        # against the measured pinned H2D ceiling.  Never the headline value.
+        # the reference's drop-in entry point, one signature per call (the
+        # verify tile's calling pattern, fd_frank_verify_synth_load.c:380)
+        calls = []
+        for r in range(220):
+            i = (r * 7919) % n
+            msg = bytes(blob[off[i]:off[i] + sz[i]])
+            t1 = time.perf_counter()
+            rc = ed25519.verify(msg, bytes(sig[i]), bytes(pub[i]))
+            calls.append((time.perf_counter() - t1) * 1e6)
+            assert rc == int(err[i])
+        calls = np.array(calls[20:])
+        out["dropin_call_us"] = {"p50": float(np.percentile(calls, 50)), "p99": float(np.percentile(calls, 99)),
+                                 "reference_us_per_call_survey": REF_US_PER_CALL_SURVEY,
+                                 "path": "fd_ed25519_verify: one signature per call, a GPU batch of one "
+                                         "(packed staging -> k_front -> k_dsm4 -> mapped result)"}
+        # PCIe-inclusive rates: the same 2^20 batch handed over as host SoA
+        # buffers, chunks of 2^17 with 2 in flight, priced against the
+        # measured pinned H2D ceiling.  Never the headline value.
         chunk = 1 << 17
         eng = ed25519.Engine(device=local, batch_max=chunk, blob_max=chunk * args.msg_sz)
         eng.verify_soa(pub[:chunk], sig[:chunk], off[:chunk], sz[:chunk], blob)
@@ -303,6 +497,14 @@ def main():
         for _ in range(reps):
             herr = eng.verify_soa(pub, sig, off, sz, blob)
         dt = (time.perf_counter() - t1) / reps
+        reg = ed25519.RegisteredPlanes(pub, sig, off, sz, blob)
+        rerr = np.zeros(n, np.int8)
+        eng.verify_soa_registered(reg[0], reg[1], reg[2], reg[3], reg[4], rerr)
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            eng.verify_soa_registered(reg[0], reg[1], reg[2], reg[3], reg[4], rerr)
+        dt_reg = (time.perf_counter() - t1) / reps
+        reg.close()
         eng.close()
         h2d_gbs = hip.h2d_bandwidth()
         per_sig = 104 + args.msg_sz
@@ -311,36 +513,18 @@ def main():
                            "pcie_bound_verifies_per_s": h2d_gbs * 1e9 / per_sig,
                            "verdicts_match_resident": bool((herr == err).all()),
                            "path": "host SoA -> pinned packed staging (2 chunks in flight) -> H2D -> kernels -> D2H"}
+        out["host_soa_registered"] = {"verifies_per_s": n / dt_reg, "chunk": chunk,
+                                      "h2d_gb_per_s": n * per_sig / dt_reg / 1e9,
+                                      "verdicts_match_resident": bool((rerr == err).all()),
+                                      "path": "caller planes registered once (fd_ed25519_amd_host_register) -> DMA "
+                                              "of each chunk's planes and message window, no host copy -> kernels"}
     if world == 1 and not args.no_stream:
-        # config 5: tango mcache/dcache feed -> verify tile -> consumer, per batch cap
-        from firedancer_amd import tango
-        m = min(n, 1 << 16)
-        rows = []
-        for bmax in (256, 1024, 4096, 16384):
-            row = {"batch_max": bmax}
-            for zc in (False, True):
-                key = "zero_copy" if zc else "copy"
-                sat = tango.bench_stream(local, bmax, 0, pub[:m], sig[:m], off[:m], sz[:m], blob, args.stream_frags,
-                                         zero_copy=zc)
-                rr = {"saturated_frags_per_s": sat["frags_per_s"], "saturated_mean_batch": sat["mean_batch"]}
-                for load in (0.5, 0.8):
-                    rate = load * sat["frags_per_s"]
-                    nf = int(min(args.stream_frags, max(20000, rate * 1.0)))
-                    r = tango.bench_stream(local, bmax, 0, pub[:m], sig[:m], off[:m], sz[:m], blob, nf, rate=rate,
-                                           zero_copy=zc)
-                    rr["at_%d%%" % int(load * 100)] = {"offered_frags_per_s": rate, "frags_per_s": r["frags_per_s"],
-                                                        "p50_us": r["p50_ns"] / 1e3, "p99_us": r["p99_ns"] / 1e3,
-                                                        "mean_batch": r["mean_batch"]}
-                row[key] = rr
-            rows.append(row)
-        out["stream_tile"] = {"path": "producer (metadata only; frames pre-placed in the data region as a NIC would) "
-                                      "-> in mcache/dcache -> verify tile (adaptive GPU batches, 4 in flight; copy: "
-                                      "host staging, zero_copy: GPU-mapped data region) -> out mcache -> consumer; "
-                                      "latency = scheduled send to tile publish",
-                              "frags_per_run": args.stream_frags, "rows": rows}
+        out["stream_tile"] = stream_rows(local, pub, sig, off, sz, blob, args)
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(pub, sig, off, sz, blob, args.cpu_sample, args.cpu_threads, err,
                                            args.cpu_seconds)
+        if "dropin_call_us" in out:
+            out["dropin_call_us"]["reference_us_per_call_this_host"] = out["cpu_baseline"]["us_per_call_1_thread"]
     print(json.dumps(out))
 
 

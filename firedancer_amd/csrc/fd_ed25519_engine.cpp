@@ -591,7 +591,7 @@ fd_ed25519_amd_verify_txns_dev( ulong txn_cnt, ulong slot_cnt, uchar const * d_p
                                (int8_t *)(w + L.skip), st ) )
     return FD_ED25519_AMD_ERR_DEVICE;
   if( slot_cnt && fd_amd_launch_verify( (uint32_t)slot_cnt, w + L.pub, w + L.sig, (uint32_t *)(w + L.off),
-                                        (uint32_t *)(w + L.sz), d_payload, err, w + L.vws, st, 0, NULL,
+                                        (uint32_t *)(w + L.sz), d_payload, err, w + L.vws, st, 1, NULL,
                                         (int8_t *)(w + L.skip) ) )
     return FD_ED25519_AMD_ERR_DEVICE;
   if( fd_amd_launch_txn_reduce( (uint32_t)txn_cnt, (uint32_t *)(w + L.fp), d_tbase, err, (int8_t *)d_txn_err, st ) )

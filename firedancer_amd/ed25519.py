@@ -336,6 +336,35 @@ class MultiEngine:
         return _verify_txns(lib().fd_ed25519_amd_multi_verify_txns, self._h, payload, txn_off, txn_sz, want_sigs)
 
 
+class RegisteredPlanes:
+    """Page-aligned copies of numpy arrays, registered with
+    fd_ed25519_amd_host_register (inputs of Engine.verify_soa_registered);
+    planes[k] is the registered copy of arrays[k].  close() unregisters."""
+
+    def __init__(self, *arrays):
+        self._raw = []
+        self.planes = []
+        for a in arrays:
+            a = np.ascontiguousarray(a)
+            nb = (max(a.nbytes, 1) + 4095) & ~4095
+            raw = np.zeros(nb + 4096, np.uint8)
+            o = (-raw.ctypes.data) % 4096
+            region = raw[o:o + nb]
+            b = region[:a.nbytes].view(a.dtype).reshape(a.shape)
+            b[...] = a
+            host_register(region)
+            self._raw.append(region)
+            self.planes.append(b)
+
+    def __getitem__(self, k):
+        return self.planes[k]
+
+    def close(self):
+        for r in self._raw:
+            host_unregister(r)
+        self._raw = []
+
+
 def host_register(arr):
     """Pin a numpy array's memory for fd_ed25519_amd_verify_soa_registered."""
     rc = lib().fd_ed25519_amd_host_register(_ptr(arr), int(arr.nbytes))

@@ -116,11 +116,12 @@ class VerifyTile:
         return d, lat[:min(lat_max, d["out_cnt"])]
 
 
-BENCH_ZERO_COPY, BENCH_WRITE, BENCH_LAP = 1, 2, 4
+BENCH_ZERO_COPY, BENCH_WRITE, BENCH_LAP, BENCH_SAMPLE_BYTES = 1, 2, 4, 8
 
 
 def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, blob, frag_cnt, rate=0.0,
-                 zero_copy=False, writes=False, lap=False, dcache_frames=0, expect_err=None, expect_tag=None):
+                 zero_copy=False, writes=False, lap=False, dcache_frames=0, expect_err=None, expect_tag=None,
+                 sample_bytes=False):
     """fd_verify_amd_bench_stream: producer (rate frags/s, 0 = saturate) -> tile -> consumer; returns
     dict(frags_per_s, p50_ns, p99_ns, p999_ns, mean_batch, published, sv_filt, ovrn, mismatches, checked).
     With expect_err/expect_tag (per pool entry) the consumer checks every published frag."""
@@ -128,7 +129,8 @@ def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, bl
     p = [np.ascontiguousarray(a) for a in (pub, sig, msg_off, msg_sz, blob)]
     ee = np.ascontiguousarray(expect_err, np.int8) if expect_err is not None else None
     et = np.ascontiguousarray(expect_tag, np.uint64) if expect_tag is not None else None
-    flags = (BENCH_ZERO_COPY if zero_copy else 0) | (BENCH_WRITE if writes else 0) | (BENCH_LAP if lap else 0)
+    flags = (BENCH_ZERO_COPY if zero_copy else 0) | (BENCH_WRITE if writes else 0) | (BENCH_LAP if lap else 0) | \
+        (BENCH_SAMPLE_BYTES if sample_bytes else 0)
     vp = ctypes.c_void_p
     rc = ed25519.lib().fd_verify_amd_bench_stream(int(device), int(batch_max), int(batch_wait_ns), float(rate), flags,
                                                   int(dcache_frames), p[0].shape[0],

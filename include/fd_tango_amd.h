@@ -123,6 +123,10 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    that were verified.  A frame is reused only once the consumer's out_fseq
    has passed the frag it last carried (backpressure otherwise), so the
    output never changes under a consumer that honours flow control.
+   Each in-flight batch runs on its own HIP stream, and streams only
+   overlap on distinct hardware queues: run the process with
+   GPU_MAX_HW_QUEUES >= 16 (HIP's default 4 put the 4 streams on 2 queues
+   and halved the small-batch rate, profiles/r02_tile_queues.txt).
    NULL on failure. */
 #define FD_VERIFY_AMD_FRAME_SZ (1408UL)   /* 22 chunks >= 96 + FD_ED25519_AMD_MSG_MAX */
 
@@ -226,6 +230,9 @@ fd_verify_amd_tickcount( void );
    NIC would (otherwise every pool frame is pre-placed once and only
    metadata is published).  FD_VERIFY_AMD_BENCH_LAP: the producer ignores
    the tile's credit (only with WRITE; overrun test).
+   FD_VERIFY_AMD_BENCH_SAMPLE_BYTES: the consumer compares the bytes of
+   every 16th published frag only (verdict, tag and order of every one), so
+   the check does not limit the saturated rate.
 
    expect_err / expect_tag (pool_n each, NULL = no check): the consumer
    checks every published frag against them -- the frag's verdict must be
@@ -246,6 +253,7 @@ fd_verify_amd_tickcount( void );
 #define FD_VERIFY_AMD_BENCH_ZERO_COPY (1)
 #define FD_VERIFY_AMD_BENCH_WRITE     (2)
 #define FD_VERIFY_AMD_BENCH_LAP       (4)
+#define FD_VERIFY_AMD_BENCH_SAMPLE_BYTES (8)
 
 int
 fd_verify_amd_bench_stream( int           device,

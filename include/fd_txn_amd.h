@@ -170,7 +170,9 @@ fd_ed25519_amd_multi_verify_txns( fd_ed25519_amd_multi_t * multi,
    fd_ed25519_amd_txn_slots computes on the host.  d_sig_err (optional,
    slot_cnt entries) receives the per-signature codes.  d_ws: at least
    fd_ed25519_amd_txn_workspace_footprint(txn_cnt, slot_cnt) bytes,
-   256-aligned. */
+   256-aligned; it begins with the signature verify's workspace, so
+   fd_ed25519_amd_work_stats_dev( slot_cnt, d_ws, ... ) reads the call's
+   per-signature work statistics. */
 ulong
 fd_ed25519_amd_txn_workspace_footprint( ulong txn_cnt, ulong slot_cnt );
 

@@ -74,29 +74,9 @@ def test_verify_txns_dev_fails_closed_on_short_slot_table():
     assert np.array_equal(terr[1:], eterr[1:])
 
 
-class _Registered:
-    """SoA planes copied into page-aligned arrays registered with
-    fd_ed25519_amd_host_register."""
-
-    def __init__(self, *arrays):
-        from firedancer_amd import ed25519
-        self.arrs = []
-        for a in arrays:
-            a = np.ascontiguousarray(a)
-            raw = np.zeros(a.nbytes + 8192, np.uint8)
-            o = (-raw.ctypes.data) % 4096
-            b = raw[o:o + max(a.nbytes, 1)].view(a.dtype)[:a.size].reshape(a.shape)
-            b[...] = a
-            ed25519.host_register(raw[o:o + ((max(a.nbytes, 1) + 4095) & ~4095)])
-            self.arrs.append((raw, o, b))
-
-    def __getitem__(self, k):
-        return self.arrs[k][2]
-
-    def close(self):
-        from firedancer_amd import ed25519
-        for raw, o, _ in self.arrs:
-            ed25519.host_unregister(raw[o:])
+def _Registered(*arrays):
+    from firedancer_amd import ed25519
+    return ed25519.RegisteredPlanes(*arrays)
 
 
 def test_registered_batches_equal_staged(engine, golden):

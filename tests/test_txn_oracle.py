@@ -109,3 +109,29 @@ def test_synthetic_multisigner_rule():
     assert terr[1] == -3 and all(e == -3 for e in serr[base[1]:base[2]])
     assert terr[2] == -4 and all(e == -4 for e in serr[base[2]:base[3]])
     assert base[-1] == nsig.sum()
+
+
+def test_oracle_multisigner_rule_matches_compiled_reference():
+    """oracle/ref_batch.c's ref_txn_verify_batch (the reference's own
+    fd_txn_parse + fd_ed25519_verify, the CPU baseline and re-check of
+    bench.py's transaction workload) gives the oracle's per-transaction
+    verdicts on corrupted synthetic transactions."""
+    import ctypes
+    import os
+    so = os.path.join(os.path.dirname(_oracle.REF_SO), "libfdref_batch.so")
+    if not os.path.exists(so):
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    rng = np.random.default_rng(12)
+    pays, nsig = _txn.build_txns(12, 120)
+    pays = [bytearray(p) for p in pays]
+    for t in rng.choice(len(pays), 40, replace=False):
+        pays[t][int(rng.integers(0, len(pays[t])))] ^= 1 << int(rng.integers(0, 8))
+    blob, off, sz = _txn.pack([bytes(p) for p in pays])
+    L = ctypes.CDLL(so)
+    vp = ctypes.c_void_p
+    L.ref_txn_verify_batch.argtypes = [ctypes.c_uint64, vp, vp, vp, vp, ctypes.c_int]
+    err = np.zeros(len(pays), np.int8)
+    L.ref_txn_verify_batch(len(pays), blob.ctypes.data, off.ctypes.data, sz.ctypes.data, err.ctypes.data, 4)
+    terr, _, _ = _oracle.txn_verify_batch(blob, off, sz)
+    assert np.array_equal(err, terr)
+    assert (err != 0).sum() >= 20
