@@ -102,3 +102,16 @@ def test_slide_restatement_properties():
         r = _slide.slide(a)
         assert sum(d << i for i, d in enumerate(r)) == a
         assert all(d == 0 or (d % 2 == 1 and -15 <= d <= 15) for d in r)
+
+
+def test_golden_fixtures_regenerate_identically():
+    """Provenance: the committed fixtures are what the generators, linked
+    against the compiled reference, write today (tests/golden/README.md)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not (os.path.isdir("/root/reference/src") and os.path.exists(os.path.join(root, "oracle", "_ref", "gen_golden"))):
+        pytest.skip("needs /root/reference and oracle/_ref (build container)")
+    r = subprocess.run([os.path.join(root, "tools", "regen_golden.sh")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("identical to the committed fixture") == 3
