@@ -41,6 +41,20 @@ FD_DEV i64 mll ( i32 a, i32 b ) { return (i64)a * (i64)b; }            /* v_mad_
 FD_DEV i64 fd_pin( i64 x ) { asm( "" : "+v"(x) ); return x; }
 FD_DEV i64 mac( i32 a, i32 b, i64 c ) { return fd_pin( (i64)a * (i64)b + c ); }
 
+/* a + b + c (mod 2^32) as one v_add3_u32: LLVM otherwise reassociates a
+   chain of adds around its operands; c may be a wave-uniform SGPR value
+   (gfx9 VOP3 takes no literal, so a constant offset goes through an SGPR). */
+FD_DEV i32 fd_add3( i32 a, i32 b, i32 c ) {
+  i32 r; asm( "v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c) ); return r;
+}
+FD_DEV i32 fd_add3s( i32 a, i32 b, i32 c ) {
+  i32 r; asm( "v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c) ); return r;
+}
+/* (a ^ b) + c as one v_xad_u32 (with b = 0 / -1 and c = 0 / 1: a or -a) */
+FD_DEV i32 fd_xad( i32 a, i32 b, i32 c ) {
+  i32 r; asm( "v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c) ); return r;
+}
+
 FD_DEV fe fe_add( fe const & f, fe const & g ) { fe h; _Pragma("unroll") for( int i=0; i<10; i++ ) h.v[i] = (i32)((u32)f.v[i] + (u32)g.v[i]); return h; }
 FD_DEV fe fe_sub( fe const & f, fe const & g ) { fe h; _Pragma("unroll") for( int i=0; i<10; i++ ) h.v[i] = (i32)((u32)f.v[i] - (u32)g.v[i]); return h; }
 FD_DEV fe fe_neg( fe const & f )               { fe h; _Pragma("unroll") for( int i=0; i<10; i++ ) h.v[i] = (i32)(0u - (u32)f.v[i]); return h; }
@@ -109,7 +123,10 @@ FD_DEV fe fe_carry_b( i64 h0, i64 h1, i64 h2, i64 h3, i64 h4, i64 h5, i64 h6, i6
    column's 2^24 pre-shifted by 26 ((h + 2^50) >> 26 == (h >> 26) + 2^24,
    low 26 bits untouched); odd columns carry no bias of their own.  This
    finishes the chain once columns 1..9 hold their carries-in.  Same limbs
-   as fe_carry / fe_carry_b. */
+   as fe_carry / fe_carry_b.  BIAS: return every limb plus its rounding
+   offset (2^25 even, 2^24 odd limbs), for a consumer that folds the offset
+   into an operation it does anyway (the k_dsm mix), saving the subtract. */
+template<bool BIAS = false>
 FD_DEV fe fe_carry_fold_out( i64 h0, i64 h1, i64 h2, i64 h3, i64 h4, i64 h5, i64 h6, i64 h7, i64 h8, i64 h9 ) {
   i64 const M26 = (1L<<26) - 1;
   i64 t4 = (h4 & M26) + (h3 >> 25);
@@ -117,17 +134,18 @@ FD_DEV fe fe_carry_fold_out( i64 h0, i64 h1, i64 h2, i64 h3, i64 h4, i64 h5, i64
   i64 t0 = (h0 & M26) + (h9 >> 25) * 19;
   i32 c0b = (i32)(t0 >> 26);
   u32 const m26 = (1u<<26) - 1u, m25 = (1u<<25) - 1u;
+  i32 const o26 = BIAS ? 0 : (1<<25), o25 = BIAS ? 0 : (1<<24);
   fe r;
-  r.v[0] = (i32)((u32)t0 & m26) - (1<<25);
-  r.v[1] = (i32)((u32)h1 & m25) - (1<<24) + c0b;
-  r.v[2] = (i32)((u32)h2 & m26) - (1<<25);
-  r.v[3] = (i32)((u32)h3 & m25) - (1<<24);
-  r.v[4] = (i32)((u32)t4 & m26) - (1<<25);
-  r.v[5] = (i32)((u32)h5 & m25) - (1<<24) + c4b;
-  r.v[6] = (i32)((u32)h6 & m26) - (1<<25);
-  r.v[7] = (i32)((u32)h7 & m25) - (1<<24);
-  r.v[8] = (i32)((u32)h8 & m26) - (1<<25);
-  r.v[9] = (i32)((u32)h9 & m25) - (1<<24);
+  r.v[0] = (i32)((u32)t0 & m26) - o26;
+  r.v[1] = (i32)((u32)h1 & m25) - o25 + c0b;
+  r.v[2] = (i32)((u32)h2 & m26) - o26;
+  r.v[3] = (i32)((u32)h3 & m25) - o25;
+  r.v[4] = (i32)((u32)t4 & m26) - o26;
+  r.v[5] = (i32)((u32)h5 & m25) - o25 + c4b;
+  r.v[6] = (i32)((u32)h6 & m26) - o26;
+  r.v[7] = (i32)((u32)h7 & m25) - o25;
+  r.v[8] = (i32)((u32)h8 & m26) - o26;
+  r.v[9] = (i32)((u32)h9 & m25) - o25;
   return r;
 }
 
@@ -180,6 +198,7 @@ FD_DEV fe fe_mul( fe const & F, fe const & G ) {
    limbs as fe_mul. */
 template<int K>
 FD_DEV void fe_term( int i, i32 const * f, i32 const * f_2, i32 const * g, i32 const * g_19, i64 & a );
+template<bool BIAS1 = false, bool BIAS2 = false>   /* per product: limbs + rounding offset (fe_carry_fold_out) */
 FD_DEV void fe_mul_fold2w( fe & R1, fe const & F1, fe const & G1, fe & R2, fe const & F2, fe const & G2 ) {
   i64 const kb = fd_opaque( (1L<<25) + (1L<<50) );
   i32 f1_2[10], g1_19[10], f2_2[10], g2_19[10];
@@ -205,8 +224,8 @@ FD_DEV void fe_mul_fold2w( fe & R1, fe const & F1, fe const & G1, fe & R2, fe co
   _Pragma("unroll") for( int i=0; i<10; i++ ) { FD_TA( 9, a9 ); FD_TB( 9, b9 ); }
 # undef FD_TA
 # undef FD_TB
-  R1 = fe_carry_fold_out( a0, a1, a2, a3, a4, a5, a6, a7, a8, a9 );
-  R2 = fe_carry_fold_out( b0, b1, b2, b3, b4, b5, b6, b7, b8, b9 );
+  R1 = fe_carry_fold_out<BIAS1>( a0, a1, a2, a3, a4, a5, a6, a7, a8, a9 );
+  R2 = fe_carry_fold_out<BIAS2>( b0, b1, b2, b3, b4, b5, b6, b7, b8, b9 );
 }
 
 /* Term i of column K of one fe_mul (the rule above fe_mul_fold2w). */

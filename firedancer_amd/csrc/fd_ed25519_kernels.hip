@@ -554,25 +554,40 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
         a2.v[k] = u.Z.v[k];                              b2.v[k] = vsel( mD, u.Z.v[k] + u.Z.v[k], QV( 0, k ) );
         a3.v[k] = vsel( mD, u.X.v[k], u.T.v[k] );        b3.v[k] = vsel( mD, u.X.v[k], QV( 3, k ) );
       }
-      fe_mul_fold2w( m0, a0, b0, m1, a1, b1 );
-      fe_mul_fold2w( m2, a2, b2, m3, a3, b3 );
+      /* m0, m1, m3 come back with their limbs' rounding offsets b (2^25
+         even, 2^24 odd) still added: the mix below folds them into its
+         own adds; m2 is exact */
+      fe_mul_fold2w<true, true>( m0, a0, b0, m1, a1, b1 );
+      fe_mul_fold2w<false, true>( m2, a2, b2, m3, a3, b3 );
     }
     /* lanes that are done (PH_DONE) keep computing on don't-care values:
-       nothing they compute is stored */
-    _Pragma("unroll") for( int k=0; k<10; k++ ) {
-      i32 A0 = m0.v[k], A1 = m1.v[k], A2 = m2.v[k], A3 = m3.v[k];
-      /* DBL mix [a-b-c, b+c, b-c, d-b+c] with a=m0 b=m1 c=m2 d=m3;
-         ADD mix [P-M, P+M, 2Z+-T, 2Z-+T] with P=m0 M=m1 Z=m2 T=m3 */
-      i32 z2 = A2 + A2;
-      /* DBL: m2 = 2Z^2, m3 = X^2 */
-      i32 dY = A1 + A3, dZ = A1 - A3, dX = A0 - dY, dT = A2 - dZ;
-      i32 aX = A0 - A1,      aY = A0 + A1;
-      i32 zp = z2 + A3, zm = z2 - A3;
-      i32 aZ = vsel( mN, zm, zp ), aT = vsel( mN, zp, zm );
-      t.X.v[k] = vsel( mD, dX, aX );
-      t.Y.v[k] = vsel( mD, dY, aY );
-      t.Z.v[k] = vsel( mD, dZ, aZ );
-      t.T.v[k] = vsel( mD, dT, aT );
+       nothing they compute is stored.
+       DBL mix [a-b-c, b+c, b-c, d-b+c] with a=m0 b=m1 c=m3 d=m2 (m2 = Z*2Z, m3 = X^2);
+       ADD mix [P-M, P+M, 2Z+sT, 2Z-sT] with P=m0 M=m1 Z=m2 T=m3, s = neg ? -1 : 1.
+       With sA3 = s'*m3 (s' = -1 on DBL lanes, one v_xad_u32), 11 ops per limb:
+         X = (m0 - m1) + (sA3 & D)            Y = m1 + (D ? m3 : m0)
+         Z = (D ? m1 : 2 m2) + sA3            T = (m2 << (D ? 0 : 2)) - Z
+       plus per-lane offset corrections cX (DBL: +b), cZ (ADD: -s b) and the
+       uniform -2b of Y, each folded into a v_add3_u32.  Limbs equal the
+       reference's wrapping int32 adds (every identity holds mod 2^32). */
+    {
+      u64 mS = mD | mN;
+      i32 Dv = vsel( mD, -1, 0 ), Sv = vsel( mS, -1, 0 ), Sn = vsel( mS, 1, 0 );
+      i32 cXe = Dv & (1<<25), cXo = Dv & (1<<24);
+      i32 cZe = vsel( mD, 0, vsel( mN, (1<<25), -(1<<25) ) ), cZo = vsel( mD, 0, vsel( mN, (1<<24), -(1<<24) ) );
+      i32 const nb2e = (i32)fd_opaque( -(2L<<25) ), nb2o = (i32)fd_opaque( -(2L<<24) );   /* SGPR */
+      i32 const sT = vsel( mD, 0, 2 );                     /* T = (m2 << sT) - Z: DBL m2 - Z, ADD 4 m2 - Z */
+      _Pragma("unroll") for( int k=0; k<10; k++ ) {
+        i32 cX = (k & 1) ? cXo : cXe, cZ = (k & 1) ? cZo : cZe;
+        i32 A0 = m0.v[k], A1 = m1.v[k], A2 = m2.v[k], A3 = m3.v[k];
+        i32 sA3 = fd_xad( A3, Sv, Sn );
+        i32 z2 = A2 + A2;
+        i32 Z = fd_add3( vsel( mD, A1, z2 ), sA3, cZ );
+        t.X.v[k] = fd_add3( A0 - A1, sA3 & Dv, cX );
+        t.Y.v[k] = fd_add3s( A1, vsel( mD, A3, A0 ), (k & 1) ? nb2o : nb2e );
+        t.Z.v[k] = Z;
+        t.T.v[k] = (i32)((u32)A2 << (u32)sT) - Z;
+      }
     }
 
     /* advance the lane's op stream: the event just executed is consumed; the next op follows from the
