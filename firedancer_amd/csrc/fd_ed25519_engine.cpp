@@ -393,7 +393,10 @@ fd_ed25519_amd_verify_soa( fd_ed25519_amd_t * e, ulong n, uchar const * pub, uch
 extern "C" int
 fd_ed25519_amd_host_register( void * base, ulong sz ) {
   if( !base || !sz ) return FD_ED25519_AMD_ERR_INVAL;
-  if( hipHostRegister( base, sz, hipHostRegisterPortable ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  /* portable: usable by every device's engine; mapped: small batches are
+     read in place by the GPU (no copy at all) */
+  if( hipHostRegister( base, sz, hipHostRegisterPortable | hipHostRegisterMapped ) != hipSuccess )
+    return FD_ED25519_AMD_ERR_DEVICE;
   return FD_ED25519_AMD_OK;
 }
 
@@ -444,7 +447,26 @@ fd_ed25519_amd_verify_soa_registered( fd_ed25519_amd_t * e, ulong n, uchar const
       (blob && blob_sz && !host_registered( blob )) )
     return FD_ED25519_AMD_ERR_INVAL;
   if( hipSetDevice( e->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
-  ulong i = 0; int k = 0; int rc = FD_ED25519_AMD_OK;
+  int rc = FD_ED25519_AMD_OK;
+  if( n <= e->cap && fd_amd_uses_latency_path( (uint32_t)n, 0 ) ) {
+    /* a latency-path batch is read once, by k_front: it reads the caller's
+       registered planes in place over PCIe, with no copy on either side */
+    void * d[5] = { NULL, NULL, NULL, NULL, NULL };
+    void const * h[5] = { pub, sig, msg_off, msg_sz, (blob && blob_sz) ? blob : pub };
+    for( int j=0; j<5; j++ )
+      if( hipHostGetDevicePointer( &d[j], (void *)h[j], 0 ) != hipSuccess ) { (void)hipGetLastError(); return FD_ED25519_AMD_ERR_INVAL; }
+    slot_t * s = &e->slot[0];
+    if( (rc = fd_amd_slot_drain( s )) ) return engine_quiesce( e, rc );
+    if( fd_amd_launch_verify( (uint32_t)n, (uint8_t const *)d[0], (uint8_t const *)d[1], (uint32_t const *)d[2],
+                              (uint32_t const *)d[3], (uint8_t const *)d[4], s->d_err, s->d_ws, s->stream, 1, NULL ) )
+      return engine_quiesce( e, FD_ED25519_AMD_ERR_DEVICE );
+    if( slot_out( s, s->h_err, s->d_err, n ) != hipSuccess || hipEventRecord( s->done, s->stream ) != hipSuccess )
+      return engine_quiesce( e, FD_ED25519_AMD_ERR_DEVICE );
+    s->out = err; s->n = n; s->busy = 1; s->want_tag = 0;
+    if( (rc = fd_amd_slot_drain( s )) ) return engine_quiesce( e, rc );
+    return FD_ED25519_AMD_OK;
+  }
+  ulong i = 0; int k = 0;
   while( i < n ) {
     slot_t * s = &e->slot[k];
     if( (rc = fd_amd_slot_drain( s )) ) return engine_quiesce( e, rc );

@@ -222,7 +222,7 @@ class Engine:
 
     def verify_soa_registered(self, pub, sig, msg_off, msg_sz, blob, err=None):
         """fd_ed25519_amd_verify_soa_registered: every plane must lie in memory
-        registered with host_register (see RegisteredBatch); no host copy."""
+        registered with host_register (see RegisteredPlanes); no host copy."""
         n = int(pub.shape[0])
         if err is None:
             err = np.zeros(n, np.int8)

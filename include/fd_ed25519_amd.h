@@ -151,7 +151,10 @@ fd_ed25519_amd_verify_soa( fd_ed25519_amd_t * eng,
    fd_ed25519_amd_verify_soa_registered moves each chunk's planes and its
    message window from the caller's memory to the device by DMA, with no
    host-side copy (fd_ed25519_amd_verify_soa copies into pinned staging
-   first).  Same arguments, verdicts and errors as
+   first); a batch small enough for the latency kernels (the
+   fd_ed25519_amd_set_small_batch_max cap, default 16384, and at most
+   batch_max) is read in place by the GPU over PCIe, with no copy at all.
+   Same arguments, verdicts and errors as
    fd_ed25519_amd_verify_soa; FD_ED25519_AMD_ERR_INVAL if a plane is not
    registered.  A chunk whose messages are scattered over much more than
    their total size is gathered through the staging instead. */
