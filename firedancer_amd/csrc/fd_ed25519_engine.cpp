@@ -766,5 +766,5 @@ fd_ed25519_strerror( int err ) {
 
 extern "C" char const *
 fd_ed25519_amd_version( void ) {
-  return "fd_ed25519_amd 0.2 (gfx950; k_prep/k_decomp/k_dsm + k_dsm4, txn front end, verify tile, GPU signer)";
+  return "fd_ed25519_amd 0.3 (gfx950; k_prep/k_decomp/k_dsm + k_front/k_dsm8/k_dsm4, txn front end, verify tile, multi-device, GPU signer)";
 }

@@ -23,9 +23,9 @@ int fd_amd_launch_verify( uint32_t n, uint8_t const * d_pub, uint8_t const * d_s
                           uint32_t const * d_sz, uint8_t const * d_blob, int8_t * d_err, void * d_ws,
                           hipStream_t stream, int want_stats, hipEvent_t const * ev /* 4 or NULL */,
                           int8_t const * d_skip = NULL, int dsm_mode = 0 );
-/* dsm_mode: 0 = by batch size (fd_ed25519_amd_set_small_batch_max), 1 = the
-   throughput path (k_prep, k_decomp, k_dsm), 2 = the latency path
-   (k_front, k_dsm4). */
+/* dsm_mode: 0 = by batch size (fd_ed25519_amd_set_latency_batch_max,
+   fd_ed25519_amd_set_small_batch_max), 1 = the throughput path (k_prep,
+   k_decomp, k_dsm), 2 = k_front + k_dsm4, 3 = k_front + k_dsm8. */
 
 /* Transaction front end (fd_txn_kernels.hip).
    k_txn_parse: one lane per transaction t = d_payload[d_toff[t] .. +d_tsz[t]).
@@ -64,8 +64,12 @@ int fd_amd_launch_tile_gather( uint32_t n, uint32_t const * d_meta, uint8_t cons
    lists k_prep writes. */
 int fd_amd_launch_digits_dense( uint32_t n, void const * d_ws, uint16_t * d_dig, hipStream_t stream );
 
-/* 1 when a batch of n takes the latency kernels (k_front + k_dsm4). */
+/* 1 when a batch of n takes the latency kernels (k_front + k_dsm8/k_dsm4). */
 int fd_amd_uses_latency_path( uint32_t n, int dsm_mode );
+/* dsm_mode for one of several concurrent batches (the streaming tile):
+   k_dsm4 up to fd_ed25519_amd_set_small_batch_max, else k_dsm; never k_dsm8,
+   whose doubled wave count oversubscribes the SIMDs when batches overlap. */
+int fd_amd_batch_dsm_mode( uint32_t n );
 
 /* d_off[i] -= lo for every nonempty message (0 for empty ones). */
 int fd_amd_launch_rebase_off( uint32_t n, uint32_t * d_off, uint32_t const * d_sz, uint32_t lo, hipStream_t stream );

@@ -985,6 +985,273 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
 }
 
 /* ------------------------------------------------------------------ */
+/* k_dsm8: k_dsm4's op stream on EIGHT lanes per signature (8 signatures per
+ * wave): two lane quads hold the same state, and every field mul of the
+ * step is split between lane l (h = 0, even columns) and lane l ^ 4 (h = 1,
+ * odd columns), 50 products each, so one step issues half the
+ * multiply-accumulates per lane.  The instruction stream stays uniform:
+ * lane h = 1 sees G shifted down one limb (G[j] = g_{j+1}, its wrap entry
+ * G19[9] = g_0) and F undoubled, so slot (c, i) of both halves is
+ * f_i * g_{2c+h-i} with that column's reference factors (x2 when i and j are
+ * odd, x19 when i + j >= 10, on the wrapped int32 pre-multiples).  The five
+ * 64-bit column sums are swapped between the two lanes with DPP
+ * row_shl/row_shr 4 under bank masks, and both lanes finish the reference
+ * carry chain (fe_carry_b on pre-biased sums): the same limbs as fe_mul. */
+struct half_t { u64 mH; i32 shF; i64 bias; };
+__device__ __forceinline__ half_t half_ctx( int hh ) {
+  half_t H;
+  H.mH = __builtin_amdgcn_ballot_w64( hh != 0 );
+  H.shF = hh ? 0 : 1;
+  H.bias = hh ? (1L<<24) : (1L<<25);
+  asm( "" : "+v"(H.shF) );
+  return H;
+}
+
+/* the partner lane's value (lane l ^ 4 of the 8-lane group) where `mine`
+   is the h = 0 / h = 1 slot: E keeps h = 0's own value and takes the partner's
+   on h = 1 lanes, O the other way round */
+__device__ __forceinline__ u32 half_from_lo( u32 v ) {   /* h = 1 lanes read lane - 4 (banks 1, 3) */
+  return (u32)__builtin_amdgcn_update_dpp( (int)v, (int)v, 0x114, 0xf, 0xa, false );
+}
+__device__ __forceinline__ u32 half_from_hi( u32 v ) {   /* h = 0 lanes read lane + 4 (banks 0, 2) */
+  return (u32)__builtin_amdgcn_update_dpp( (int)v, (int)v, 0x104, 0xf, 0x5, false );
+}
+
+__device__ __forceinline__ fe
+fe_mul_half( fe const & F, fe const & G, half_t const & H ) {
+  i32 gs[9], g19[10], f2[10];
+  _Pragma("unroll") for( int j=0; j<9; j++ ) gs[j] = vsel( H.mH, G.v[j+1], G.v[j] );
+  _Pragma("unroll") for( int j=1; j<9; j++ ) g19[j] = wmul( gs[j], 19 );
+  g19[9] = vsel( H.mH, G.v[0], wmul( G.v[9], 19 ) );
+  _Pragma("unroll") for( int i=1; i<10; i+=2 ) f2[i] = (i32)((u32)F.v[i] << (u32)H.shF);
+  i64 a[5];
+  _Pragma("unroll") for( int c=0; c<5; c++ ) a[c] = H.bias;
+  _Pragma("unroll") for( int i=0; i<10; i++ ) {
+    _Pragma("unroll") for( int c=0; c<5; c++ ) {
+      int j = 2*c - i;
+      i32 g = (j >= 0) ? gs[j] : g19[j + 10];
+      i32 f = (i & 1) ? f2[i] : F.v[i];
+      a[c] = mac( f, g, a[c] );
+    }
+  }
+  i64 E[5], O[5];
+  _Pragma("unroll") for( int c=0; c<5; c++ ) {
+    u32 lo = (u32)a[c], hi = (u32)((u64)a[c] >> 32);
+    E[c] = (i64)(((u64)half_from_lo( hi ) << 32) | half_from_lo( lo ));
+    O[c] = (i64)(((u64)half_from_hi( hi ) << 32) | half_from_hi( lo ));
+  }
+  return fe_carry_b( E[0], O[0], E[1], O[1], E[2], O[2], E[3], O[3], E[4], O[4] );
+}
+
+__device__ __forceinline__ fe
+quad8_p3_ownc( fe const & C, half_t const & H ) {
+  fe a, b;
+  _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = qp<0,0,2,2>( C.v[k] ); b.v[k] = qp<1,3,1,3>( C.v[k] ); }
+  return fe_mul_half( a, b, H );
+}
+
+__device__ __forceinline__ void
+quad8_body_ownc( fe & C, fe const & pm, fe const & qrow, bool isD, bool neg, u64 mD, int qd, half_t const & H ) {
+  /* operand a = c1*P1 + c2*P2 with P1 = quad_perm(2,2,2,0) -> X X X Z and
+     P2 = quad_perm(1,1,0,3) -> Y Y Z T:  DBL a = [X+Y, Y, X, Z],
+     ADD a = [X+Y, Y-X, Z, T];  b = DBL ? a << (q==3) : qrow */
+  i32 c1 = (qd == 0) ? 1 : (qd == 1) ? (isD ? 0 : -1) : (isD ? 1 : 0);
+  i32 c2 = (qd <= 1 || !isD) ? 1 : 0;
+  i32 sh = (qd == 3) ? 1 : 0;
+  asm( "" : "+v"(c1), "+v"(c2) );
+  fe a, b;
+  _Pragma("unroll") for( int k=0; k<10; k++ ) {
+    i32 av = lin2( c1, qp<2,2,2,0>( pm.v[k] ), c2, qp<1,1,0,3>( pm.v[k] ) );
+    a.v[k] = av;
+    b.v[k] = vsel( mD, (i32)((u32)av << sh), qrow.v[k] );
+  }
+  fe m = fe_mul_half( a, b, H );
+  i32 s0 = neg ? -1 : 1;
+  i32 x = isD ? (qd == 1 ? -1 : (qd == 3 ? 0 : 1)) : (qd >= 2 ? 1 : 0);
+  i32 y = isD ? ((qd & 1) ? 1 : -1)               : (qd <= 1 ? 2 : (qd == 2 ? -1 : 1));
+  i32 z = isD ? (qd == 0 ? 0 : (qd == 2 ? -1 : 1)) : (qd == 0 ? s0 : (qd == 1 ? -s0 : 0));
+  asm( "" : "+v"(x), "+v"(y), "+v"(z) );   /* opaque: keep full v_mad_i64_i32 (no small-range rewrites) */
+  _Pragma("unroll") for( int k=0; k<10; k++ )
+    C.v[k] = lin3( x, qp<1,1,0,0>( m.v[k] ), y, qp<2,2,1,1>( m.v[k] ), z, qp<3,3,2,2>( m.v[k] ) );
+}
+
+
+__global__ void __launch_bounds__(64)
+k_dsm8( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats ) {
+  __shared__ i32 bi[8][40];
+  for( int k=threadIdx.x; k<8*40; k+=64 ) {
+    int e = k / 40, c = (k % 40) / 10, l = k % 10;
+    i32 v;
+    if( c == 0 ) v = (l == 0);
+    else if( c == 1 ) v = BI_TABLE[e][1][l];
+    else if( c == 2 ) v = BI_TABLE[e][0][l];
+    else v = BI_TABLE[e][2][l];
+    bi[e][c*10 + l] = v;
+  }
+  __syncthreads();
+
+  u32 gt = blockIdx.x * 64u + threadIdx.x;
+  u32 i = gt >> 3;
+  int qd = (int)(threadIdx.x & 3u);
+  int hh = (int)((threadIdx.x >> 2) & 1u);            /* which half of every field mul this lane computes */
+  bool act = (i < n) && (err[i] == 1);
+  if( act && (ws[L.ds + 2u*i] | ws[L.ds + 2u*i + 1u]) ) {            /* A or R undecodable */
+    act = false;
+    if( qd == 0 && !hh ) err[i] = (i8)-2;
+  }
+  size_t N = L.N;
+  u32 ii = (i < n) ? i : 0u;
+  i32 * Ail = (i32 *)(ws + L.Ai) + (size_t)ii*384u;
+  u64 const m1 = __builtin_amdgcn_ballot_w64( qd & 1 ), m2 = __builtin_amdgcn_ballot_w64( qd & 2 );
+  half_t const H = half_ctx( hh );
+
+  /* -A and its odd multiples (cached rows; lane q writes row q) */
+  {
+    p3 A;
+    i32 const * Aw = (i32 const *)(ws + L.A);
+    _Pragma("unroll") for( int k=0; k<10; k++ ) {
+      A.X.v[k] = act ? Aw[(size_t)(k   )*N + ii] : 0;
+      A.Y.v[k] = act ? Aw[(size_t)(10+k)*N + ii] : (k==0);
+      A.T.v[k] = act ? Aw[(size_t)(20+k)*N + ii] : 0;
+      A.Z.v[k] = (k==0);
+    }
+    fe row = quad_cached_row( A, m1, m2 );
+#   define AI_ROW4( e ) do {                                                        \
+      int4 * d_ = (int4 *)(Ail + (e)*48 + qd*12);                                   \
+      d_[0] = make_int4( row.v[0], row.v[1], row.v[2], row.v[3] );                 \
+      d_[1] = make_int4( row.v[4], row.v[5], row.v[6], row.v[7] );                 \
+      d_[2] = make_int4( row.v[8], row.v[9], 0, 0 );                               \
+    } while(0)
+    if( act && !hh ) AI_ROW4( 0 );
+    u64 const all = ~0UL, none = 0UL;
+    p1p1 t; fe z0 = fe_zero();
+    quad_body( t, A, z0, all, none, m1, m2 );            /* DBL(A) */
+    p3 A2; quad_p3( A2, t, m1, m2 );
+    for( int e=0; e<7; e++ ) {
+      fe R0, R1, R2, R3;
+      qgather( row, R0, R1, R2, R3 );                    /* rows Z, Y-X, Y+X, 2dT of entry e */
+      fe br;
+      _Pragma("unroll") for( int k=0; k<10; k++ ) br.v[k] = q4( m1, m2, R2.v[k], R1.v[k], R0.v[k], R3.v[k] );
+      quad_body( t, A2, br, none, none, m1, m2 );        /* A2 + Ai[e] */
+      p3 u; quad_p3( u, t, m1, m2 );
+      row = quad_cached_row( u, m1, m2 );
+      if( act && !hh ) AI_ROW4( e+1 );
+    }
+#   undef AI_ROW4
+  }
+
+  u64 const * dg = (u64 const *)(ws + L.dig) + (size_t)ii*32u;
+  int p   = act ? ((int const *)(ws + L.top))[ii] : -1;
+  int ph  = act ? (p >= 0 ? PH_DBL : PH_FIN) : PH_DONE;
+  evq eva, evb;                                      /* digit events of h and s */
+  {
+    __shared__ u64 evl[8][33];                       /* one row per signature of the wave */
+    u64 * row = evl[threadIdx.x >> 3];
+    u32 ne = act ? ((u32 const *)(ws + L.evn))[ii] : 0u;
+    u32 wa = ((ne & 0xffu) + 3u) >> 2, wb = (((ne >> 8) & 0xffu) + 3u) >> 2;
+    for( u32 k=threadIdx.x & 7u; k<wa; k+=8u ) row[k]       = dg[k];   /* the 8 lanes copy the row together */
+    for( u32 k=threadIdx.x & 7u; k<wb; k+=8u ) row[16u + k] = dg[16u + k];
+    __syncthreads();
+    eva.init( (u16 const *)row,        (int)(ne & 0xffu) );
+    evb.init( (u16 const *)(row + 16), (int)((ne >> 8) & 0xffu) );
+  }
+  i32 const * Rw = (i32 const *)(ws + L.R);
+  u32 nha = 0, nhb = 0;
+  u32 nit = (u32)(p + 1);
+  bool qneg = false;
+  fe qrow = fe_zero();
+  fe C = (qd == 2) ? fe_zero() : fe_one();   /* identity: own coordinate (Z, T, X, Y)[q] = (1, 1, 0, 1) */
+
+  for( ;; ) {
+    fe pm = quad8_p3_ownc( C, H );              /* q0 u.Z, q1 u.Y, q2 u.X, q3 u.T */
+
+    bool fin = (ph == PH_FIN);
+    /* each lane parks its own p1p1->p3 product in its row of entry 0 of the
+       signature's Ai table (no ADD op reads it any more); the compare runs
+       once after the loop */
+    if( __any( fin ) ) {
+      if( fin ) {
+        int4 * d_ = (int4 *)(Ail + qd*12);
+        d_[0] = make_int4( pm.v[0], pm.v[1], pm.v[2], pm.v[3] );
+        d_[1] = make_int4( pm.v[4], pm.v[5], pm.v[6], pm.v[7] );
+        d_[2] = make_int4( pm.v[8], pm.v[9], 0, 0 );
+        ph = PH_DONE;
+      }
+    }
+    if( __all( ph == PH_DONE ) ) break;
+
+    bool isD = (ph == PH_DBL);
+    u64 mD = __builtin_amdgcn_ballot_w64( isD );
+    quad8_body_ownc( C, pm, qrow, isD, qneg, mD, qd, H );
+
+    /* the event just executed is consumed; the next op follows from the
+       event heads (an event at position p means a digit at p) */
+    if( ph == PH_ADDA ) eva.pop();
+    else if( ph == PH_ADDB ) evb.pop();
+    bool ha = eva.pos == p, hb = evb.pos == p;
+    int da = eva.dig, db = evb.dig;
+    int nph;
+    if( ph == PH_DBL )       nph = ha ? PH_ADDA : (hb ? PH_ADDB : -1);
+    else if( ph == PH_ADDA ) nph = hb ? PH_ADDB : -1;
+    else if( ph == PH_ADDB ) nph = -1;
+    else                     nph = PH_DONE;
+    if( nph == -1 ) {
+      p--;
+      nph = (p < 0) ? PH_FIN : PH_DBL;
+    }
+    ph = nph;
+
+    /* this lane's row of the next op's operand: q0 qP, q1 qM, q2 qZ, q3 qT;
+       rows of an entry are [Z, Y-X, Y+X, 2dT], a negative digit swaps Y-X/Y+X */
+    if( ph == PH_ADDA || ph == PH_ADDB ) {
+      int d = (ph == PH_ADDA) ? da : db;
+      int e = (d < 0 ? -d : d) >> 1;
+      qneg = d < 0;
+      int row = (qd == 0) ? (qneg ? 1 : 2) : (qd == 1) ? (qneg ? 2 : 1) : (qd == 2) ? 0 : 3;
+      if( ph == PH_ADDA ) {
+        nha++;
+        int4 const * src = (int4 const *)(Ail + e*48 + row*12);
+        int4 x0 = src[0], x1 = src[1], x2 = src[2];
+        qrow.v[0] = x0.x; qrow.v[1] = x0.y; qrow.v[2] = x0.z; qrow.v[3] = x0.w;
+        qrow.v[4] = x1.x; qrow.v[5] = x1.y; qrow.v[6] = x1.z; qrow.v[7] = x1.w;
+        qrow.v[8] = x2.x; qrow.v[9] = x2.y;
+      } else {
+        nhb++;
+        _Pragma("unroll") for( int k=0; k<10; k++ ) qrow.v[k] = bi[e][row*10 + k];
+      }
+    }
+  }
+
+  /* the limb compare (fd_ed25519_user.c:417-425), once per wave, all lanes
+     converged: q0 Z*RX vs X, q1 Z*RY vs Y, quad AND */
+  {
+    fe pm;
+    int4 const * s_ = (int4 const *)(Ail + qd*12);
+    int4 x0 = s_[0], x1 = s_[1], x2 = s_[2];
+    pm.v[0] = x0.x; pm.v[1] = x0.y; pm.v[2] = x0.z; pm.v[3] = x0.w;
+    pm.v[4] = x1.x; pm.v[5] = x1.y; pm.v[6] = x1.z; pm.v[7] = x1.w;
+    pm.v[8] = x2.x; pm.v[9] = x2.y;
+    _Pragma("unroll") for( int k=0; k<10; k++ ) qrow.v[k] = Rw[(size_t)((qd & 1)*10 + k)*N + ii];
+    fe Z, ref;
+    _Pragma("unroll") for( int k=0; k<10; k++ ) {
+      Z.v[k] = qb<0>( pm.v[k] );
+      ref.v[k] = qp<2,1,2,1>( pm.v[k] );    /* q0 <- X (lane 2), q1 <- Y (own) */
+    }
+    fe xz = fe_mul_fold1( Z, qrow );
+    bool eq = true;
+    _Pragma("unroll") for( int k=0; k<8; k++ ) eq = eq && (xz.v[k] == ref.v[k]);
+    int e01 = (int)eq;
+    int both = qb<0>( e01 ) & qb<1>( e01 );
+    if( act && qd == 0 && !hh ) err[i] = (i8)(both ? 0 : -3);
+  }
+
+  if( want_stats && i < n && qd == 0 && !hh ) {
+    u32 * st = (u32 *)(ws + L.st);
+    st[i] = act ? nit : 0u; st[N + i] = act ? nha : 0u; st[2*N + i] = act ? nhb : 0u;
+  }
+}
+
+/* ------------------------------------------------------------------ */
 /* k_tile_gather: the streaming tile's staging.  Frag i (fsz[i] bytes at
    chunk ichunk[i] of `src`, host memory mapped into the GPU: the input
    dcache in zero-copy mode, the tile's own output dcache in copy mode) is
@@ -1092,18 +1359,32 @@ fd_amd_launch_copy_out( void * d_dst, void const * d_src, size_t n, hipStream_t 
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-/* Batches up to this size use k_dsm4 (fd_ed25519_amd_set_small_batch_max). */
+/* Kernel choice by batch size: up to g_dsm8_max signatures k_dsm8 (8 lanes
+   per signature: the shortest op stream, but twice k_dsm4's waves), up to
+   g_dsm4_max k_dsm4, larger batches k_dsm.  Measured (profiles/
+   r02_k_dsm4_latency_experiments.txt): k_dsm8 is faster while its waves fit
+   one per SIMD (n <= 8192 on 1024 SIMDs), slower beyond. */
 static volatile u32 g_dsm4_max = 16384u;
-static u32 fd_amd_dsm4_max( void ) { return g_dsm4_max; }
+static volatile u32 g_dsm8_max = 8192u;
 
 extern "C" void
 fd_ed25519_amd_set_small_batch_max( unsigned long n ) {
   g_dsm4_max = n > 0xFFFFFFFFUL ? 0xFFFFFFFFu : (u32)n;
 }
 
+extern "C" void
+fd_ed25519_amd_set_latency_batch_max( unsigned long n ) {
+  g_dsm8_max = n > 0xFFFFFFFFUL ? 0xFFFFFFFFu : (u32)n;
+}
+
+int
+fd_amd_batch_dsm_mode( uint32_t n ) {
+  return n <= g_dsm4_max ? 2 : 1;
+}
+
 int
 fd_amd_uses_latency_path( uint32_t n, int dsm_mode ) {
-  return dsm_mode == 2 || (dsm_mode == 0 && n <= fd_amd_dsm4_max());
+  return dsm_mode >= 2 || (dsm_mode == 0 && (n <= g_dsm4_max || n <= g_dsm8_max));
 }
 
 int
@@ -1115,11 +1396,13 @@ fd_amd_launch_verify( u32 n, u8 const * d_pub, u8 const * d_sig, u32 const * d_o
   u8 * ws = (u8 *)d_ws;
   u32 nb = (n + 63u) / 64u;
   bool small = fd_amd_uses_latency_path( n, dsm_mode );
+  bool eight = dsm_mode == 3 || (dsm_mode == 0 && n <= g_dsm8_max);
   if( ev ) (void)hipEventRecord( ev[0], stream );
-  if( small ) {   /* latency path: one front launch (hash || decompress), then k_dsm4 */
+  if( small ) {   /* latency path: one front launch (hash || decompress), then k_dsm8 or k_dsm4 */
     hipLaunchKernelGGL( k_front, dim3(3u*nb), dim3(64), 0, stream, n, nb, d_pub, d_sig, d_off, d_sz, d_blob, d_err, ws, L, d_skip );
     if( ev ) { (void)hipEventRecord( ev[1], stream ); (void)hipEventRecord( ev[2], stream ); }
-    hipLaunchKernelGGL( k_dsm4, dim3((n + 15u)/16u), dim3(64), 0, stream, n, d_err, ws, L, want_stats );
+    if( eight ) hipLaunchKernelGGL( k_dsm8, dim3((n + 7u)/8u), dim3(64), 0, stream, n, d_err, ws, L, want_stats );
+    else        hipLaunchKernelGGL( k_dsm4, dim3((n + 15u)/16u), dim3(64), 0, stream, n, d_err, ws, L, want_stats );
   } else {
     hipLaunchKernelGGL( k_prep,   dim3(nb),    dim3(64), 0, stream, n, d_pub, d_sig, d_off, d_sz, d_blob, d_err, ws, L, d_skip );
     if( ev ) (void)hipEventRecord( ev[1], stream );

@@ -293,14 +293,16 @@ tile_launch( fd_verify_amd_tile_t * t, int k, ulong n, bool txn, uint8_t const *
      switching batches of >= 4096/8192 to the 1-lane kernel while others were
      in flight lowered the saturated rate at every batch_max and doubled
      latency; the in-flight work (4 x batch_max) is too small for the 1-lane
-     kernel to fill the GPU. */
+     kernel to fill the GPU.  Not the 8-lane k_dsm8 either: with 4 batches in
+     flight its doubled wave count oversubscribes the SIMDs. */
+  int mode = fd_amd_batch_dsm_mode( (uint32_t)(txn ? ts.nsig : n) );
   if( txn ) {
     ulong nsig = ts.nsig;
     if( fd_amd_launch_txn_parse( (uint32_t)n, ts.d_mir, s->d_toff, s->d_tsz, s->d_fp, NULL, 0, m_tbase,
                                  s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_skip, s->stream ) )
       return FD_ED25519_AMD_ERR_DEVICE;
     if( nsig && fd_amd_launch_verify( (uint32_t)nsig, s->d_pub, s->d_sig, s->d_off, s->d_sz, ts.d_mir, s->d_err,
-                                      s->d_ws, s->stream, 0, NULL, s->d_skip, 0 ) )
+                                      s->d_ws, s->stream, 0, NULL, s->d_skip, mode ) )
       return FD_ED25519_AMD_ERR_DEVICE;
     if( fd_amd_launch_txn_reduce( (uint32_t)n, s->d_fp, m_tbase, s->d_err, s->d_terr, s->stream ) )
       return FD_ED25519_AMD_ERR_DEVICE;
@@ -311,7 +313,7 @@ tile_launch( fd_verify_amd_tile_t * t, int k, ulong n, bool txn, uint8_t const *
     }
   } else {
     if( fd_amd_launch_verify( (uint32_t)n, s->d_pub, s->d_sig, s->d_off, s->d_sz, ts.d_mir, s->d_err, s->d_ws,
-                              s->stream, 1, NULL, NULL, 0 ) )
+                              s->stream, 1, NULL, NULL, mode ) )
       return FD_ED25519_AMD_ERR_DEVICE;
     if( fd_amd_slot_out( s, s->h_err, s->d_err, n ) ) return FD_ED25519_AMD_ERR_DEVICE;
     ws_layout_t L = fd_amd_ws_layout( n );

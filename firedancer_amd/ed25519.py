@@ -78,6 +78,8 @@ def lib():
     L.fd_ed25519_amd_sign_dev.restype = i
     L.fd_ed25519_amd_set_small_batch_max.argtypes = [ul]
     L.fd_ed25519_amd_set_small_batch_max.restype = None
+    L.fd_ed25519_amd_set_latency_batch_max.argtypes = [ul]
+    L.fd_ed25519_amd_set_latency_batch_max.restype = None
     L.fd_verify_amd_tile_new.argtypes = [i, ul, ul, ul, ul]
     L.fd_verify_amd_tile_new.restype = vp
     L.fd_verify_amd_tile_out_chunk0.argtypes = [vp]
@@ -443,7 +445,23 @@ def set_small_batch_max(n):
     lib().fd_ed25519_amd_set_small_batch_max(int(n))
 
 
+def set_latency_batch_max(n):
+    """Batches of at most n signatures use the 8-lane latency kernel (k_dsm8)."""
+    lib().fd_ed25519_amd_set_latency_batch_max(int(n))
+
+
+def select_dsm_kernel(name):
+    """Force one double-scalar-mult kernel for every batch size (tests):
+    'k_dsm', 'k_dsm4', 'k_dsm8'; 'default' restores the size rule."""
+    big = 1 << 32
+    small, lat = {"k_dsm": (0, 0), "k_dsm4": (big, 0), "k_dsm8": (big, big),
+                  "default": (SMALL_BATCH_MAX_DEFAULT, LATENCY_BATCH_MAX_DEFAULT)}[name]
+    set_small_batch_max(small)
+    set_latency_batch_max(lat)
+
+
 SMALL_BATCH_MAX_DEFAULT = 16384
+LATENCY_BATCH_MAX_DEFAULT = 8192
 FD_TXN_AMD_ERR_PARSE = -4
 FD_TXN_MAX_SZ = 3570
 

@@ -290,13 +290,19 @@ fd_ed25519_amd_sign_dev( ulong         n,
                          uchar *       d_sig,
                          void *        stream );
 
-/* Kernel choice for the double-scalar multiply.  Batches of at most n
-   signatures (default 16384) run the latency kernel (four lanes per
-   signature, k_dsm4); larger ones the throughput kernel (one lane per
-   signature, k_dsm).  Both give identical verdicts; 0 disables the
-   latency kernel.  Process-wide. */
+/* Kernel choice for the double-scalar multiply, by batch size.  Batches
+   of at most fd_ed25519_amd_set_latency_batch_max signatures (default 8192)
+   run k_dsm8 (eight lanes per signature: the shortest per-batch latency
+   while its waves fit one per SIMD); batches of at most
+   fd_ed25519_amd_set_small_batch_max (default 16384) run k_dsm4 (four lanes
+   per signature); larger ones the throughput kernel k_dsm (one lane per
+   signature).  All give identical verdicts; 0 disables a kernel.
+   Process-wide. */
 void
 fd_ed25519_amd_set_small_batch_max( ulong n );
+
+void
+fd_ed25519_amd_set_latency_batch_max( ulong n );
 
 /* Library version / build string. */
 char const *

@@ -232,13 +232,14 @@ def test_prep_digits_vs_python(golden):
         assert tp[j] == (max(nz) if nz else -1)
 
 
-@pytest.fixture(params=["k_dsm", "k_dsm4"])
+@pytest.fixture(params=["k_dsm", "k_dsm4", "k_dsm8"])
 def dsm_kernel(request):
-    """Run a test once per double-scalar-mult kernel (throughput / latency)."""
+    """Run a test once per double-scalar-mult kernel (throughput, 4-lane and
+    8-lane latency kernels), each forced for every batch size."""
     from firedancer_amd import ed25519
-    ed25519.set_small_batch_max(0 if request.param == "k_dsm" else 1 << 20)
+    ed25519.select_dsm_kernel(request.param)
     yield request.param
-    ed25519.set_small_batch_max(ed25519.SMALL_BATCH_MAX_DEFAULT)
+    ed25519.select_dsm_kernel("default")
 
 
 def test_both_kernels_golden_and_mixed(engine, golden, dsm_kernel):

@@ -9,7 +9,7 @@ sys.path.insert(0, os.getcwd())
 import numpy as np  # noqa: E402
 from firedancer_amd import ed25519, hip, workload  # noqa: E402
 
-ed25519.set_small_batch_max(1 << 22)
+ed25519.select_dsm_kernel(os.environ.get("FD_DSM_KERNEL", "k_dsm4"))
 for n in (1024, 4096, 16384, 32768, 65536, 131072):
     pub, sig, off, sz, blob = workload.sig_batch(n, 200, 5)
     d = {k: hip.DeviceBuffer.from_array(v) for k, v in dict(pub=pub, sig=sig, off=off, sz=sz, blob=blob).items()}

@@ -3,8 +3,8 @@ of oracle/PARITY_LOG.md (regenerated draw for draw from oracle/vecgen.h,
 signed on the GPU -- byte-identical to the reference signer -- and given the
 same 10 % single-bit flips).  Every verdict is compared with the oracle run on
 the box's host cores, and each stream's code histogram with the reference's
-histogram recorded in PARITY_LOG.md.  Odd streams force the latency kernel
-(k_dsm4) for every chunk, even streams run the throughput kernel (k_dsm).
+histogram recorded in PARITY_LOG.md.  Stream k forces kernel k % 3 (k_dsm,
+k_dsm4, k_dsm8) for every chunk.
 
 usage: python tools/gpu_sweep.py [stream indices...] > gpurun_out/sweep.jsonl
 """
@@ -43,8 +43,8 @@ def run(k):
     prv, blob, _, sz, fk, fp = _oracle.stream_inputs(rs, N, szlo, szhi, True)
     off64 = np.zeros(N, np.int64)
     off64[1:] = np.cumsum(sz[:-1], dtype=np.int64)      # the generator's u32 offsets wrap past 4 GB
-    dsm4 = bool(k & 1)
-    ed25519.set_small_batch_max((1 << 21) if dsm4 else ed25519.SMALL_BATCH_MAX_DEFAULT)
+    kern = ("k_dsm", "k_dsm4", "k_dsm8")[k % 3]
+    ed25519.select_dsm_kernel(kern)
     eng = ed25519.Engine(device=0, batch_max=1 << 20, blob_max=(1 << 20) * max(szhi, 1))
     err = np.zeros(N, np.int8)
     exp = np.zeros(N, np.int8)
@@ -71,12 +71,12 @@ def run(k):
         t_cpu += time.time() - t2
         print("  stream %d: %d/%d" % (seed, c1, N), file=sys.stderr, flush=True)
     eng.close()
-    ed25519.set_small_batch_max(ed25519.SMALL_BATCH_MAX_DEFAULT)
+    ed25519.select_dsm_kernel("default")
     hist = tuple(int((err == -c).sum()) for c in range(4))
     bad = np.nonzero(err != exp)[0]
     false_rej = int(((fk == 0) & (err == -3)).sum())
     return {"seed": seed, "szlo": szlo, "szhi": szhi, "signatures": N,
-            "kernel": "k_dsm4" if dsm4 else "k_dsm", "mismatches_vs_oracle": int(bad.size),
+            "kernel": kern, "mismatches_vs_oracle": int(bad.size),
             "first_mismatches": [int(i) for i in bad[:5]], "hist": hist,
             "hist_equals_reference": hist == ref_hist, "false_rejects": false_rej,
             "total_s": round(time.time() - t0, 1), "gpu_verify_s": round(t_gpu, 2), "oracle_s": round(t_cpu, 1)}
