@@ -195,7 +195,7 @@ def dsm_roofline(st, kernel_ms, n, kernel="k_dsm", note=None):
     achieved = mac / (kernel_ms * 1e-3) / 1e12
     r = {"bound": "valu-imad64", "kernel": kernel, "achieved": achieved, "peak": PEAK_TMAC, "unit": "TMAC/s",
          "frac": achieved / PEAK_TMAC, "traffic": pmc_traffic("k_dsm", n),
-         "traffic_note": "HBM bytes per launch from the committed PMC pass (profiles/r01_pmc_latest.json: "
+         "traffic_note": "HBM bytes per launch from the committed PMC pass (profiles/r02_pmc_latest.json: "
                          "2*FETCH_SIZE+WRITE_SIZE KB, gfx950 correction), scaled to this batch",
          "mac_per_sig": mac / max(live, 1.0)}
     if note:
@@ -207,7 +207,9 @@ def pmc_traffic(kernel, n):
     """HBM bytes per launch of `kernel` at batch n, from the PMC summary
     committed under profiles/ (tools/prof_pmc.sh + tools/pmc_summary.py on
     the same build), scaled linearly from the profiled batch size."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_latest.json")
+    path = os.path.join(ROOT, "profiles", "r02_pmc_latest.json")
+    if not os.path.exists(path):
+        path = os.path.join(ROOT, "profiles", "r01_pmc_latest.json")
     try:
         d = json.load(open(path))
         b = d[kernel]["derived"]["hbm_bytes_per_launch"]
