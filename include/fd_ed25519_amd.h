@@ -184,7 +184,9 @@ fd_ed25519_amd_verify_soa_registered( fd_ed25519_amd_t * eng,
    its device, its verdicts device -> host.  The reference scales the same
    way, as N independent verify tiles each with its own input
    (src/app/frank/fd_frank_init:67-80).  batch_max / blob_max are per
-   engine.  NULL on failure (any device unusable). */
+   engine.  One call at a time per multi engine (its worker threads serve
+   one batch at a time); independent multi engines may run concurrently.
+   NULL on failure (any device unusable). */
 typedef struct fd_ed25519_amd_multi fd_ed25519_amd_multi_t;
 
 fd_ed25519_amd_multi_t *
