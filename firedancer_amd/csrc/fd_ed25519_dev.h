@@ -319,6 +319,52 @@ FD_DEV fe fe_sq_fold( fe const & F ) {
 
 FD_DEV fe fe_sq( fe const & f ) { return fe_sq_fold( f ); }
 
+/* Term (i, j = K-i mod 10), i <= j, of column K of a square: the pair's
+   coefficient is 2 (i != j) x 2 (i, j both odd) x 19 (i + j >= 10) x 2 (D2,
+   the reference's sq2), its power of two applied to f_i as a shift, the 19
+   taken from f19[j] (j >= 5 whenever i + j >= 10).  For |f| <= 2^26 no
+   operand wraps (f << 3 <= 2^29, 19 f <= 2^30.25), so the column sums are
+   the exact integers sum_{i+j=K} c_ij f_i f_j -- the sums of fe_mul( f, f )
+   (resp. fe_mul( f, f+f )) -- and the carry gives the same limbs. */
+template<int K, bool D2>
+FD_DEV void sq_term( int i, i32 const * f, i32 const * f19, i64 & a ) {
+  int const j = (K - i + 10) % 10;
+  if( i > j ) return;
+  int const c2 = (i != j) + ((i & 1) && (j & 1)) + (D2 ? 1 : 0);
+  bool const x19 = (i + j) >= 10;
+  i32 const lhs = c2 ? (i32)((u32)f[i] << c2) : f[i];
+  a = mac( lhs, x19 ? f19[j] : f[j], a );
+}
+
+/* Two squares (55 products each) with fe_mul_fold2w's column order and
+   carry fold.  D2: the column sums of f * (f + f) (the AVX sq2). */
+template<bool D2A, bool D2B>
+FD_DEV void fe_sq_fold2w( fe & R1, fe const & F1, fe & R2, fe const & F2 ) {
+  i64 const kb = fd_opaque( (1L<<25) + (1L<<50) );
+  i32 f1_19[10], f2_19[10];
+  _Pragma("unroll") for( int k=0; k<10; k++ ) { f1_19[k] = wmul( F1.v[k], 19 ); f2_19[k] = wmul( F2.v[k], 19 ); }
+  i32 const * f1 = F1.v; i32 const * f2 = F2.v;
+# define FD_SA( K_, A_ ) sq_term<K_, D2A>( i, f1, f1_19, A_ )
+# define FD_SB( K_, B_ ) sq_term<K_, D2B>( i, f2, f2_19, B_ )
+  i64 a0 = kb, b0 = kb, a4 = kb, b4 = kb, a2 = kb, b2 = kb, a6 = kb, b6 = kb, a8 = kb, b8 = kb;
+  _Pragma("unroll") for( int i=0; i<10; i++ ) {
+    FD_SA( 0, a0 ); FD_SB( 0, b0 ); FD_SA( 4, a4 ); FD_SB( 4, b4 ); FD_SA( 2, a2 ); FD_SB( 2, b2 );
+    FD_SA( 6, a6 ); FD_SB( 6, b6 ); FD_SA( 8, a8 ); FD_SB( 8, b8 );
+  }
+  i64 a1 = a0 >> 26, b1 = b0 >> 26, a5 = a4 >> 26, b5 = b4 >> 26;
+  _Pragma("unroll") for( int i=0; i<10; i++ ) { FD_SA( 1, a1 ); FD_SB( 1, b1 ); FD_SA( 5, a5 ); FD_SB( 5, b5 ); }
+  a2 += a1 >> 25; b2 += b1 >> 25; a6 += a5 >> 25; b6 += b5 >> 25;
+  i64 a3 = a2 >> 26, b3 = b2 >> 26, a7 = a6 >> 26, b7 = b6 >> 26;
+  _Pragma("unroll") for( int i=0; i<10; i++ ) { FD_SA( 3, a3 ); FD_SB( 3, b3 ); FD_SA( 7, a7 ); FD_SB( 7, b7 ); }
+  a8 += a7 >> 25; b8 += b7 >> 25;
+  i64 a9 = a8 >> 26, b9 = b8 >> 26;
+  _Pragma("unroll") for( int i=0; i<10; i++ ) { FD_SA( 9, a9 ); FD_SB( 9, b9 ); }
+# undef FD_SA
+# undef FD_SB
+  R1 = fe_carry_fold_out( a0, a1, a2, a3, a4, a5, a6, a7, a8, a9 );
+  R2 = fe_carry_fold_out( b0, b1, b2, b3, b4, b5, b6, b7, b8, b9 );
+}
+
 FD_DEV fe fe_sq_iter( fe h, int n ) {
   _Pragma("unroll 1")
   for( int i=0; i<n; i++ ) h = fe_sq( h );

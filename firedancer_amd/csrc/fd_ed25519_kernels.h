@@ -9,7 +9,7 @@
 
 typedef struct {
   size_t N;      /* n rounded up to 64 */
-  size_t dig, evn, top, A, R, Ai, st, tag, ds;   /* byte offsets of the workspace planes */
+  size_t dig, evn, top, A, R, Ai, st, tag, ds, init, ctr;   /* byte offsets of the workspace planes */
   size_t total;  /* footprint in bytes */
 } ws_layout_t;
 

@@ -39,6 +39,7 @@
 
 #include "fd_ed25519_dev.h"
 #include "fd_ed25519_kernels.h"
+#include <stdlib.h>
 
 typedef int8_t i8;
 typedef uint16_t u16;
@@ -63,6 +64,8 @@ fd_amd_ws_layout( size_t n ) {
   L.st  = o; o = ws_al( o + 4UL*3UL*N );
   L.tag = o; o = ws_al( o + 8UL*N );
   L.ds  = o; o = ws_al( o + 2UL*N );
+  L.init = o; o = ws_al( o + 16UL*N );        /* uint4 [N]: k_dsmp op-stream start (k_ai) */
+  L.ctr  = o; o = ws_al( o + 4UL );            /* u32: k_dsmp work counter (zeroed by k_ai) */
   L.total = o;
   return L;
 }
@@ -433,9 +436,9 @@ struct evq {
  * takes one more step (PH_FIN): its p1p1->p2 result is R', compared with
  * the limb memcmp of fd_ed25519_user.c:417-425, then it idles (PH_DONE).
  */
-__global__ void __launch_bounds__(64)
-k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats ) {
-  __shared__ i32 bi[8][40];
+__device__ __forceinline__ void
+dsm_lane_body( u32 i, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats,
+               i32 (* __restrict__ bi)[40], u64 (* __restrict__ evl)[33] ) {
   for( int k=threadIdx.x; k<8*40; k+=64 ) {
     int e = k / 40, c = (k % 40) / 10, l = k % 10;
     i32 v;
@@ -447,7 +450,6 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
   }
   __syncthreads();
 
-  u32 i = blockIdx.x * 64u + threadIdx.x;
   bool act = (i < n) && (err[i] == 1);
   if( act && (ws[L.ds + 2u*i] | ws[L.ds + 2u*i + 1u]) ) { err[i] = (i8)-2; act = false; }   /* A or R undecodable */
   size_t N = L.N;
@@ -492,8 +494,7 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
   int ph  = act ? (p >= 0 ? PH_DBL : PH_FIN) : PH_DONE;
   evq eva, evb;                                      /* digit events of h and s */
   {
-    __shared__ u64 evl[64][33];                      /* this wave's event rows (33: bank spread) */
-    u64 * row = evl[threadIdx.x];
+    u64 * row = evl[threadIdx.x];                    /* this wave's event rows (33: bank spread) */
     u32 ne = act ? ((u32 const *)(ws + L.evn))[ii] : 0u;
     u32 wa = ((ne & 0xffu) + 3u) >> 2, wb = (((ne >> 8) & 0xffu) + 3u) >> 2;
     for( u32 k=0; k<wa; k++ ) row[k]       = dg[k];
@@ -658,6 +659,13 @@ k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
     u32 * st = (u32 *)(ws + L.st);
     st[i] = act ? nit : 0u; st[N + i] = act ? nha : 0u; st[2*N + i] = act ? nhb : 0u;
   }
+}
+
+__global__ void __launch_bounds__(64)
+k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats ) {
+  __shared__ i32 bi[8][40];
+  __shared__ u64 evl[64][33];
+  dsm_lane_body( blockIdx.x * 64u + threadIdx.x, n, err, ws, L, want_stats, bi, evl );
 }
 
 /* ------------------------------------------------------------------ */
@@ -1252,6 +1260,408 @@ k_dsm8( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
 }
 
 /* ------------------------------------------------------------------ */
+/* Pooled DSM for large batches: k_ai -> k_dsmp -> k_fin.
+ *
+ * k_dsm runs every op of a signature's stream (DBL / ADD-A / ADD-B, see
+ * above) as the same 8-mul step, so a lane that doubles while its
+ * neighbours add still computes general products: each step pays for
+ * p1p1->p3 (4 muls) + 4 general muls + per-lane operand selects.  In the
+ * reference's own flow (avx/fd_ed25519_ge.c:488-523) a doubling costs
+ * p1p1->p2 (3 muls) + 4 squares (55 products each, not 100), and DBLs are
+ * about three quarters of the stream.  k_dsmp keeps a POOL of FD_POOL_P
+ * signatures per wave in LDS (their p1p1 state and op-stream cursor) and,
+ * every step, runs 64 of them that want the SAME op class: a DBL step
+ * (p2 + 4 squares) or an ADD step (p3 + 4 muls; ADD-A and ADD-B differ only
+ * in where the table operand comes from).  With P >= 128 a full class
+ * always exists (nA < 64 => nD > 64); at P = 112 nearly always.  Same field
+ * ops as the reference, in the same order per signature: identical limbs.
+ *
+ *   k_ai    one lane per signature: k_dsm's activity check (-2 on an
+ *           undecodable point) and Ai table of odd multiples of -A, plus
+ *           the op-stream start init[i] = { -, heads, p|ja<<16|jb<<24, op }
+ *           (heads: the top remaining h / s digit events, 0xffff = none).
+ *   k_dsmp  one wave per workgroup, gridDim.x waves; waves claim
+ *           signatures for their free pool slots from a shared counter.  A
+ *           finished signature parks its final p1p1 in its own Ai slab.
+ *   k_fin   one lane per signature: p1p1 -> p2 and the limb compare of
+ *           fd_ed25519_user.c:417-425; work statistics.
+ */
+#ifndef FD_POOL_P
+#define FD_POOL_P 112
+#endif
+enum { OP_D = 0, OP_AA = 1, OP_AB = 2, OP_EMPTY = 3, OP_NONE = 4 };
+
+/* the base-point table in the Ai slab's row layout: entry e = rows
+   [Z = 1 | Y-X | Y+X | 2dT] x 12 limbs (10 used), so ADD-A and ADD-B load
+   their operand with the same code from different bases */
+__device__ i32 g_bi12[8][48];
+#ifdef FD_POOL_DEBUG
+__device__ u32 g_pool_dbg[4];   /* steps, live lanes, ADD steps, refill-only steps (summed over waves) */
+__device__ u64 g_pool_dbg_t[8192][2];   /* per wave: wall_clock64 at start and exit */
+#endif
+
+__global__ void __launch_bounds__(64)
+k_ai( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L ) {
+  if( blockIdx.x == 0 ) {
+    for( int k=threadIdx.x; k<8*48; k+=64 ) {
+      int e = k / 48, c = (k % 48) / 12, l = k % 12;
+      i32 v = 0;
+      if( l < 10 ) {
+        if( c == 0 ) v = (l == 0);
+        else if( c == 1 ) v = BI_TABLE[e][1][l];
+        else if( c == 2 ) v = BI_TABLE[e][0][l];
+        else v = BI_TABLE[e][2][l];
+      }
+      g_bi12[e][k % 48] = v;
+    }
+  }
+  u32 i = blockIdx.x * 64u + threadIdx.x;
+  if( i == 0u ) *(u32 *)(ws + L.ctr) = 0u;
+  bool act = (i < n) && (err[i] == 1);
+  if( act && (ws[L.ds + 2u*i] | ws[L.ds + 2u*i + 1u]) ) { err[i] = (i8)-2; act = false; }
+  size_t N = L.N;
+  u32 ii = (i < n) ? i : 0u;
+  i32 * Ail = (i32 *)(ws + L.Ai) + (size_t)ii*384u;
+  {
+    p3 A;
+    i32 const * Aw = (i32 const *)(ws + L.A);
+    _Pragma("unroll") for( int k=0; k<10; k++ ) {
+      A.X.v[k] = act ? Aw[(size_t)(k   )*N + ii] : 0;
+      A.Y.v[k] = act ? Aw[(size_t)(10+k)*N + ii] : (k==0);
+      A.T.v[k] = act ? Aw[(size_t)(20+k)*N + ii] : 0;
+      A.Z.v[k] = (k==0);
+    }
+    fe cZ, cYmX, cYpX, cT2d;
+    ge_to_cached( cZ, cYmX, cYpX, cT2d, A );
+#   define AI_ROW( e, r, f ) do {                                                   \
+      int4 * d_ = (int4 *)(Ail + (e)*48 + (r)*12);                                  \
+      d_[0] = make_int4( f.v[0], f.v[1], f.v[2], f.v[3] );                          \
+      d_[1] = make_int4( f.v[4], f.v[5], f.v[6], f.v[7] );                          \
+      d_[2] = make_int4( f.v[8], f.v[9], 0, 0 );                                    \
+    } while(0)
+#   define AI_STORE( e ) do { AI_ROW( e, 0, cZ ); AI_ROW( e, 1, cYmX ); AI_ROW( e, 2, cYpX ); AI_ROW( e, 3, cT2d ); } while(0)
+    if( act ) AI_STORE( 0 );
+    p1p1 t = ge_dbl( A.X, A.Y, A.Z );
+    p3 A2 = ge_p1p1_to_p3( t );
+    for( int e=0; e<7; e++ ) {
+      p1p1 s2 = ge_add<false>( A2, cZ, cYmX, cYpX, cT2d, false );
+      p3 u = ge_p1p1_to_p3( s2 );
+      ge_to_cached( cZ, cYmX, cYpX, cT2d, u );
+      if( act ) AI_STORE( e+1 );
+    }
+#   undef AI_STORE
+#   undef AI_ROW
+  }
+  if( i < n ) {
+    uint4 in = make_uint4( 0u, 0xffffffffu, 0u, (u32)OP_EMPTY );
+    int p = act ? ((int const *)(ws + L.top))[i] : -1;
+    if( p >= 0 ) {
+      u32 ne = ((u32 const *)(ws + L.evn))[i];
+      u32 na = ne & 0xffu, nb = (ne >> 8) & 0xffu;
+      u16 const * ev = (u16 const *)(ws + L.dig) + (size_t)i*128u;
+      u32 hA = na ? (u32)ev[na - 1u] : 0xffffu, hB = nb ? (u32)ev[64u + nb - 1u] : 0xffffu;
+      in = make_uint4( 0u, hA | (hB << 16), ((u32)p & 0xffffu) | (na << 16) | (nb << 24), (u32)OP_D );
+    }
+    ((uint4 *)(ws + L.init))[i] = in;
+  }
+}
+
+__device__ __forceinline__ void
+pool_load_t( p1p1 & t, int4 const * s ) {
+  _Pragma("unroll") for( int r=0; r<10; r++ ) {
+    int4 x = s[r];
+    i32 v[4] = { x.x, x.y, x.z, x.w };
+    _Pragma("unroll") for( int c=0; c<4; c++ ) {
+      int k = 4*r + c;                     /* limb k of [X | Y | Z | T] */
+      if( k < 10 ) t.X.v[k] = v[c]; else if( k < 20 ) t.Y.v[k-10] = v[c];
+      else if( k < 30 ) t.Z.v[k-20] = v[c]; else t.T.v[k-30] = v[c];
+    }
+  }
+}
+
+__device__ __forceinline__ void
+pool_store_t( int4 * s, p1p1 const & t ) {
+  _Pragma("unroll") for( int r=0; r<10; r++ ) {
+    i32 v[4];
+    _Pragma("unroll") for( int c=0; c<4; c++ ) {
+      int k = 4*r + c;
+      v[c] = (k < 10) ? t.X.v[k] : (k < 20) ? t.Y.v[k-10] : (k < 30) ? t.Z.v[k-20] : t.T.v[k-30];
+    }
+    s[r] = make_int4( v[0], v[1], v[2], v[3] );
+  }
+}
+
+template<typename PTR>
+__device__ __forceinline__ void
+pool_load_ts( p1p1 & t, PTR s, u32 stride ) {
+  _Pragma("unroll") for( int r=0; r<10; r++ ) {
+    int4 x = s[(u32)r * stride];
+    i32 v[4] = { x.x, x.y, x.z, x.w };
+    _Pragma("unroll") for( int c=0; c<4; c++ ) {
+      int k = 4*r + c;
+      if( k < 10 ) t.X.v[k] = v[c]; else if( k < 20 ) t.Y.v[k-10] = v[c];
+      else if( k < 30 ) t.Z.v[k-20] = v[c]; else t.T.v[k-30] = v[c];
+    }
+  }
+}
+
+template<typename PTR>
+__device__ __forceinline__ void
+pool_store_ts( PTR s, u32 stride, p1p1 const & t ) {
+  _Pragma("unroll") for( int r=0; r<10; r++ ) {
+    i32 v[4];
+    _Pragma("unroll") for( int c=0; c<4; c++ ) {
+      int k = 4*r + c;
+      v[c] = (k < 10) ? t.X.v[k] : (k < 20) ? t.Y.v[k-10] : (k < 30) ? t.Z.v[k-20] : t.T.v[k-30];
+    }
+    s[(u32)r * stride] = make_int4( v[0], v[1], v[2], v[3] );
+  }
+}
+
+/* relative cost of a DBL and an ADD step (VALU issue, measured ratios of
+   their instruction mixes); only used when neither class fills a wave */
+#define FD_POOL_COST_D 13u
+#define FD_POOL_COST_A 17u
+
+__device__ __forceinline__ u32 lane_rank( u64 m ) {   /* set bits of m below this lane */
+  return __builtin_amdgcn_mbcnt_hi( (u32)(m >> 32), __builtin_amdgcn_mbcnt_lo( (u32)m, 0u ) );
+}
+
+/* The pool's op classes live in four wave-uniform 64-bit masks (slot s is
+   bit s & 63 of word s >> 6): mD = DBL next, mA = ADD-A / ADD-B next,
+   neither = free.  A step takes the first (up to) 64 slots of one class in
+   slot order; lane l learns the l-th of them from a rank list in LDS, loads
+   its slot's state from LDS, runs the op and writes the state back; the slots'
+   new classes return to the masks through each slot's owner lane (s & 63),
+   which pulls the processing lane's verdict with ds_bpermute. */
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
+  constexpr u32 P = FD_POOL_P;
+  static_assert( P >= 64 && P <= 128, "pool: each lane owns slots l and l + 64" );
+  __shared__ int4  s_t[10][P];   /* p1p1 state [X | Y | Z | T], 16-B column r of slot s at [r][s]:
+                                    a lane's b128 starts at bank 4 (s mod 16), not 8 (s mod 8) */
+  __shared__ uint4 s_m[P];       /* { sig, heads, p | ja<<16 | jb<<24, op } */
+  __shared__ u32   s_list[64];   /* slot of each rank in the step's selection */
+  u32 const l = threadIdx.x, w = blockIdx.x;
+  uint4 const * init = (uint4 const *)(ws + L.init);
+  u16 const * dig = (u16 const *)(ws + L.dig);
+  i32 * Ai = (i32 *)(ws + L.Ai);
+  u64 const valid1 = (P >= 128u) ? ~0UL : ((1UL << (P - 64u)) - 1UL);   /* slots 64.. that exist */
+
+  u64 mD0 = 0, mD1 = 0, mA0 = 0, mA1 = 0;
+#ifdef FD_POOL_DEBUG
+  u64 dbg_t0 = wall_clock64();
+#endif
+  u32 * ctr = (u32 *)(ws + L.ctr);   /* next unclaimed signature, shared by all waves */
+  bool more = true;                  /* wave-uniform: the counter has not passed n */
+  /* hang guard: every step advances at least one op of at most 448 per
+     signature, and a wave can claim at most all n signatures */
+  u64 const iter_max = ((u64)n + 2u*P) * 448u;
+#ifdef FD_POOL_DEBUG
+  u32 dbg_steps = 0, dbg_lanes = 0, dbg_add = 0, dbg_idle = 0;
+#endif
+  for( u64 iter = 0; iter < iter_max; iter++ ) {
+    u32 nD = (u32)(__builtin_popcountll( mD0 ) + __builtin_popcountll( mD1 ));
+    u32 nA = (u32)(__builtin_popcountll( mA0 ) + __builtin_popcountll( mA1 ));
+    u64 f0 = ~(mD0 | mA0), f1 = ~(mD1 | mA1) & valid1;   /* free slots */
+    u32 nfree = (u32)(__builtin_popcountll( f0 ) + __builtin_popcountll( f1 ));
+    /* refill in batches (one global round trip per 16 finished signatures),
+       or whenever no class fills a wave */
+    if( more && nfree && (nfree >= 16u || (nD < 64u && nA < 64u)) ) {
+#ifdef FD_POOL_DEBUG
+      dbg_idle++;
+#endif
+      /* claim nfree signatures (one vector atomic; faster waves claim more,
+         so the waves of a launch finish together) */
+      u32 base = 0u;
+      if( l == 0u ) base = atomicAdd( ctr, nfree );
+      base = (u32)__builtin_amdgcn_readfirstlane( (int)base );
+      if( base + nfree >= n || base + nfree < base ) more = false;
+      u32 pf0 = (u32)__builtin_popcountll( f0 );
+      u64 s0 = (u64)base + lane_rank( f0 ), s1 = (u64)base + pf0 + lane_rank( f1 );
+      bool r0 = ((f0 >> l) & 1u) && s0 < n, r1 = ((f1 >> l) & 1u) && s1 < n;
+      uint4 in0 = init[r0 ? s0 : 0u], in1 = init[r1 ? s1 : 0u];
+      r0 = r0 && in0.w == OP_D; r1 = r1 && in1.w == OP_D;   /* inactive signatures leave the slot free */
+      p1p1 id;   /* new signatures enter with the identity (p1p1 whose p2 is (0,1,1)) */
+      id.X = fe_zero(); id.Y = fe_one(); id.Z = fe_one(); id.T = fe_one();
+      if( r0 ) { s_m[l] = make_uint4( (u32)s0, in0.y, in0.z, (u32)OP_D ); pool_store_ts( &s_t[0][l], P, id ); }
+      if( r1 ) { s_m[l + 64u] = make_uint4( (u32)s1, in1.y, in1.z, (u32)OP_D ); pool_store_ts( &s_t[0][l + 64u], P, id ); }
+      mD0 |= __builtin_amdgcn_ballot_w64( r0 );
+      mD1 |= __builtin_amdgcn_ballot_w64( r1 );
+      nD = (u32)(__builtin_popcountll( mD0 ) + __builtin_popcountll( mD1 ));
+    }
+    if( !(nD + nA) ) {
+      if( !more ) break;   /* pool empty, nothing left to take */
+      continue;
+    }
+
+    /* the step's class and slots */
+    bool addc = nA >= 64u ? true : nD >= 64u ? false : nA * FD_POOL_COST_D > nD * FD_POOL_COST_A;
+    u64 C0 = addc ? mA0 : mD0, C1 = addc ? mA1 : mD1;
+    u32 pc0 = (u32)__builtin_popcountll( C0 );
+    u32 nsel = pc0 + (u32)__builtin_popcountll( C1 );
+    if( nsel > 64u ) nsel = 64u;
+    /* owner view: rank of my slots in the selection (processing lane) */
+    u32 rk0 = lane_rank( C0 ), rk1 = pc0 + lane_rank( C1 );
+    bool in0 = (C0 >> l) & 1u, in1 = ((C1 >> l) & 1u) && rk1 < 64u;
+    u64 S1 = __builtin_amdgcn_ballot_w64( in1 );            /* selected slots of word 1 (word 0: all of C0) */
+    if( addc ) { mA0 &= ~C0; mA1 &= ~S1; } else { mD0 &= ~C0; mD1 &= ~S1; }
+#ifdef FD_POOL_DEBUG
+    dbg_steps++; dbg_lanes += nsel; dbg_add += addc;
+#endif
+    bool live = l < nsel;
+    /* slot of rank l: each selected slot's owner writes it at its rank (the
+       wave's LDS accesses complete in order: no barrier for a one-wave group) */
+    if( in0 ) s_list[rk0] = l;
+    if( in1 ) s_list[rk1] = l + 64u;
+    __builtin_amdgcn_wave_barrier();
+    u32 s = live ? s_list[l] : 0u;
+    uint4 m = s_m[s];
+    u32 op = live ? m.w : (u32)OP_AB;   /* dead lanes: harmless reads, nothing stored */
+    u32 si = live ? m.x : 0u;
+    u32 hA = m.y & 0xffffu, hB = m.y >> 16;
+    int p = (int)(short)(m.z & 0xffffu);
+    u32 ja = (m.z >> 16) & 0xffu, jb = m.z >> 24;
+    /* the consumed event's successor (popped after the op): its dword */
+    u32 pidx = (op == OP_AA && ja >= 2u) ? ja - 2u : (op == OP_AB && jb >= 2u) ? 64u + jb - 2u : 0u;
+    u32 nh = ((u32 const *)(dig + (size_t)si*128u))[pidx >> 1];
+    p1p1 t;
+    pool_load_ts( t, &s_t[0][s], P );
+
+    if( addc ) {
+      int dg = (op == OP_AA) ? (int)(i8)(hA >> 8) : (int)(i8)(hB >> 8);
+      bool neg = live && dg < 0;
+      int e = live ? ((dg < 0 ? -dg : dg) >> 1) & 7 : 0;
+      i32 const * qb = (live && op == OP_AA) ? Ai + (size_t)si*384u + e*48 : &g_bi12[e][0];
+      int const rowM = neg ? 2 : 1, rowP = neg ? 1 : 2;
+      fe q[4];
+#     define Q_ROW( R_, C_ ) do {                                                     \
+        int4 const * src_ = (int4 const *)(qb + (C_)*12);                            \
+        int4 x0 = src_[0], x1 = src_[1], x2 = src_[2];                               \
+        q[R_].v[0] = x0.x; q[R_].v[1] = x0.y; q[R_].v[2] = x0.z; q[R_].v[3] = x0.w;  \
+        q[R_].v[4] = x1.x; q[R_].v[5] = x1.y; q[R_].v[6] = x1.z; q[R_].v[7] = x1.w;  \
+        q[R_].v[8] = x2.x; q[R_].v[9] = x2.y;                                        \
+      } while(0)
+      Q_ROW( 0, 0 ); Q_ROW( 1, rowM ); Q_ROW( 2, rowP ); Q_ROW( 3, 3 );
+#     undef Q_ROW
+      p3 u = ge_p1p1_to_p3_fold( t );
+      /* the table operand is first touched here, after p1p1 -> p3 (its x19
+         pre-multiples would otherwise be scheduled first and wait for it) */
+      _Pragma("unroll") for( int r=0; r<4; r++ )
+        asm volatile( "" : "+v"(q[r].v[0]), "+v"(q[r].v[1]), "+v"(q[r].v[2]), "+v"(q[r].v[3]), "+v"(q[r].v[4]),
+                           "+v"(q[r].v[5]), "+v"(q[r].v[6]), "+v"(q[r].v[7]), "+v"(q[r].v[8]), "+v"(q[r].v[9])
+                         : "v"(u.X.v[9]), "v"(u.T.v[9]) );
+      fe ypx = fe_add( u.Y, u.X ), ymx = fe_sub( u.Y, u.X );
+      fe PP, MM, ZZ, TT;
+      fe_mul_fold2w( PP, ypx, q[2], MM, ymx, q[1] );
+      fe_mul_fold2w( ZZ, u.Z, q[0], TT, u.T, q[3] );
+      i32 sx = neg ? -1 : 0, sn = neg ? 1 : 0;
+      _Pragma("unroll") for( int k=0; k<10; k++ ) {
+        i32 z2 = ZZ.v[k] + ZZ.v[k];
+        i32 sT = fd_xad( TT.v[k], sx, sn );          /* neg ? -TT : TT */
+        t.X.v[k] = PP.v[k] - MM.v[k];
+        t.Y.v[k] = PP.v[k] + MM.v[k];
+        t.Z.v[k] = z2 + sT;
+        t.T.v[k] = z2 - sT;
+      }
+    } else {
+      /* p1p1 -> p2 (the first three products of p1p1 -> p3), then the
+         doubling (avx/fd_ed25519_ge.c:493-498) with squares */
+      fe uZ, uY, uX;
+      fe_mul_fold2w( uZ, t.Z, t.T, uY, t.Z, t.Y );
+      uX = fe_mul_fold1( t.X, t.T );
+      fe xy = fe_add( uX, uY );
+      fe a, b, c, d;
+      fe_sq_fold2w<false, false>( a, xy, b, uY );
+      fe_sq_fold2w<false, true>( c, uX, d, uZ );
+      _Pragma("unroll") for( int k=0; k<10; k++ ) {
+        i32 z = b.v[k] - c.v[k];
+        t.X.v[k] = a.v[k] - b.v[k] - c.v[k];
+        t.Y.v[k] = b.v[k] + c.v[k];
+        t.Z.v[k] = z;
+        t.T.v[k] = d.v[k] - z;
+      }
+    }
+
+    /* advance the op stream: pop the consumed event, then the next op */
+    u32 nop = (u32)OP_EMPTY;
+    if( live ) {
+      u32 ev = (nh >> ((pidx & 1u) << 4)) & 0xffffu;
+      if( op == OP_AA ) { ja--; hA = ja ? ev : 0xffffu; } else if( op == OP_AB ) { jb--; hB = jb ? ev : 0xffffu; }
+      int posA = (hA == 0xffffu) ? -1 : (int)(hA & 0xffu);
+      int posB = (hB == 0xffffu) ? -1 : (int)(hB & 0xffu);
+      if( op == OP_D && posA == p )                       nop = OP_AA;
+      else if( (op == OP_D || op == OP_AA) && posB == p ) nop = OP_AB;
+      else { p--; nop = (p < 0) ? (u32)OP_EMPTY : (u32)OP_D; }
+      if( nop == OP_EMPTY ) {
+        pool_store_t( (int4 *)(Ai + (size_t)si*384u), t );   /* park the final p1p1 for k_fin */
+      } else {
+        pool_store_ts( &s_t[0][s], P, t );
+        s_m[s] = make_uint4( si, hA | (hB << 16), ((u32)p & 0xffffu) | (ja << 16) | (jb << 24), nop );
+      }
+    }
+    /* the slots' new classes, at their owner lanes */
+    u32 v0 = (u32)__builtin_amdgcn_ds_bpermute( (int)(rk0 << 2), (int)nop );
+    u32 v1 = (u32)__builtin_amdgcn_ds_bpermute( (int)((rk1 & 63u) << 2), (int)nop );
+    mD0 |= __builtin_amdgcn_ballot_w64( in0 && v0 == OP_D );
+    mA0 |= __builtin_amdgcn_ballot_w64( in0 && (v0 == OP_AA || v0 == OP_AB) );
+    mD1 |= __builtin_amdgcn_ballot_w64( in1 && v1 == OP_D );
+    mA1 |= __builtin_amdgcn_ballot_w64( in1 && (v1 == OP_AA || v1 == OP_AB) );
+  }
+#ifdef FD_POOL_DEBUG
+  if( l == 0u ) { atomicAdd( &g_pool_dbg[0], dbg_steps ); atomicAdd( &g_pool_dbg[1], dbg_lanes ); atomicAdd( &g_pool_dbg[2], dbg_add ); atomicAdd( &g_pool_dbg[3], dbg_idle ); }
+  if( l == 0u && w < 8192u ) { g_pool_dbg_t[w][0] = dbg_t0; g_pool_dbg_t[w][1] = wall_clock64(); }
+#else
+  (void)w;
+#endif
+#ifdef FD_POOL_DEBUG
+#endif
+}
+
+#ifdef FD_POOL_DEBUG
+extern "C" int
+fd_amd_pool_debug( unsigned * out, int reset ) {
+  if( hipMemcpyFromSymbol( out, HIP_SYMBOL( g_pool_dbg ), sizeof(unsigned)*4 ) != hipSuccess ) return -1;
+  if( reset ) { unsigned z[4] = { 0, 0, 0, 0 }; if( hipMemcpyToSymbol( HIP_SYMBOL( g_pool_dbg ), z, sizeof(z) ) != hipSuccess ) return -1; }
+  return 0;
+}
+extern "C" int
+fd_amd_pool_debug_times( unsigned long * out /* [8192][2] */ ) {
+  return hipMemcpyFromSymbol( out, HIP_SYMBOL( g_pool_dbg_t ), sizeof(unsigned long)*8192*2 ) == hipSuccess ? 0 : -1;
+}
+#endif
+
+__global__ void __launch_bounds__(64)
+k_fin( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats ) {
+  u32 i = blockIdx.x * 64u + threadIdx.x;
+  if( i >= n ) return;
+  size_t N = L.N;
+  bool act = err[i] == 1;
+  int top = ((int const *)(ws + L.top))[i];
+  if( act ) {
+    p1p1 t;
+    if( top < 0 ) { t.X = fe_zero(); t.Y = fe_one(); t.Z = fe_one(); t.T = fe_one(); }
+    else pool_load_t( t, (int4 const *)((i32 const *)(ws + L.Ai) + (size_t)i*384u) );
+    fe uZ, uY, uX;
+    fe_mul_fold2w( uZ, t.Z, t.T, uY, t.Z, t.Y );
+    uX = fe_mul_fold1( t.X, t.T );
+    i32 const * Rw = (i32 const *)(ws + L.R);
+    fe RX, RY;
+    _Pragma("unroll") for( int k=0; k<10; k++ ) { RX.v[k] = Rw[(size_t)k*N + i]; RY.v[k] = Rw[(size_t)(10+k)*N + i]; }
+    fe xZ, yZ;
+    fe_mul_fold2w( xZ, uZ, RX, yZ, uZ, RY );
+    bool eq = true;
+    _Pragma("unroll") for( int k=0; k<8; k++ ) eq = eq && (xZ.v[k] == uX.v[k]) && (yZ.v[k] == uY.v[k]);
+    err[i] = (i8)(eq ? 0 : -3);
+  }
+  if( want_stats ) {
+    u32 ne = ((u32 const *)(ws + L.evn))[i];
+    u32 * st = (u32 *)(ws + L.st);
+    st[i] = act ? (u32)(top + 1) : 0u; st[N + i] = act ? (ne & 0xffu) : 0u; st[2*N + i] = act ? ((ne >> 8) & 0xffu) : 0u;
+  }
+}
+
+/* ------------------------------------------------------------------ */
 /* k_tile_gather: the streaming tile's staging.  Frag i (fsz[i] bytes at
    chunk ichunk[i] of `src`, host memory mapped into the GPU: the input
    dcache in zero-copy mode, the tile's own output dcache in copy mode) is
@@ -1366,6 +1776,31 @@ fd_amd_launch_copy_out( void * d_dst, void const * d_src, size_t n, hipStream_t 
    one per SIMD (n <= 8192 on 1024 SIMDs), slower beyond. */
 static volatile u32 g_dsm4_max = 16384u;
 static volatile u32 g_dsm8_max = 8192u;
+static volatile u32 g_pool_min = 0xFFFFFFFFu;   /* k_dsmp off by default: see DESIGN.md s6 (pooled A/B) */
+
+extern "C" void
+fd_ed25519_amd_set_pool_batch_min( unsigned long n ) {
+  g_pool_min = n > 0xFFFFFFFFUL ? 0xFFFFFFFFu : (u32)n;
+}
+
+/* k_dsmp grid: one single-wave workgroup per resident wave slot (8 per CU:
+   LDS-bound at FD_POOL_P slots, VGPR-bound at 2 waves per SIMD), fewer
+   when the batch would leave pools nearly empty */
+static u32
+pool_waves( u32 n ) {
+  static int cus = 0;
+  if( !cus ) {
+    int dev = 0, v = 0;
+    if( hipGetDevice( &dev ) != hipSuccess || hipDeviceGetAttribute( &v, hipDeviceAttributeMultiprocessorCount, dev ) != hipSuccess || v <= 0 ) v = 256;
+    cus = v;
+  }
+  u32 wmax = 8u * (u32)cus;
+#ifdef FD_POOL_DEBUG
+  if( char const * e = getenv( "FD_POOL_WAVES" ) ) { u32 v = (u32)atoi( e ); if( v ) wmax = v; }
+#endif
+  u32 want = (n + 63u) / 64u;
+  return want < wmax ? (want ? want : 1u) : wmax;
+}
 
 extern "C" void
 fd_ed25519_amd_set_small_batch_max( unsigned long n ) {
@@ -1384,7 +1819,7 @@ fd_amd_batch_dsm_mode( uint32_t n ) {
 
 int
 fd_amd_uses_latency_path( uint32_t n, int dsm_mode ) {
-  return dsm_mode >= 2 || (dsm_mode == 0 && (n <= g_dsm4_max || n <= g_dsm8_max));
+  return dsm_mode == 2 || dsm_mode == 3 || (dsm_mode == 0 && (n <= g_dsm4_max || n <= g_dsm8_max));
 }
 
 int
@@ -1404,11 +1839,18 @@ fd_amd_launch_verify( u32 n, u8 const * d_pub, u8 const * d_sig, u32 const * d_o
     if( eight ) hipLaunchKernelGGL( k_dsm8, dim3((n + 7u)/8u), dim3(64), 0, stream, n, d_err, ws, L, want_stats );
     else        hipLaunchKernelGGL( k_dsm4, dim3((n + 15u)/16u), dim3(64), 0, stream, n, d_err, ws, L, want_stats );
   } else {
+    bool pooled = dsm_mode == 4 || (dsm_mode == 0 && n >= g_pool_min);
     hipLaunchKernelGGL( k_prep,   dim3(nb),    dim3(64), 0, stream, n, d_pub, d_sig, d_off, d_sz, d_blob, d_err, ws, L, d_skip );
     if( ev ) (void)hipEventRecord( ev[1], stream );
     hipLaunchKernelGGL( k_decomp, dim3(2u*nb), dim3(64), 0, stream, n, d_pub, d_sig, d_err, ws, L );
     if( ev ) (void)hipEventRecord( ev[2], stream );
-    hipLaunchKernelGGL( k_dsm,    dim3(nb),    dim3(64), 0, stream, n, d_err, ws, L, want_stats );
+    if( pooled ) {
+      hipLaunchKernelGGL( k_ai,   dim3(nb),    dim3(64), 0, stream, n, d_err, ws, L );
+      hipLaunchKernelGGL( k_dsmp, dim3(pool_waves( n )), dim3(64), 0, stream, n, ws, L );
+      hipLaunchKernelGGL( k_fin,  dim3(nb),    dim3(64), 0, stream, n, d_err, ws, L, want_stats );
+    } else {
+      hipLaunchKernelGGL( k_dsm,  dim3(nb),    dim3(64), 0, stream, n, d_err, ws, L, want_stats );
+    }
   }
   if( ev ) (void)hipEventRecord( ev[3], stream );
   return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -80,6 +80,8 @@ def lib():
     L.fd_ed25519_amd_set_small_batch_max.restype = None
     L.fd_ed25519_amd_set_latency_batch_max.argtypes = [ul]
     L.fd_ed25519_amd_set_latency_batch_max.restype = None
+    L.fd_ed25519_amd_set_pool_batch_min.argtypes = [ul]
+    L.fd_ed25519_amd_set_pool_batch_min.restype = None
     L.fd_verify_amd_tile_new.argtypes = [i, ul, ul, ul, ul]
     L.fd_verify_amd_tile_new.restype = vp
     L.fd_verify_amd_tile_out_chunk0.argtypes = [vp]
@@ -450,18 +452,26 @@ def set_latency_batch_max(n):
     lib().fd_ed25519_amd_set_latency_batch_max(int(n))
 
 
+def set_pool_batch_min(n):
+    """Throughput batches of at least n signatures use the pooled kernel (k_dsmp)."""
+    lib().fd_ed25519_amd_set_pool_batch_min(int(n))
+
+
 def select_dsm_kernel(name):
     """Force one double-scalar-mult kernel for every batch size (tests):
-    'k_dsm', 'k_dsm4', 'k_dsm8'; 'default' restores the size rule."""
-    big = 1 << 32
-    small, lat = {"k_dsm": (0, 0), "k_dsm4": (big, 0), "k_dsm8": (big, big),
-                  "default": (SMALL_BATCH_MAX_DEFAULT, LATENCY_BATCH_MAX_DEFAULT)}[name]
+    'k_dsm', 'k_dsmp', 'k_dsm4', 'k_dsm8'; 'default' restores the size rule."""
+    big = (1 << 32) - 1
+    small, lat, pool = {"k_dsm": (0, 0, big), "k_dsmp": (0, 0, 0), "k_dsm4": (big, 0, big),
+                        "k_dsm8": (big, big, big),
+                        "default": (SMALL_BATCH_MAX_DEFAULT, LATENCY_BATCH_MAX_DEFAULT, POOL_BATCH_MIN_DEFAULT)}[name]
     set_small_batch_max(small)
     set_latency_batch_max(lat)
+    set_pool_batch_min(pool)
 
 
 SMALL_BATCH_MAX_DEFAULT = 16384
 LATENCY_BATCH_MAX_DEFAULT = 8192
+POOL_BATCH_MIN_DEFAULT = (1 << 32) - 1   # k_dsmp opt-in (DESIGN.md s6)
 FD_TXN_AMD_ERR_PARSE = -4
 FD_TXN_MAX_SZ = 3570
 

@@ -298,13 +298,19 @@ fd_ed25519_amd_sign_dev( ulong         n,
    while its waves fit one per SIMD); batches of at most
    fd_ed25519_amd_set_small_batch_max (default 16384) run k_dsm4 (four lanes
    per signature); larger ones the throughput kernel k_dsm (one lane per
-   signature).  All give identical verdicts; 0 disables a kernel.
-   Process-wide. */
+   signature, its own op per lane), or k_dsmp (one lane per signature,
+   signatures pooled per wave so that a wave runs one op class at a time)
+   for batches of at least fd_ed25519_amd_set_pool_batch_min signatures
+   (default ~0UL: off; measured on par with k_dsm).  All give
+   identical verdicts; 0 disables a latency kernel.  Process-wide. */
 void
 fd_ed25519_amd_set_small_batch_max( ulong n );
 
 void
 fd_ed25519_amd_set_latency_batch_max( ulong n );
+
+void
+fd_ed25519_amd_set_pool_batch_min( ulong n );
 
 /* Library version / build string. */
 char const *

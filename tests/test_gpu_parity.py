@@ -232,10 +232,11 @@ def test_prep_digits_vs_python(golden):
         assert tp[j] == (max(nz) if nz else -1)
 
 
-@pytest.fixture(params=["k_dsm", "k_dsm4", "k_dsm8"])
+@pytest.fixture(params=["k_dsm", "k_dsmp", "k_dsm4", "k_dsm8"])
 def dsm_kernel(request):
-    """Run a test once per double-scalar-mult kernel (throughput, 4-lane and
-    8-lane latency kernels), each forced for every batch size."""
+    """Run a test once per double-scalar-mult kernel (throughput per-lane and
+    pooled, 4-lane and 8-lane latency kernels), each forced for every batch
+    size."""
     from firedancer_amd import ed25519
     ed25519.select_dsm_kernel(request.param)
     yield request.param
