@@ -74,6 +74,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sigs", "--n", dest="n", type=int, default=1 << 20, help="signatures per GPU per step")
     ap.add_argument("--msg-sz", type=int, default=200)
+    ap.add_argument("--dsm-kernel", choices=("default", "k_dsm", "k_dsmp"), default="default",
+                    help="throughput double-scalar-mult kernel (A/B; default: the library's size rule)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="batches in flight (consecutive steps alternate streams, as the engine's chunks do)")
     ap.add_argument("--total-sigs", type=int, default=1 << 24,
                     help="txn workload: signatures over all ranks (strong scaling)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
@@ -185,16 +189,26 @@ def make_workload(n, msg_sz, seed):
     return workload.sig_batch(n, msg_sz, seed)
 
 
+def dsm_kernels(n, choice):
+    """The double-scalar-mult launches a resident batch of n runs: the pooled
+    k_ai + k_dsmp + k_fin from the library's pool threshold up, else k_dsm."""
+    from firedancer_amd import ed25519
+    pooled = choice == "k_dsmp" or (choice == "default" and n >= ed25519.POOL_BATCH_MIN_DEFAULT)
+    return ["k_ai", "k_dsmp", "k_fin"] if pooled else ["k_dsm"]
+
+
 def dsm_roofline(st, kernel_ms, n, kernel="k_dsm", note=None):
-    """Algorithmic k_dsm multiply-accumulates (from the kernel's own work
-    statistics) per launch / kernel time, against the integer-multiply peak."""
+    """Algorithmic double-scalar-mult multiply-accumulates (from the kernels'
+    own work statistics) per launch / the DSM stage's time, against the
+    integer-multiply peak.  kernel: '+'-joined launch names of the stage."""
     st = st.astype(np.float64)
     I, nh, ns = st[0].sum(), st[1].sum(), st[2].sum()
     live = float((st[0] > 0).sum())
     mac = MAC_MUL * (68 * live + 3 * I + 8 * nh + 7 * ns + 2 * live) + MAC_SQ * (4 * live + 4 * I)
     achieved = mac / (kernel_ms * 1e-3) / 1e12
+    traffic = [pmc_traffic(k, n) for k in kernel.split("+")] if "(" not in kernel else [None]
     r = {"bound": "valu-imad64", "kernel": kernel, "achieved": achieved, "peak": PEAK_TMAC, "unit": "TMAC/s",
-         "frac": achieved / PEAK_TMAC, "traffic": pmc_traffic("k_dsm", n),
+         "frac": achieved / PEAK_TMAC, "traffic": None if None in traffic else sum(traffic),
          "traffic_note": "HBM bytes per launch from the committed PMC pass (profiles/r02_pmc_latest.json: "
                          "2*FETCH_SIZE+WRITE_SIZE KB, gfx950 correction), scaled to this batch",
          "mac_per_sig": mac / max(live, 1.0)}
@@ -379,7 +393,16 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        # gloo prints its connection report on stdout from C++; keep stdout
+        # for rank 0's one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
 
     from firedancer_amd import ed25519, hip
 
@@ -394,44 +417,65 @@ def main():
         return run_txn(args, rank, world, dist)
 
     n = args.n
+    if args.dsm_kernel != "default":
+        ed25519.select_dsm_kernel(args.dsm_kernel)
     t0 = time.perf_counter()
     pub, sig, off, sz, blob = make_workload(n, args.msg_sz, 1000 + rank)
     gen_s = time.perf_counter() - t0
 
     d = {k: hip.DeviceBuffer.from_array(v) for k, v in
          dict(pub=pub, sig=sig, off=off, sz=sz, blob=blob).items()}
-    d_err = hip.DeviceBuffer(n)
-    d_ws = hip.DeviceBuffer(ed25519.workspace_footprint(n))
+    # consecutive steps alternate between `streams` (stream, verdicts,
+    # workspace) sets, as the engine keeps two chunks in flight: one batch's
+    # hashing/decompression fills the SIMDs the previous batch's last
+    # double-scalar-mult waves leave idle
+    ns = max(1, args.streams)
+    sets = [(hip.Stream(), hip.DeviceBuffer(n), hip.DeviceBuffer(ed25519.workspace_footprint(n))) for _ in range(ns)]
     d_stats = hip.DeviceBuffer(4 * 3 * n)
-    stream = hip.Stream()
-    run = lambda ev=None: ed25519.verify_dev_ev(n, d["pub"].ptr, d["sig"].ptr, d["off"].ptr, d["sz"].ptr,  # noqa: E731
-                                                 d["blob"].ptr, d_err.ptr, d_ws.ptr, stream.handle, ev)
+    stream, d_err, d_ws = sets[0]
 
-    for _ in range(args.warmup):
-        run()
-    stream.synchronize()
+    def run(k, ev=None):
+        st_, er_, ws_ = sets[k % ns]
+        ed25519.verify_dev_ev(n, d["pub"].ptr, d["sig"].ptr, d["off"].ptr, d["sz"].ptr, d["blob"].ptr, er_.ptr,
+                              ws_.ptr, st_.handle, ev)
 
-    evs = [[hip.Event() for _ in range(4)] for _ in range(args.steps)]
+    def sync_all():
+        for st_, _, _ in sets:
+            st_.synchronize()
+
+    for k in range(max(args.warmup, ns)):
+        run(k)
+    sync_all()
+
     if dist:
         dist.barrier()
-    stream.synchronize()
+    sync_all()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        run(evs[k])
-    stream.synchronize()
+        run(k)
+    sync_all()
     elapsed = time.perf_counter() - t0
     if dist:
         from firedancer_amd.shard import max_over_ranks
         elapsed = max_over_ranks(elapsed)
         dist.barrier()
 
+    # per-kernel times (and the roofline) from HIP events on one stream with
+    # nothing else running, after the timed region
+    nev = 3
+    evs = [[hip.Event() for _ in range(4)] for _ in range(nev)]
+    for k in range(nev):
+        run(0, evs[k])
+    sync_all()
     stage_ms = np.zeros(3)
     for ev in evs:
         for j in range(3):
             stage_ms[j] += ev[j].elapsed_ms(ev[j + 1])
-    stage_ms /= args.steps
+    stage_ms /= nev
 
     err = d_err.to_array(np.int8, n)
+    for _, er_, _ in sets[1:]:
+        assert np.array_equal(er_.to_array(np.int8, n), err)
     ed25519.work_stats_dev(n, d_ws.ptr, d_stats.ptr, stream.handle)
     stream.synchronize()
     st = d_stats.to_array(np.uint32, 3 * n).reshape(3, n)
@@ -453,10 +497,15 @@ def main():
         "dtype": DTYPE,
         "data": "synthetic: fresh random keypairs and messages, signed on the GPU (k_sign), inputs resident in HBM",
         "config": {"workload": "configs[1]: 1xMI355X batch of 2^20 single-signer sigs, 200-byte messages",
-                   "sigs_per_gpu_per_step": n, "msg_sz": args.msg_sz, "parallelism": "shard%d" % world},
-        "stage_ms": {"k_prep": stage_ms[0], "k_decomp": stage_ms[1], "k_dsm": stage_ms[2]},
+                   "sigs_per_gpu_per_step": n, "msg_sz": args.msg_sz, "parallelism": "shard%d" % world,
+                   "streams": ns},
+        "stage_ms": {"k_prep": stage_ms[0], "k_decomp": stage_ms[1], "k_dsm": stage_ms[2],
+                     "note": "one batch alone on one stream (HIP events), after the timed region"},
         "verdicts": {"ok": int((err == 0).sum()), "rejected": int((err != 0).sum())},
-        "roofline": dsm_roofline(st, stage_ms[2], n),
+        "roofline": dsm_roofline(st, stage_ms[2], n, kernel="+".join(dsm_kernels(n, args.dsm_kernel)),
+                                 note="DSM stage of one batch alone on one stream (HIP events); with %d "
+                                      "streams in the timed region the next batch's k_prep/k_decomp also fill "
+                                      "the SIMDs its last waves leave idle" % ns),
         "workload_gen_s": gen_s,
     }
     if not args.no_latency:

@@ -1418,10 +1418,11 @@ pool_store_ts( PTR s, u32 stride, p1p1 const & t ) {
   }
 }
 
-/* relative cost of a DBL and an ADD step (VALU issue, measured ratios of
-   their instruction mixes); only used when neither class fills a wave */
-#define FD_POOL_COST_D 13u
-#define FD_POOL_COST_A 17u
+/* a pure DBL step is chosen while its lane count is at least this percentage
+   of a mixed step's (the measured cost ratio of the two steps) */
+#ifndef FD_POOL_DBL_PCT
+#define FD_POOL_DBL_PCT 78u
+#endif
 
 __device__ __forceinline__ u32 lane_rank( u64 m ) {   /* set bits of m below this lane */
   return __builtin_amdgcn_mbcnt_hi( (u32)(m >> 32), __builtin_amdgcn_mbcnt_lo( (u32)m, 0u ) );
@@ -1495,19 +1496,26 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
       continue;
     }
 
-    /* the step's class and slots */
-    bool addc = nA >= 64u ? true : nD >= 64u ? false : nA * FD_POOL_COST_D > nD * FD_POOL_COST_A;
-    u64 C0 = addc ? mA0 : mD0, C1 = addc ? mA1 : mD1;
-    u32 pc0 = (u32)__builtin_popcountll( C0 );
-    u32 nsel = pc0 + (u32)__builtin_popcountll( C1 );
-    if( nsel > 64u ) nsel = 64u;
-    /* owner view: rank of my slots in the selection (processing lane) */
-    u32 rk0 = lane_rank( C0 ), rk1 = pc0 + lane_rank( C1 );
-    bool in0 = (C0 >> l) & 1u, in1 = ((C1 >> l) & 1u) && rk1 < 64u;
-    u64 S1 = __builtin_amdgcn_ballot_w64( in1 );            /* selected slots of word 1 (word 0: all of C0) */
-    if( addc ) { mA0 &= ~C0; mA1 &= ~S1; } else { mD0 &= ~C0; mD1 &= ~S1; }
+    /* the step: a pure DBL step (p2 + 4 squares) on up to 64 DBL slots, or
+       a MIXED step (k_dsm's uniform 8-mul step) that takes every ADD slot
+       first and fills the rest with DBL slots.  An ADD op costs the same in
+       either, so ADDs always go through mixed steps; a DBL step wins while
+       it is nearly as full as a mixed one (cost ratio ~0.78, measured). */
+    u32 kD = nD < 64u ? nD : 64u, kM = (nD + nA) < 64u ? (nD + nA) : 64u;
+    bool mixed = 100u * kD < FD_POOL_DBL_PCT * kM;
+    u32 nsel = mixed ? kM : kD;
+    u32 aoff = mixed ? nA : 0u;                                 /* DBL ranks start after the ADDs */
+    u32 pa0 = (u32)__builtin_popcountll( mA0 ), pd0 = (u32)__builtin_popcountll( mD0 );
+    bool isA0 = (mA0 >> l) & 1u, isA1 = (mA1 >> l) & 1u, isD0 = (mD0 >> l) & 1u, isD1 = (mD1 >> l) & 1u;
+    /* owner view: rank of my slots in the selection (= their processing lane) */
+    u32 rk0 = isA0 ? lane_rank( mA0 ) : aoff + lane_rank( mD0 );
+    u32 rk1 = isA1 ? pa0 + lane_rank( mA1 ) : aoff + pd0 + lane_rank( mD1 );
+    bool in0 = (isD0 || (mixed && isA0)) && rk0 < 64u;
+    bool in1 = (isD1 || (mixed && isA1)) && rk1 < 64u;
+    u64 S0 = __builtin_amdgcn_ballot_w64( in0 ), S1 = __builtin_amdgcn_ballot_w64( in1 );
+    mA0 &= ~S0; mA1 &= ~S1; mD0 &= ~S0; mD1 &= ~S1;
 #ifdef FD_POOL_DEBUG
-    dbg_steps++; dbg_lanes += nsel; dbg_add += addc;
+    dbg_steps++; dbg_lanes += nsel; dbg_add += mixed;
 #endif
     bool live = l < nsel;
     /* slot of rank l: each selected slot's owner writes it at its rank (the
@@ -1517,22 +1525,27 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
     __builtin_amdgcn_wave_barrier();
     u32 s = live ? s_list[l] : 0u;
     uint4 m = s_m[s];
-    u32 op = live ? m.w : (u32)OP_AB;   /* dead lanes: harmless reads, nothing stored */
+    u32 op = live ? m.w : (u32)OP_D;    /* dead lanes: harmless reads, nothing stored */
     u32 si = live ? m.x : 0u;
     u32 hA = m.y & 0xffffu, hB = m.y >> 16;
     int p = (int)(short)(m.z & 0xffffu);
     u32 ja = (m.z >> 16) & 0xffu, jb = m.z >> 24;
     /* the consumed event's successor (popped after the op): its dword */
     u32 pidx = (op == OP_AA && ja >= 2u) ? ja - 2u : (op == OP_AB && jb >= 2u) ? 64u + jb - 2u : 0u;
-    u32 nh = ((u32 const *)(dig + (size_t)si*128u))[pidx >> 1];
+    bool pop = (op == OP_AA && ja >= 2u) || (op == OP_AB && jb >= 2u);
+    /* lanes that pop nothing read one shared, cache-resident word instead of
+       their own event row (a load under a branch would wait at the join) */
+    u32 const * nha = pop ? (u32 const *)(dig + (size_t)si*128u) + (pidx >> 1) : (u32 const *)&g_bi12[0][0];
+    u32 nh = *nha;
     p1p1 t;
     pool_load_ts( t, &s_t[0][s], P );
 
-    if( addc ) {
+    if( mixed ) {
+      bool isadd = op == OP_AA || op == OP_AB;
       int dg = (op == OP_AA) ? (int)(i8)(hA >> 8) : (int)(i8)(hB >> 8);
-      bool neg = live && dg < 0;
-      int e = live ? ((dg < 0 ? -dg : dg) >> 1) & 7 : 0;
-      i32 const * qb = (live && op == OP_AA) ? Ai + (size_t)si*384u + e*48 : &g_bi12[e][0];
+      bool neg = isadd && dg < 0;
+      int e = isadd ? ((dg < 0 ? -dg : dg) >> 1) & 7 : 0;
+      i32 const * qb = (op == OP_AA) ? Ai + (size_t)si*384u + e*48 : &g_bi12[e][0];
       int const rowM = neg ? 2 : 1, rowP = neg ? 1 : 2;
       fe q[4];
 #     define Q_ROW( R_, C_ ) do {                                                     \
@@ -1551,18 +1564,39 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
         asm volatile( "" : "+v"(q[r].v[0]), "+v"(q[r].v[1]), "+v"(q[r].v[2]), "+v"(q[r].v[3]), "+v"(q[r].v[4]),
                            "+v"(q[r].v[5]), "+v"(q[r].v[6]), "+v"(q[r].v[7]), "+v"(q[r].v[8]), "+v"(q[r].v[9])
                          : "v"(u.X.v[9]), "v"(u.T.v[9]) );
-      fe ypx = fe_add( u.Y, u.X ), ymx = fe_sub( u.Y, u.X );
-      fe PP, MM, ZZ, TT;
-      fe_mul_fold2w( PP, ypx, q[2], MM, ymx, q[1] );
-      fe_mul_fold2w( ZZ, u.Z, q[0], TT, u.T, q[3] );
-      i32 sx = neg ? -1 : 0, sn = neg ? 1 : 0;
-      _Pragma("unroll") for( int k=0; k<10; k++ ) {
-        i32 z2 = ZZ.v[k] + ZZ.v[k];
-        i32 sT = fd_xad( TT.v[k], sx, sn );          /* neg ? -TT : TT */
-        t.X.v[k] = PP.v[k] - MM.v[k];
-        t.Y.v[k] = PP.v[k] + MM.v[k];
-        t.Z.v[k] = z2 + sT;
-        t.T.v[k] = z2 - sT;
+      /* k_dsm's op body and mix (see k_dsm) */
+      u64 mD = __builtin_amdgcn_ballot_w64( !isadd ), mN = __builtin_amdgcn_ballot_w64( neg );
+      fe m0, m1, m2, m3;
+      {
+        fe a0, b0, a1, b1, a2, b2, a3, b3;
+        _Pragma("unroll") for( int k=0; k<10; k++ ) {
+          i32 xy = u.X.v[k] + u.Y.v[k];
+          a0.v[k] = xy;                                     b0.v[k] = vsel( mD, xy, q[2].v[k] );
+          a1.v[k] = vsel( mD, u.Y.v[k], u.Y.v[k] - u.X.v[k] ); b1.v[k] = vsel( mD, u.Y.v[k], q[1].v[k] );
+          a2.v[k] = u.Z.v[k];                              b2.v[k] = vsel( mD, u.Z.v[k] + u.Z.v[k], q[0].v[k] );
+          a3.v[k] = vsel( mD, u.X.v[k], u.T.v[k] );        b3.v[k] = vsel( mD, u.X.v[k], q[3].v[k] );
+        }
+        fe_mul_fold2w<true, true>( m0, a0, b0, m1, a1, b1 );
+        fe_mul_fold2w<false, true>( m2, a2, b2, m3, a3, b3 );
+      }
+      {
+        u64 mS = mD | mN;
+        i32 Dv = vsel( mD, -1, 0 ), Sv = vsel( mS, -1, 0 ), Sn = vsel( mS, 1, 0 );
+        i32 cXe = Dv & (1<<25), cXo = Dv & (1<<24);
+        i32 cZe = vsel( mD, 0, vsel( mN, (1<<25), -(1<<25) ) ), cZo = vsel( mD, 0, vsel( mN, (1<<24), -(1<<24) ) );
+        i32 const nb2e = (i32)fd_opaque( -(2L<<25) ), nb2o = (i32)fd_opaque( -(2L<<24) );   /* SGPR */
+        i32 const sT = vsel( mD, 0, 2 );
+        _Pragma("unroll") for( int k=0; k<10; k++ ) {
+          i32 cX = (k & 1) ? cXo : cXe, cZ = (k & 1) ? cZo : cZe;
+          i32 A0 = m0.v[k], A1 = m1.v[k], A2 = m2.v[k], A3 = m3.v[k];
+          i32 sA3 = fd_xad( A3, Sv, Sn );
+          i32 z2 = A2 + A2;
+          i32 Z = fd_add3( vsel( mD, A1, z2 ), sA3, cZ );
+          t.X.v[k] = fd_add3( A0 - A1, sA3 & Dv, cX );
+          t.Y.v[k] = fd_add3s( A1, vsel( mD, A3, A0 ), (k & 1) ? nb2o : nb2e );
+          t.Z.v[k] = Z;
+          t.T.v[k] = (i32)((u32)A2 << (u32)sT) - Z;
+        }
       }
     } else {
       /* p1p1 -> p2 (the first three products of p1p1 -> p3), then the
@@ -1776,7 +1810,7 @@ fd_amd_launch_copy_out( void * d_dst, void const * d_src, size_t n, hipStream_t 
    one per SIMD (n <= 8192 on 1024 SIMDs), slower beyond. */
 static volatile u32 g_dsm4_max = 16384u;
 static volatile u32 g_dsm8_max = 8192u;
-static volatile u32 g_pool_min = 0xFFFFFFFFu;   /* k_dsmp off by default: see DESIGN.md s6 (pooled A/B) */
+static volatile u32 g_pool_min = 1u << 19;   /* k_dsmp from 2^19 signatures (pooled A/B) */
 
 extern "C" void
 fd_ed25519_amd_set_pool_batch_min( unsigned long n ) {

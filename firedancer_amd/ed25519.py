@@ -471,7 +471,7 @@ def select_dsm_kernel(name):
 
 SMALL_BATCH_MAX_DEFAULT = 16384
 LATENCY_BATCH_MAX_DEFAULT = 8192
-POOL_BATCH_MIN_DEFAULT = (1 << 32) - 1   # k_dsmp opt-in
+POOL_BATCH_MIN_DEFAULT = 1 << 19   # k_dsmp from 2^19 signatures
 FD_TXN_AMD_ERR_PARSE = -4
 FD_TXN_MAX_SZ = 3570
 

@@ -301,8 +301,8 @@ fd_ed25519_amd_sign_dev( ulong         n,
    signature, its own op per lane), or k_dsmp (one lane per signature,
    signatures pooled per wave so that a wave runs one op class at a time)
    for batches of at least fd_ed25519_amd_set_pool_batch_min signatures
-   (default ~0UL: off; measured on par with k_dsm).  All give
-   identical verdicts; 0 disables a latency kernel.  Process-wide. */
+   (default 2^19; ~0UL disables it).  All give identical verdicts; 0
+   disables a latency kernel.  Process-wide. */
 void
 fd_ed25519_amd_set_small_batch_max( ulong n );
 

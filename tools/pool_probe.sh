@@ -1,4 +1,4 @@
 #!/bin/bash
-# k_dsmp A/B: tail workgroup share (FD_POOL_TAIL_DIV: 1/div of the batch on the per-lane tail path)
+# k_dsmp A/B: DBL-step threshold variants (ab/dbg<pct>.so, FD_POOL_DEBUG builds)
 export GPU_MAX_HW_QUEUES=16
-for div in 0 32 16 8; do FD_POOL_TAIL_DIV=$div FD_AMD_LIB=$PWD/ab/dbg112.so timeout -k 10 120 python3 tools/pool_probe.py || exit 1; done
+for v in 78 70 88; do FD_AMD_LIB=$PWD/ab/dbg$v.so timeout -k 10 120 python3 tools/pool_probe.py || exit 1; done
