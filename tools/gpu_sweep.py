@@ -4,7 +4,7 @@ signed on the GPU -- byte-identical to the reference signer -- and given the
 same 10 % single-bit flips).  Every verdict is compared with the oracle run on
 the box's host cores, and each stream's code histogram with the reference's
 histogram recorded in PARITY_LOG.md.  Stream k forces kernel k % 3 (k_dsm,
-k_dsm4, k_dsm8) for every chunk.
+k_dsm4, k_dsm8) for every chunk, or FD_SWEEP_KERNEL (e.g. k_dsmp) for all.
 
 usage: python tools/gpu_sweep.py [stream indices...] > gpurun_out/sweep.jsonl
 """
@@ -43,7 +43,7 @@ def run(k):
     prv, blob, _, sz, fk, fp = _oracle.stream_inputs(rs, N, szlo, szhi, True)
     off64 = np.zeros(N, np.int64)
     off64[1:] = np.cumsum(sz[:-1], dtype=np.int64)      # the generator's u32 offsets wrap past 4 GB
-    kern = ("k_dsm", "k_dsm4", "k_dsm8")[k % 3]
+    kern = os.environ.get("FD_SWEEP_KERNEL") or ("k_dsm", "k_dsm4", "k_dsm8")[k % 3]
     ed25519.select_dsm_kernel(kern)
     eng = ed25519.Engine(device=0, batch_max=1 << 20, blob_max=(1 << 20) * max(szhi, 1))
     err = np.zeros(N, np.int8)
