@@ -132,3 +132,51 @@ def test_carry_rewrites_match_reference_chain():
         assert biased_carry(s) == r, s
         assert folded_carry(s) == r, s
         assert folded_carry_k9(s) == r, s
+
+
+# ---- squares: the column sums of fe_sq_fold2w / sq_term (fd_ed25519_dev.h) ----
+
+def _mul_cols(f, g):
+    """Column sums of fe_mul( f, g ): term (i, j) weighted x2 when i and j
+    are both odd and x19 when i + j >= 10 (avx/fd_ed25519_fe_avx_inl.h)."""
+    h = [0] * 10
+    for i in range(10):
+        for j in range(10):
+            h[(i + j) % 10] += (2 if (i & 1 and j & 1) else 1) * (19 if i + j >= 10 else 1) * f[i] * g[j]
+    return h
+
+
+def _sq_cols(f, d2):
+    """sq_term's 55 products: pair (i <= j) of column K with its power of two
+    as a shift of f_i and the 19 on f_j; every operand must fit int32."""
+    h = [0] * 10
+    for K in range(10):
+        for i in range(10):
+            j = (K - i + 10) % 10
+            if i > j:
+                continue
+            c2 = (i != j) + (1 if (i & 1 and j & 1) else 0) + (1 if d2 else 0)
+            lhs = f[i] << c2
+            rhs = 19 * f[j] if i + j >= 10 else f[j]
+            assert -(1 << 31) <= lhs < (1 << 31) and -(1 << 31) <= rhs < (1 << 31)
+            h[K] += lhs * rhs
+    return h
+
+
+def test_square_columns_equal_mul_columns():
+    """fe_sq_fold2w<D2> computes exactly the column sums of fe_mul( f, f )
+    (resp. fe_mul( f, f+f )), without wrapping an operand, for the input
+    ranges k_dsmp feeds it: |limb| <= 2^26 (X+Y of carried limbs) and
+    |limb| <= 2^25 for the sq2 input Z -- so it gives the same limbs as the
+    general product the reference's sq / sq2 equal."""
+    rng = random.Random(2025)
+    cases = [[(1 << 26)] * 10, [-(1 << 26)] * 10, [(1 << 26) * (-1) ** k for k in range(10)]]
+    cases += [[rng.randint(-(1 << 26), 1 << 26) for _ in range(10)] for _ in range(3000)]
+    for f in cases:
+        assert _sq_cols(f, False) == _mul_cols(f, f)
+        z = [max(-(1 << 25), min(1 << 25, v >> 1)) for v in f]
+        assert _sq_cols(z, True) == _mul_cols(z, [2 * v for v in z])
+    # and the sums stay inside int64 with the fold's 2^25 + 2^50 start value
+    for f in cases[:3]:
+        for v in _sq_cols(f, False):
+            assert abs(v) + (1 << 25) + (1 << 50) < (1 << 63)
