@@ -1423,6 +1423,10 @@ pool_store_ts( PTR s, u32 stride, p1p1 const & t ) {
 #ifndef FD_POOL_DBL_PCT
 #define FD_POOL_DBL_PCT 78u
 #endif
+/* free slots that trigger a refill (one counter atomic + init loads) */
+#ifndef FD_POOL_REFILL
+#define FD_POOL_REFILL 8u
+#endif
 
 __device__ __forceinline__ u32 lane_rank( u64 m ) {   /* set bits of m below this lane */
   return __builtin_amdgcn_mbcnt_hi( (u32)(m >> 32), __builtin_amdgcn_mbcnt_lo( (u32)m, 0u ) );
@@ -1468,7 +1472,7 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
     u32 nfree = (u32)(__builtin_popcountll( f0 ) + __builtin_popcountll( f1 ));
     /* refill in batches (one global round trip per 16 finished signatures),
        or whenever no class fills a wave */
-    if( more && nfree && (nfree >= 16u || (nD < 64u && nA < 64u)) ) {
+    if( more && nfree && (nfree >= FD_POOL_REFILL || (nD < 64u && nA < 64u)) ) {
 #ifdef FD_POOL_DEBUG
       dbg_idle++;
 #endif
