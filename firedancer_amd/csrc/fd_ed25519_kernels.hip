@@ -1297,7 +1297,7 @@ enum { OP_D = 0, OP_AA = 1, OP_AB = 2, OP_EMPTY = 3, OP_NONE = 4 };
 __device__ i32 g_bi12[8][48];
 #ifdef FD_POOL_DEBUG
 __device__ u32 g_pool_dbg[4];   /* steps, live lanes, ADD steps, refill-only steps (summed over waves) */
-__device__ u64 g_pool_dbg_t[8192][2];   /* per wave: wall_clock64 at start and exit */
+__device__ u64 g_pool_dbg_t[8192][4];   /* per wave: wall_clock64 at start, at exhaustion of the counter, at exit; steps after exhaustion | lanes << 32 */
 #endif
 
 __global__ void __launch_bounds__(64)
@@ -1455,7 +1455,7 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
 
   u64 mD0 = 0, mD1 = 0, mA0 = 0, mA1 = 0;
 #ifdef FD_POOL_DEBUG
-  u64 dbg_t0 = wall_clock64();
+  u64 dbg_t0 = wall_clock64(), dbg_te = 0; bool dbg_after = false; u64 dbg_sa = 0, dbg_la = 0;
 #endif
   u32 * ctr = (u32 *)(ws + L.ctr);   /* next unclaimed signature, shared by all waves */
   bool more = true;                  /* wave-uniform: the counter has not passed n */
@@ -1481,7 +1481,12 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
       u32 base = 0u;
       if( l == 0u ) base = atomicAdd( ctr, nfree );
       base = (u32)__builtin_amdgcn_readfirstlane( (int)base );
-      if( base + nfree >= n || base + nfree < base ) more = false;
+      if( base + nfree >= n || base + nfree < base ) {
+        more = false;
+#ifdef FD_POOL_DEBUG
+        dbg_te = wall_clock64(); dbg_after = true;
+#endif
+      }
       u32 pf0 = (u32)__builtin_popcountll( f0 );
       u64 s0 = (u64)base + lane_rank( f0 ), s1 = (u64)base + pf0 + lane_rank( f1 );
       bool r0 = ((f0 >> l) & 1u) && s0 < n, r1 = ((f1 >> l) & 1u) && s1 < n;
@@ -1520,6 +1525,7 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
     mA0 &= ~S0; mA1 &= ~S1; mD0 &= ~S0; mD1 &= ~S1;
 #ifdef FD_POOL_DEBUG
     dbg_steps++; dbg_lanes += nsel; dbg_add += mixed;
+    if( dbg_after ) { dbg_sa++; dbg_la += nsel; }
 #endif
     bool live = l < nsel;
     /* slot of rank l: each selected slot's owner writes it at its rank (the
@@ -1648,7 +1654,7 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
   }
 #ifdef FD_POOL_DEBUG
   if( l == 0u ) { atomicAdd( &g_pool_dbg[0], dbg_steps ); atomicAdd( &g_pool_dbg[1], dbg_lanes ); atomicAdd( &g_pool_dbg[2], dbg_add ); atomicAdd( &g_pool_dbg[3], dbg_idle ); }
-  if( l == 0u && w < 8192u ) { g_pool_dbg_t[w][0] = dbg_t0; g_pool_dbg_t[w][1] = wall_clock64(); }
+  if( l == 0u && w < 8192u ) { g_pool_dbg_t[w][0] = dbg_t0; g_pool_dbg_t[w][1] = dbg_te; g_pool_dbg_t[w][2] = wall_clock64(); g_pool_dbg_t[w][3] = dbg_sa | (dbg_la << 32); }
 #else
   (void)w;
 #endif
@@ -1664,8 +1670,8 @@ fd_amd_pool_debug( unsigned * out, int reset ) {
   return 0;
 }
 extern "C" int
-fd_amd_pool_debug_times( unsigned long * out /* [8192][2] */ ) {
-  return hipMemcpyFromSymbol( out, HIP_SYMBOL( g_pool_dbg_t ), sizeof(unsigned long)*8192*2 ) == hipSuccess ? 0 : -1;
+fd_amd_pool_debug_times( unsigned long * out /* [8192][4] */ ) {
+  return hipMemcpyFromSymbol( out, HIP_SYMBOL( g_pool_dbg_t ), sizeof(unsigned long)*8192*4 ) == hipSuccess ? 0 : -1;
 }
 #endif
 

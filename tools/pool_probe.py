@@ -54,16 +54,18 @@ for kern in ("k_dsm", "k_dsmp"):
         steps, lanes, add, idle = list(buf)
         res["pool"] = {"steps": steps, "fill": lanes / max(1, 64 * steps), "add_frac": add / max(1, steps),
                        "idle": idle}
-        tb = np.zeros((8192, 2), np.uint64)
+        tb = np.zeros((8192, 4), np.uint64)
         if L.fd_amd_pool_debug_times(ctypes.c_void_p(tb.ctypes.data)) == 0:
             W = int(os.environ.get("FD_POOL_WAVES") or 2048)
-            t = tb[:W].astype(np.float64)
-            t -= t[:, 0].min()
+            t = tb[:W, :3].astype(np.float64)
+            t0 = t[:, 0].min()
             f = 100e6 / 1e3   # wall_clock64 ticks per ms (100 MHz)
-            st, en = t[:, 0] / f, t[:, 1] / f
-            span = en.max()
-            res["waves_ms"] = {"start_p50": float(np.median(st)), "start_max": float(st.max()),
-                               "end_min": float(en.min()), "end_p50": float(np.median(en)), "end_max": float(span),
-                               "avg_resident": float((en - st).sum() / span)}
+            st, te, en = (t[:, 0] - t0) / f, (t[:, 1] - t0) / f, (t[:, 2] - t0) / f
+            sa = (tb[:W, 3] & 0xffffffff).astype(np.float64)
+            la = (tb[:W, 3] >> 32).astype(np.float64)
+            q = lambda a: [round(float(np.percentile(a, x)), 3) for x in (0, 10, 50, 90, 100)]
+            res["waves_ms"] = {"start": q(st), "exhausted": q(te), "end": q(en), "drain": q(en - te),
+                               "steps_after": q(sa), "fill_after": float(la.sum() / max(1.0, 64 * sa.sum())),
+                               "avg_resident": float((en - st).sum() / en.max())}
 ed25519.select_dsm_kernel("default")
 print(json.dumps(res), flush=True)
