@@ -311,3 +311,22 @@ def test_dropin_long_messages():
         assert ed25519.verify(msg, sig, pub) == 0 == _oracle.verify(msg, sig, pub)
         bad = bytearray(msg); bad[sz // 2] ^= 1
         assert ed25519.verify(bytes(bad), sig, pub) == _oracle.verify(bytes(bad), sig, pub) == -3
+
+
+def test_pooled_kernel_ragged_batches(golden):
+    """k_dsmp (pooled op classes) forced on ragged batch sizes: a single
+    signature, partial waves, pools that never fill, sizes around 64 and the
+    pool size (112), and the golden set; verdicts equal the reference's."""
+    from firedancer_amd import ed25519
+    ed25519.select_dsm_kernel("k_dsmp")
+    eng = ed25519.Engine(device=0, batch_max=4096, blob_max=4096 * 1232)
+    try:
+        for n in (1, 2, 63, 64, 65, 111, 112, 113, 127, 129, 1000, len(golden)):
+            n = min(n, len(golden))
+            sel = np.arange(n)
+            err = eng.verify_soa(golden.pub[sel], golden.sig[sel], golden.msg_off[sel], golden.msg_sz[sel],
+                                 golden.blob)
+            assert np.array_equal(err, golden.expect[sel]), n
+    finally:
+        eng.close()
+        ed25519.select_dsm_kernel("default")
