@@ -298,6 +298,29 @@ def test_config2_full_size_properties():
         assert _oracle.verify(bytes(blob[off[i]:off[i] + 200]), bytes(sig[i]), bytes(pub[i])) == int(outs[0][i]) == -3
 
 
+def test_config2_full_size_mixed_vs_oracle():
+    """configs[1]'s shape (2^20 x 200-B messages) with configs[2]'s 10 %
+    corruption (one bit flipped in sig, message or pub), through the device
+    path and its default kernel at this size (the pooled k_dsmp): every one
+    of the 2^20 verdicts equals the CPU oracle's."""
+    from firedancer_amd import ed25519, hip
+    n = 1 << 20
+    b = _sign_stream(20241, n, 200, 200, True)
+    d = {k: hip.DeviceBuffer.from_array(v) for k, v in
+         dict(pub=b.pub, sig=b.sig, off=b.msg_off, sz=b.msg_sz, blob=b.blob).items()}
+    err = hip.DeviceBuffer(n)
+    ws = hip.DeviceBuffer(ed25519.workspace_footprint(n))
+    st = hip.Stream()
+    ed25519.verify_dev(n, d["pub"].ptr, d["sig"].ptr, d["off"].ptr, d["sz"].ptr, d["blob"].ptr, err.ptr,
+                       ws.ptr, st.handle)
+    st.synchronize()
+    got = err.to_array(np.int8, n)
+    exp = _oracle.verify_batch(b)
+    assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:10]
+    hist = [int((exp == -k).sum()) for k in range(4)]
+    assert hist[0] > 0.85 * n and hist[2] > 0 and hist[3] > 0.05 * n, hist
+
+
 def test_dropin_long_messages():
     """The reference verifies messages of any size; the drop-in entry point
     grows its staging (64 KB .. 1 MB messages, valid and corrupted)."""
