@@ -1513,15 +1513,19 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
     u32 kD = nD < 64u ? nD : 64u, kM = (nD + nA) < 64u ? (nD + nA) : 64u;
     bool mixed = 100u * kD < FD_POOL_DBL_PCT * kM;
     u32 nsel = mixed ? kM : kD;
-    u32 aoff = mixed ? nA : 0u;                                 /* DBL ranks start after the ADDs */
-    u32 pa0 = (u32)__builtin_popcountll( mA0 ), pd0 = (u32)__builtin_popcountll( mD0 );
-    bool isA0 = (mA0 >> l) & 1u, isA1 = (mA1 >> l) & 1u, isD0 = (mD0 >> l) & 1u, isD1 = (mD1 >> l) & 1u;
-    /* owner view: rank of my slots in the selection (= their processing lane) */
-    u32 rk0 = isA0 ? lane_rank( mA0 ) : aoff + lane_rank( mD0 );
-    u32 rk1 = isA1 ? pa0 + lane_rank( mA1 ) : aoff + pd0 + lane_rank( mD1 );
-    bool in0 = (isD0 || (mixed && isA0)) && rk0 < 64u;
-    bool in1 = (isD1 || (mixed && isA1)) && rk1 < 64u;
-    u64 S0 = __builtin_amdgcn_ballot_w64( in0 ), S1 = __builtin_amdgcn_ballot_w64( in1 );
+    /* owner view: the rank of my slots in the selection order [ADD slots
+       0..63, ADD slots 64.., DBL slots 0..63, DBL slots 64..] (ADDs only in a
+       mixed step) is their processing lane.  Class bits are the wave-uniform
+       masks used as lane masks (inverse ballot, v_cndmask): no per-lane
+       shifts of the masks. */
+    u64 const sA0 = mixed ? mA0 : 0UL, sA1 = mixed ? mA1 : 0UL;
+    u32 const aoff = mixed ? nA : 0u;                           /* DBL ranks start after the ADDs */
+    u32 const pa0 = (u32)__builtin_popcountll( sA0 ), pd0 = (u32)__builtin_popcountll( mD0 );
+    u32 rk0 = (u32)vsel( sA0, (i32)lane_rank( sA0 ), (i32)(aoff + lane_rank( mD0 )) );
+    u32 rk1 = (u32)vsel( sA1, (i32)(pa0 + lane_rank( sA1 )), (i32)(aoff + pd0 + lane_rank( mD1 )) );
+    u64 S0 = (sA0 | mD0) & __builtin_amdgcn_ballot_w64( rk0 < 64u );
+    u64 S1 = (sA1 | mD1) & __builtin_amdgcn_ballot_w64( rk1 < 64u );
+    bool in0 = __builtin_amdgcn_inverse_ballot_w64( S0 ), in1 = __builtin_amdgcn_inverse_ballot_w64( S1 );
     mA0 &= ~S0; mA1 &= ~S1; mD0 &= ~S0; mD1 &= ~S1;
 #ifdef FD_POOL_DEBUG
     dbg_steps++; dbg_lanes += nsel; dbg_add += mixed;
@@ -1627,16 +1631,20 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
       }
     }
 
-    /* advance the op stream: pop the consumed event, then the next op */
-    u32 nop = (u32)OP_EMPTY;
+    /* advance the op stream: pop the consumed event, then the next op
+       (branch-free: every select is a lane mask) */
+    bool const isAA = op == OP_AA, isAB = op == OP_AB, isDb = op == OP_D;
+    {
+      u32 ev = __builtin_amdgcn_ubfe( nh, (pidx & 1u) << 4, 16u );
+      ja -= (u32)isAA; jb -= (u32)isAB;
+      hA = isAA ? (ja ? ev : 0xffffu) : hA;
+      hB = isAB ? (jb ? ev : 0xffffu) : hB;
+    }
+    bool const toAA = isDb && hA != 0xffffu && (hA & 0xffu) == (u32)p;
+    bool const toAB = !toAA && (isDb || isAA) && hB != 0xffffu && (hB & 0xffu) == (u32)p;
+    p -= (int)!(toAA || toAB);
+    u32 nop = !live ? (u32)OP_EMPTY : toAA ? (u32)OP_AA : toAB ? (u32)OP_AB : (p < 0) ? (u32)OP_EMPTY : (u32)OP_D;
     if( live ) {
-      u32 ev = (nh >> ((pidx & 1u) << 4)) & 0xffffu;
-      if( op == OP_AA ) { ja--; hA = ja ? ev : 0xffffu; } else if( op == OP_AB ) { jb--; hB = jb ? ev : 0xffffu; }
-      int posA = (hA == 0xffffu) ? -1 : (int)(hA & 0xffu);
-      int posB = (hB == 0xffffu) ? -1 : (int)(hB & 0xffu);
-      if( op == OP_D && posA == p )                       nop = OP_AA;
-      else if( (op == OP_D || op == OP_AA) && posB == p ) nop = OP_AB;
-      else { p--; nop = (p < 0) ? (u32)OP_EMPTY : (u32)OP_D; }
       if( nop == OP_EMPTY ) {
         pool_store_t( (int4 *)(Ai + (size_t)si*384u), t );   /* park the final p1p1 for k_fin */
       } else {
@@ -1647,10 +1655,10 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
     /* the slots' new classes, at their owner lanes */
     u32 v0 = (u32)__builtin_amdgcn_ds_bpermute( (int)(rk0 << 2), (int)nop );
     u32 v1 = (u32)__builtin_amdgcn_ds_bpermute( (int)((rk1 & 63u) << 2), (int)nop );
-    mD0 |= __builtin_amdgcn_ballot_w64( in0 && v0 == OP_D );
-    mA0 |= __builtin_amdgcn_ballot_w64( in0 && (v0 == OP_AA || v0 == OP_AB) );
-    mD1 |= __builtin_amdgcn_ballot_w64( in1 && v1 == OP_D );
-    mA1 |= __builtin_amdgcn_ballot_w64( in1 && (v1 == OP_AA || v1 == OP_AB) );
+    u64 const d0 = __builtin_amdgcn_ballot_w64( v0 == OP_D ), d1 = __builtin_amdgcn_ballot_w64( v1 == OP_D );
+    u64 const x0 = __builtin_amdgcn_ballot_w64( v0 < OP_EMPTY ), x1 = __builtin_amdgcn_ballot_w64( v1 < OP_EMPTY );
+    mD0 |= S0 & d0; mA0 |= S0 & x0 & ~d0;                       /* OP_AA / OP_AB: below OP_EMPTY, not OP_D */
+    mD1 |= S1 & d1; mA1 |= S1 & x1 & ~d1;
   }
 #ifdef FD_POOL_DEBUG
   if( l == 0u ) { atomicAdd( &g_pool_dbg[0], dbg_steps ); atomicAdd( &g_pool_dbg[1], dbg_lanes ); atomicAdd( &g_pool_dbg[2], dbg_add ); atomicAdd( &g_pool_dbg[3], dbg_idle ); }
