@@ -48,6 +48,7 @@ def hip():
     H.hipEventDestroy.argtypes = [vp]
     H.hipEventRecord.argtypes = [vp, vp]
     H.hipEventSynchronize.argtypes = [vp]
+    H.hipStreamWaitEvent.argtypes = [vp, vp, u]
     H.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), vp, vp]
     H.hipHostMalloc.argtypes = [ctypes.POINTER(vp), sz, u]
     H.hipHostFree.argtypes = [vp]
@@ -179,6 +180,10 @@ class Stream:
 
     def synchronize(self):
         check(hip().hipStreamSynchronize(self.handle), "hipStreamSynchronize")
+
+    def wait(self, event):
+        """Later work on this stream waits for `event`'s latest record."""
+        check(hip().hipStreamWaitEvent(self.handle, event.handle, 0), "hipStreamWaitEvent")
 
     def destroy(self):
         if self.handle:
