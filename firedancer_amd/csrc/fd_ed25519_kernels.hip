@@ -1428,6 +1428,7 @@ pool_store_ts( PTR s, u32 stride, p1p1 const & t ) {
 #define FD_POOL_REFILL 8u
 #endif
 
+
 __device__ __forceinline__ u32 lane_rank( u64 m ) {   /* set bits of m below this lane */
   return __builtin_amdgcn_mbcnt_hi( (u32)(m >> 32), __builtin_amdgcn_mbcnt_lo( (u32)m, 0u ) );
 }
@@ -1505,26 +1506,62 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
       continue;
     }
 
-    /* the step: a pure DBL step (p2 + 4 squares) on up to 64 DBL slots, or
-       a MIXED step (k_dsm's uniform 8-mul step) that takes every ADD slot
-       first and fills the rest with DBL slots.  An ADD op costs the same in
-       either, so ADDs always go through mixed steps; a DBL step wins while
-       it is nearly as full as a mixed one (cost ratio ~0.78, measured). */
     u32 kD = nD < 64u ? nD : 64u, kM = (nD + nA) < 64u ? (nD + nA) : 64u;
-    bool mixed = 100u * kD < FD_POOL_DBL_PCT * kM;
-    u32 nsel = mixed ? kM : kD;
-    /* owner view: the rank of my slots in the selection order [ADD slots
-       0..63, ADD slots 64.., DBL slots 0..63, DBL slots 64..] (ADDs only in a
-       mixed step) is their processing lane.  Class bits are the wave-uniform
-       masks used as lane masks (inverse ballot, v_cndmask): no per-lane
-       shifts of the masks. */
-    u64 const sA0 = mixed ? mA0 : 0UL, sA1 = mixed ? mA1 : 0UL;
-    u32 const aoff = mixed ? nA : 0u;                           /* DBL ranks start after the ADDs */
-    u32 const pa0 = (u32)__builtin_popcountll( sA0 ), pd0 = (u32)__builtin_popcountll( mD0 );
-    u32 rk0 = (u32)vsel( sA0, (i32)lane_rank( sA0 ), (i32)(aoff + lane_rank( mD0 )) );
-    u32 rk1 = (u32)vsel( sA1, (i32)(pa0 + lane_rank( sA1 )), (i32)(aoff + pd0 + lane_rank( mD1 )) );
-    u64 S0 = (sA0 | mD0) & __builtin_amdgcn_ballot_w64( rk0 < 64u );
-    u64 S1 = (sA1 | mD1) & __builtin_amdgcn_ballot_w64( rk1 < 64u );
+    bool mixed;
+    u32 nsel, rk0, rk1;
+    u64 S0, S1;
+    if( !more ) {
+      /* drain (nothing left to claim): the pool's last signatures set the
+         launch's end.  The class is chosen as in the main phase; within it
+         the (up to) 64 slots with the most ops left, p + ja + jb (remaining
+         doublings and adds), go first -- in a mixed step every ADD slot
+         ranks above every DBL slot.  A threshold search on those counts (10
+         ballots) finds the 64th largest; ties go in slot order.  (Slot
+         order alone left the youngest signatures waiting: 393 / 620 steps
+         after the counter ran out, median / max, vs 382 / 479.) */
+      mixed = 100u * kD < FD_POOL_DBL_PCT * kM;
+      u64 const L0 = mixed ? (mA0 | mD0) : mD0, L1 = mixed ? (mA1 | mD1) : mD1;
+      u32 const K = mixed ? kM : kD;
+      u32 const z0 = s_m[l].z, z1 = s_m[l + 64u < P ? l + 64u : l].z;
+      u32 const r0 = (z0 & 0xffffu) + ((z0 >> 16) & 0xffu) + (z0 >> 24) + (u32)vsel( mixed ? mA0 : 0UL, 512, 0 );
+      u32 const r1 = (z1 & 0xffffu) + ((z1 >> 16) & 0xffu) + (z1 >> 24) + (u32)vsel( mixed ? mA1 : 0UL, 512, 0 );
+      u32 T = 0u;
+      _Pragma("unroll") for( int b=9; b>=0; b-- ) {   /* keys are below 1024 */
+        u32 const Tb = T | (1u << b);
+        u32 const c = (u32)(__builtin_popcountll( L0 & __builtin_amdgcn_ballot_w64( r0 >= Tb ) ) +
+                            __builtin_popcountll( L1 & __builtin_amdgcn_ballot_w64( r1 >= Tb ) ));
+        T = c >= K ? Tb : T;
+      }
+      u64 const G0 = L0 & __builtin_amdgcn_ballot_w64( r0 > T ), G1 = L1 & __builtin_amdgcn_ballot_w64( r1 > T );
+      u64 const E0 = L0 & ~G0 & __builtin_amdgcn_ballot_w64( r0 >= T ), E1 = L1 & ~G1 & __builtin_amdgcn_ballot_w64( r1 >= T );
+      u32 const need = K - (u32)(__builtin_popcountll( G0 ) + __builtin_popcountll( G1 ));
+      u32 const e0 = (u32)__builtin_popcountll( E0 );
+      S0 = G0 | (E0 & __builtin_amdgcn_ballot_w64( lane_rank( E0 ) < need ));
+      S1 = G1 | (E1 & __builtin_amdgcn_ballot_w64( e0 + lane_rank( E1 ) < need ));
+      rk0 = lane_rank( S0 ); rk1 = (u32)__builtin_popcountll( S0 ) + lane_rank( S1 );
+      nsel = K;
+    } else {
+      /* the step: a pure DBL step (p2 + 4 squares) on up to 64 DBL slots,
+         or a MIXED step (k_dsm's uniform 8-mul step) that takes every ADD
+         slot first and fills the rest with DBL slots.  An ADD op costs the
+         same in either, so ADDs always go through mixed steps; a DBL step
+         wins while it is nearly as full as a mixed one (cost ratio ~0.78,
+         measured). */
+      mixed = 100u * kD < FD_POOL_DBL_PCT * kM;
+      nsel = mixed ? kM : kD;
+      /* owner view: the rank of my slots in the selection order [ADD slots
+         0..63, ADD slots 64.., DBL slots 0..63, DBL slots 64..] (ADDs only
+         in a mixed step) is their processing lane.  Class bits are the
+         wave-uniform masks used as lane masks (inverse ballot, v_cndmask):
+         no per-lane shifts of the masks. */
+      u64 const sA0 = mixed ? mA0 : 0UL, sA1 = mixed ? mA1 : 0UL;
+      u32 const aoff = mixed ? nA : 0u;                         /* DBL ranks start after the ADDs */
+      u32 const pa0 = (u32)__builtin_popcountll( sA0 ), pd0 = (u32)__builtin_popcountll( mD0 );
+      rk0 = (u32)vsel( sA0, (i32)lane_rank( sA0 ), (i32)(aoff + lane_rank( mD0 )) );
+      rk1 = (u32)vsel( sA1, (i32)(pa0 + lane_rank( sA1 )), (i32)(aoff + pd0 + lane_rank( mD1 )) );
+      S0 = (sA0 | mD0) & __builtin_amdgcn_ballot_w64( rk0 < 64u );
+      S1 = (sA1 | mD1) & __builtin_amdgcn_ballot_w64( rk1 < 64u );
+    }
     bool in0 = __builtin_amdgcn_inverse_ballot_w64( S0 ), in1 = __builtin_amdgcn_inverse_ballot_w64( S1 );
     mA0 &= ~S0; mA1 &= ~S1; mD0 &= ~S0; mD1 &= ~S1;
 #ifdef FD_POOL_DEBUG
