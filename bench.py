@@ -9,8 +9,10 @@ k_decomp -> the double-scalar multiply: k_ai + k_dsmp + k_fin at this size)
 over one batch of n synthetic signatures (2^20 single-signer signatures,
 200-byte Solana-txn-sized messages, fresh random keypairs), with the inputs
 already resident in HBM when the timed region starts.  Consecutive steps
-alternate between --streams (default 2) stream/workspace sets, as the
-engine keeps two chunks in flight.  For N > 1 (launched by torch.distributed.run) every rank verifies
+alternate between --streams (default 3) stream/workspace sets: three
+batches in flight (measured +2 % over two: a batch's multiply starts in the
+previous one's drain and the fronts queue behind fewer multiplies;
+profiles/r02_k_dsmp_pool_ab.txt).  For N > 1 (launched by torch.distributed.run) every rank verifies
 its own batch of n signatures on its own GPU -- signatures are independent,
 so there is no data-path collective (weak scaling); gloo is used only for
 the start/stop barriers and the max-over-ranks of the time.
@@ -78,8 +80,8 @@ def parse():
     ap.add_argument("--msg-sz", type=int, default=200)
     ap.add_argument("--dsm-kernel", choices=("default", "k_dsm", "k_dsmp"), default="default",
                     help="throughput double-scalar-mult kernel (A/B; default: the library's size rule)")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="batches in flight (consecutive steps alternate streams, as the engine's chunks do)")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="batches in flight (consecutive steps alternate streams / workspaces)")
     ap.add_argument("--total-sigs", type=int, default=1 << 24,
                     help="txn workload: signatures over all ranks (strong scaling)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
@@ -440,8 +442,8 @@ def main():
     d = {k: hip.DeviceBuffer.from_array(v) for k, v in
          dict(pub=pub, sig=sig, off=off, sz=sz, blob=blob).items()}
     # consecutive steps alternate between `streams` (stream, verdicts,
-    # workspace) sets, as the engine keeps two chunks in flight: one batch's
-    # hashing/decompression fills the SIMDs the previous batch's last
+    # workspace) sets, batches in flight: one batch's hashing/decompression
+    # and the start of its multiply fill the SIMDs the previous batch's last
     # double-scalar-mult waves leave idle
     ns = max(1, args.streams)
     sets = [(hip.Stream(), hip.DeviceBuffer(n), hip.DeviceBuffer(ed25519.workspace_footprint(n))) for _ in range(ns)]
