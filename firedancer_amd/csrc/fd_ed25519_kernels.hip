@@ -821,15 +821,18 @@ quad_cached_row( p3 const & u, u64 m1, u64 m2 ) {
 
 __global__ void __launch_bounds__(64)
 k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats ) {
-  __shared__ i32 bi[8][40];
-  for( int k=threadIdx.x; k<8*40; k+=64 ) {
-    int e = k / 40, c = (k % 40) / 10, l = k % 10;
-    i32 v;
-    if( c == 0 ) v = (l == 0);
-    else if( c == 1 ) v = BI_TABLE[e][1][l];
-    else if( c == 2 ) v = BI_TABLE[e][0][l];
-    else v = BI_TABLE[e][2][l];
-    bi[e][c*10 + l] = v;
+  /* the base-point table in the Ai slab's row layout (see k_dsm8) */
+  __shared__ __attribute__((aligned(16))) i32 bi12[8][48];
+  for( int k=threadIdx.x; k<8*48; k+=64 ) {
+    int e = k / 48, c = (k % 48) / 12, l = k % 12;
+    i32 v = 0;
+    if( l < 10 ) {
+      if( c == 0 ) v = (l == 0);
+      else if( c == 1 ) v = BI_TABLE[e][1][l];
+      else if( c == 2 ) v = BI_TABLE[e][0][l];
+      else v = BI_TABLE[e][2][l];
+    }
+    bi12[e][k % 48] = v;
   }
   __syncthreads();
 
@@ -927,39 +930,29 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
 
     /* the event just executed is consumed; the next op follows from the
        event heads (an event at position p means a digit at p) */
-    if( ph == PH_ADDA ) eva.pop();
-    else if( ph == PH_ADDB ) evb.pop();
-    bool ha = eva.pos == p, hb = evb.pos == p;
-    int da = eva.dig, db = evb.dig;
-    int nph;
-    if( ph == PH_DBL )       nph = ha ? PH_ADDA : (hb ? PH_ADDB : -1);
-    else if( ph == PH_ADDA ) nph = hb ? PH_ADDB : -1;
-    else if( ph == PH_ADDB ) nph = -1;
-    else                     nph = PH_DONE;
-    if( nph == -1 ) {
-      p--;
-      nph = (p < 0) ? PH_FIN : PH_DBL;
-    }
-    ph = nph;
+    /* branch-free, as in k_dsm8 */
+    bool const wasA = ph == PH_ADDA, wasB = ph == PH_ADDB, wasD = ph == PH_DBL;
+    eva.j -= (int)wasA; evb.j -= (int)wasB;
+    eva.load(); evb.load();
+    bool const toA = wasD && eva.pos == p;
+    bool const toB = !toA && (wasD || wasA) && evb.pos == p;
+    bool const adv = (wasD || wasA || wasB) && !toA && !toB;
+    p -= (int)adv;
+    ph = toA ? PH_ADDA : toB ? PH_ADDB : adv ? ((p < 0) ? PH_FIN : PH_DBL) : ph;
+    nha += (u32)toA; nhb += (u32)toB;
 
     /* this lane's row of the next op's operand: q0 qP, q1 qM, q2 qZ, q3 qT;
        rows of an entry are [Z, Y-X, Y+X, 2dT], a negative digit swaps Y-X/Y+X */
-    if( ph == PH_ADDA || ph == PH_ADDB ) {
-      int d = (ph == PH_ADDA) ? da : db;
-      int e = (d < 0 ? -d : d) >> 1;
+    {
+      int const d = toA ? eva.dig : evb.dig;
+      int const e = ((d < 0 ? -d : d) >> 1) & 7;
       qneg = d < 0;
-      int row = (qd == 0) ? (qneg ? 1 : 2) : (qd == 1) ? (qneg ? 2 : 1) : (qd == 2) ? 0 : 3;
-      if( ph == PH_ADDA ) {
-        nha++;
-        int4 const * src = (int4 const *)(Ail + e*48 + row*12);
-        int4 x0 = src[0], x1 = src[1], x2 = src[2];
-        qrow.v[0] = x0.x; qrow.v[1] = x0.y; qrow.v[2] = x0.z; qrow.v[3] = x0.w;
-        qrow.v[4] = x1.x; qrow.v[5] = x1.y; qrow.v[6] = x1.z; qrow.v[7] = x1.w;
-        qrow.v[8] = x2.x; qrow.v[9] = x2.y;
-      } else {
-        nhb++;
-        _Pragma("unroll") for( int k=0; k<10; k++ ) qrow.v[k] = bi[e][row*10 + k];
-      }
+      int const row = (qd == 0) ? (qneg ? 1 : 2) : (qd == 1) ? (qneg ? 2 : 1) : (qd == 2) ? 0 : 3;
+      int4 const * src = toA ? (int4 const *)(Ail + e*48 + row*12) : (int4 const *)&bi12[e][row*12];
+      int4 x0 = src[0], x1 = src[1], x2 = src[2];
+      qrow.v[0] = x0.x; qrow.v[1] = x0.y; qrow.v[2] = x0.z; qrow.v[3] = x0.w;
+      qrow.v[4] = x1.x; qrow.v[5] = x1.y; qrow.v[6] = x1.z; qrow.v[7] = x1.w;
+      qrow.v[8] = x2.x; qrow.v[9] = x2.y;
     }
   }
 
