@@ -438,15 +438,18 @@ struct evq {
  */
 __device__ __forceinline__ void
 dsm_lane_body( u32 i, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats,
-               i32 (* __restrict__ bi)[40], u64 (* __restrict__ evl)[33] ) {
-  for( int k=threadIdx.x; k<8*40; k+=64 ) {
-    int e = k / 40, c = (k % 40) / 10, l = k % 10;
+               i32 (* __restrict__ bi)[48], u64 (* __restrict__ evl)[33] ) {
+  /* the base-point table in the Ai slab's row layout (rows [Z = 1 | Y-X |
+     Y+X | 2dT] x 12 limbs), so ADD-A and ADD-B operands load alike */
+  for( int k=threadIdx.x; k<8*48; k+=64 ) {
+    int e = k / 48, c = (k % 48) / 12, l = k % 12;
     i32 v;
-    if( c == 0 ) v = (l == 0);                         /* Z = 1 */
+    if( l >= 10 ) v = 0;
+    else if( c == 0 ) v = (l == 0);                    /* Z = 1 */
     else if( c == 1 ) v = BI_TABLE[e][1][l];           /* Y-X */
     else if( c == 2 ) v = BI_TABLE[e][0][l];           /* Y+X */
     else v = BI_TABLE[e][2][l];                        /* 2dxy */
-    bi[e][c*10 + l] = v;
+    bi[e][k % 48] = v;
   }
   __syncthreads();
 
@@ -593,28 +596,25 @@ dsm_lane_body( u32 i, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_lay
 
     /* advance the lane's op stream: the event just executed is consumed; the next op follows from the
        event heads (an event at position p means a digit at p) */
-    if( ph == PH_ADDA ) eva.pop();
-    else if( ph == PH_ADDB ) evb.pop();
-    bool ha = eva.pos == p, hb = evb.pos == p;
-    int da = eva.dig, db = evb.dig;
-    int nph;
-    if( ph == PH_DBL )       nph = ha ? PH_ADDA : (hb ? PH_ADDB : -1);
-    else if( ph == PH_ADDA ) nph = hb ? PH_ADDB : -1;
-    else if( ph == PH_ADDB ) nph = -1;
-    else                     nph = PH_DONE;
-    if( nph == -1 ) {
-      p--;
-      nph = (p < 0) ? PH_FIN : PH_DBL;
-    }
-    ph = nph;
+    bool const wasA = ph == PH_ADDA, wasB = ph == PH_ADDB, wasD = ph == PH_DBL;
+    eva.j -= (int)wasA; evb.j -= (int)wasB;
+    eva.load(); evb.load();
+    bool const toA = wasD && eva.pos == p;
+    bool const toB = !toA && (wasD || wasA) && evb.pos == p;
+    bool const adv = (wasD || wasA || wasB) && !toA && !toB;
+    p -= (int)adv;
+    ph = toA ? PH_ADDA : toB ? PH_ADDB : adv ? ((p < 0) ? PH_FIN : PH_DBL) : ph;
+    nha += (u32)toA; nhb += (u32)toB;
 
-    /* stage the next op's operand into qs (consumed after the next
-       p1p1->p3, so the DMA latency hides under 4 field muls) */
-    if( ph == PH_ADDA ) {
-      nha++;
-      int e = (da < 0 ? -da : da) >> 1;
-      qneg = da < 0;
-      int4 const * src = (int4 const *)(Ail + e*48);
+    /* stage the next op's operand into q (consumed after the next
+       p1p1->p3, so the load latency hides under 4 field muls); every lane
+       loads, only an ADD reads it; ADD-A from the Ai slab, ADD-B from the
+       LDS table, through one generic pointer (no branch) */
+    {
+      int const d = toA ? eva.dig : evb.dig;
+      int const e = ((d < 0 ? -d : d) >> 1) & 7;
+      qneg = d < 0;
+      int4 const * src = toA ? (int4 const *)(Ail + e*48) : (int4 const *)&bi[e][0];
       int rowM = qneg ? 2 : 1, rowP = qneg ? 1 : 2;
 #     define Q_ROW( r, c ) do {                                                      \
         int4 x0 = src[3*(c)], x1 = src[3*(c)+1], x2 = src[3*(c)+2];                \
@@ -624,17 +624,6 @@ dsm_lane_body( u32 i, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_lay
       } while(0)
       Q_ROW( 0, 0 ); Q_ROW( 1, rowM ); Q_ROW( 2, rowP ); Q_ROW( 3, 3 );
 #     undef Q_ROW
-    } else if( ph == PH_ADDB ) {
-      nhb++;
-      int e = (db < 0 ? -db : db) >> 1;
-      qneg = db < 0;
-      int oM = qneg ? 20 : 10, oP = qneg ? 10 : 20;
-      _Pragma("unroll") for( int k=0; k<10; k++ ) {
-        Q_SET( 0, k, bi[e][k] );
-        Q_SET( 1, k, bi[e][oM + k] );
-        Q_SET( 2, k, bi[e][oP + k] );
-        Q_SET( 3, k, bi[e][30 + k] );
-      }
     }
   }
 # undef QV
@@ -663,7 +652,7 @@ dsm_lane_body( u32 i, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_lay
 
 __global__ void __launch_bounds__(64)
 k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats ) {
-  __shared__ i32 bi[8][40];
+  __shared__ __attribute__((aligned(16))) i32 bi[8][48];
   __shared__ u64 evl[64][33];
   dsm_lane_body( blockIdx.x * 64u + threadIdx.x, n, err, ws, L, want_stats, bi, evl );
 }
