@@ -539,7 +539,7 @@ def main():
         lat = np.array(lat[3:])
         out["latency_ms_4096"] = {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
                                   "path": "host SoA -> packed pinned staging (read in place by k_front) -> k_front -> "
-                                          "k_dsm4 -> verdicts through mapped memory"}
+                                          "k_dsm8 -> verdicts through mapped memory"}
         # the same batches from registered caller memory: k_front reads the
         # caller's planes in place, no copy on either side
         reg = ed25519.RegisteredPlanes(pub, sig, off, sz, blob)
@@ -556,7 +556,7 @@ def main():
         lat = np.array(lat[3:])
         out["latency_ms_4096_registered"] = {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
                                              "path": "registered caller SoA (fd_ed25519_amd_verify_soa_registered) read "
-                                                     "in place by k_front -> k_dsm4 -> verdicts through mapped memory"}
+                                                     "in place by k_front -> k_dsm8 -> verdicts through mapped memory"}
         # the reference's drop-in entry point, one signature per call (the
         # verify tile's calling pattern, fd_frank_verify_synth_load.c:380)
         calls = []
@@ -571,7 +571,7 @@ def main():
         out["dropin_call_us"] = {"p50": float(np.percentile(calls, 50)), "p99": float(np.percentile(calls, 99)),
                                  "reference_us_per_call_survey": REF_US_PER_CALL_SURVEY,
                                  "path": "fd_ed25519_verify: one signature per call, a GPU batch of one "
-                                         "(packed staging -> k_front -> k_dsm4 -> mapped result)"}
+                                         "(packed staging -> k_front -> k_dsm8 -> mapped result)"}
         # PCIe-inclusive rates: the same 2^20 batch handed over as host SoA
         # buffers, chunks of 2^17 with 2 in flight, priced against the
         # measured pinned H2D ceiling.  Never the headline value.
