@@ -987,13 +987,21 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
  * 64-bit column sums are swapped between the two lanes with DPP
  * row_shl/row_shr 4 under bank masks, and both lanes finish the reference
  * carry chain (fe_carry_b on pre-biased sums): the same limbs as fe_mul. */
-struct half_t { u64 mH; i32 shF; i64 bias; };
+#ifndef FD_DSM8_SPLIT
+#define FD_DSM8_SPLIT 1
+#endif
+struct half_t { u64 mH; i32 shF; i64 bias; i64 m4, k5; u32 shz, mo0; i32 bo0; };
 __device__ __forceinline__ half_t half_ctx( int hh ) {
   half_t H;
   H.mH = __builtin_amdgcn_ballot_w64( hh != 0 );
   H.shF = hh ? 0 : 1;
   H.bias = hh ? (1L<<24) : (1L<<25);
-  asm( "" : "+v"(H.shF) );
+  H.m4  = hh ? -1L : (1L<<26) - 1;           /* split carry (fe_mul_half5): see there */
+  H.k5  = hh ? -1L : 0L;
+  H.shz = hh ? 25u : 0u;
+  H.mo0 = hh ? (1u<<25) - 1u : (1u<<26) - 1u;
+  H.bo0 = hh ? (1<<24) : (1<<25);
+  asm( "" : "+v"(H.shF), "+v"(H.m4), "+v"(H.k5), "+v"(H.shz), "+v"(H.mo0), "+v"(H.bo0) );
   return H;
 }
 
@@ -1031,6 +1039,123 @@ fe_mul_half( fe const & F, fe const & G, half_t const & H ) {
     O[c] = (i64)(((u64)half_from_hi( hi ) << 32) | half_from_hi( lo ));
   }
   return fe_carry_b( E[0], O[0], E[1], O[1], E[2], O[2], E[3], O[3], E[4], O[4] );
+}
+
+/* Split-carry form of fe_mul_half: the two lanes of a pair run the two
+   halves of the reference carry chain side by side instead of both running
+   all of it, and each returns five limbs (fe5); fe_join5 makes the full
+   element when an operation needs it.  The chain of fe_carry_b is two
+   interleaved runs, 0->1->2->3->(4) and 4->5->6->7->8->9->(0); in slots
+   s0..s5 lane h = 0 holds h0..h4 (s5 = 0) and lane h = 1 holds h4..h9, so
+   one instruction stream advances both runs (the widths 26,25,26,25,26
+   agree; only the mask of step 4 differs: t4 = (h4 & M26) + h3>>25 on
+   h = 0, h8 += h7>>25 on h = 1).  The two cross terms, c4b into limb 5 and
+   h9>>25 into limb 0, are swapped with DPP after the run.  Limbs out:
+   h = 0 -> (r0, r1, r2, r3, r4), h = 1 -> (r9, r5, r6, r7, r8).  The same
+   limbs as fe_carry_b, so the same as the reference's fe_mul. */
+struct fe5 { i32 v[5]; };
+
+__device__ __forceinline__ i64 dpp64_from_lo( i64 old, i64 src ) {   /* h = 1 lanes take lane - 4's src */
+  u32 lo = (u32)__builtin_amdgcn_update_dpp( (int)(u32)old, (int)(u32)src, 0x114, 0xf, 0xa, false );
+  u32 hi = (u32)__builtin_amdgcn_update_dpp( (int)(u32)((u64)old >> 32), (int)(u32)((u64)src >> 32), 0x114, 0xf, 0xa, false );
+  return (i64)(((u64)hi << 32) | lo);
+}
+__device__ __forceinline__ i64 dpp64_from_hi( i64 old, i64 src ) {   /* h = 0 lanes take lane + 4's src */
+  u32 lo = (u32)__builtin_amdgcn_update_dpp( (int)(u32)old, (int)(u32)src, 0x104, 0xf, 0x5, false );
+  u32 hi = (u32)__builtin_amdgcn_update_dpp( (int)(u32)((u64)old >> 32), (int)(u32)((u64)src >> 32), 0x104, 0xf, 0x5, false );
+  return (i64)(((u64)hi << 32) | lo);
+}
+
+__device__ __forceinline__ fe5
+fe_mul_half5( fe const & F, fe const & G, half_t const & H ) {
+  i32 gs[9], g19[10], f2[10];
+  _Pragma("unroll") for( int j=0; j<9; j++ ) gs[j] = vsel( H.mH, G.v[j+1], G.v[j] );
+  _Pragma("unroll") for( int j=1; j<9; j++ ) g19[j] = wmul( gs[j], 19 );
+  g19[9] = vsel( H.mH, G.v[0], wmul( G.v[9], 19 ) );
+  _Pragma("unroll") for( int i=1; i<10; i+=2 ) f2[i] = (i32)((u32)F.v[i] << (u32)H.shF);
+  i64 a[5];
+  _Pragma("unroll") for( int c=0; c<5; c++ ) a[c] = H.bias;
+  _Pragma("unroll") for( int i=0; i<10; i++ ) {
+    _Pragma("unroll") for( int c=0; c<5; c++ ) {
+      int j = 2*c - i;
+      i32 g = (j >= 0) ? gs[j] : g19[j + 10];
+      i32 f = (i & 1) ? f2[i] : F.v[i];
+      a[c] = mac( f, g, a[c] );
+    }
+  }
+  /* a[c] is column 2c (h = 0) or 2c+1 (h = 1), pre-biased */
+  i64 s1 = dpp64_from_hi( a[2], a[0] );    /* h1 | h5 */
+  i64 s0 = dpp64_from_lo( a[0], a[2] );    /* h0 | h4 */
+  i64 s2 = dpp64_from_lo( a[1], a[3] );    /* h2 | h6 */
+  i64 s3 = dpp64_from_hi( a[3], a[1] );    /* h3 | h7 */
+  i64 s4 = dpp64_from_lo( a[2], a[4] );    /* h4 | h8 */
+  i64 s5 = a[4] & H.k5;                    /* 0  | h9 */
+  s1 += s0 >> 26;
+  s2 += s1 >> 25;
+  s3 += s2 >> 26;
+  s4 = (s4 & H.m4) + (s3 >> 25);           /* t4 | h8 */
+  s5 += s4 >> 26;                          /* c4b | h9 */
+  i64 const y = s5 >> H.shz;               /* c4b | h9 >> 25 */
+  u32 const ylo = (u32)y, yhi = (u32)((u64)y >> 32);
+  u32 zl = (u32)__builtin_amdgcn_update_dpp( (int)ylo, (int)ylo, 0x104, 0xf, 0x5, false );
+  zl = (u32)__builtin_amdgcn_update_dpp( (int)zl, (int)ylo, 0x114, 0xf, 0xa, false );
+  u32 const zh = (u32)__builtin_amdgcn_update_dpp( (int)yhi, (int)yhi, 0x104, 0xf, 0x5, false );
+  i64 const z = (i64)(((u64)zh << 32) | zl);   /* h = 0: h9 >> 25; h = 1: c4b (low word) */
+  i64 const t0 = (s0 & ((1L<<26) - 1)) + z * 19;
+  i32 const cin = vsel( H.mH, (i32)zl, (i32)(t0 >> 26) );
+  u32 const w0 = (u32)vsel( H.mH, (i32)(u32)s5, (i32)(u32)t0 );
+  fe5 o;
+  o.v[0] = (i32)(w0 & H.mo0) - H.bo0;
+  o.v[1] = (i32)((u32)s1 & ((1u<<25) - 1u)) - (1<<24) + cin;
+  o.v[2] = (i32)((u32)s2 & ((1u<<26) - 1u)) - (1<<25);
+  o.v[3] = (i32)((u32)s3 & ((1u<<25) - 1u)) - (1<<24);
+  o.v[4] = (i32)((u32)s4 & ((1u<<26) - 1u)) - (1<<25);
+  return o;
+}
+
+__device__ __forceinline__ fe fe_join5( fe5 const & o ) {
+  fe r;
+  r.v[0] = (i32)half_from_lo( (u32)o.v[0] );
+  r.v[9] = (i32)half_from_hi( (u32)o.v[0] );
+  _Pragma("unroll") for( int k=1; k<5; k++ ) {
+    r.v[k]   = (i32)half_from_lo( (u32)o.v[k] );
+    r.v[k+4] = (i32)half_from_hi( (u32)o.v[k] );
+  }
+  return r;
+}
+
+__device__ __forceinline__ fe5
+quad8_p3_ownc5( fe const & C, half_t const & H ) {
+  fe a, b;
+  _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = qp<0,0,2,2>( C.v[k] ); b.v[k] = qp<1,3,1,3>( C.v[k] ); }
+  return fe_mul_half5( a, b, H );
+}
+
+/* quad8_body_ownc on split limbs: every per-limb step (the operand
+   combination, the mix) runs on the lane's five limbs, and the pair joins
+   the operand before the mul and the mixed coordinate after it */
+__device__ __forceinline__ void
+quad8_body_ownc5( fe & C, fe5 const & pm, fe const & qrow, bool isD, bool neg, u64 mD, int qd, half_t const & H ) {
+  i32 c1 = (qd == 0) ? 1 : (qd == 1) ? (isD ? 0 : -1) : (isD ? 1 : 0);
+  i32 c2 = (qd <= 1 || !isD) ? 1 : 0;
+  i32 sh = (qd == 3) ? 1 : 0;
+  asm( "" : "+v"(c1), "+v"(c2) );
+  fe5 a5;
+  _Pragma("unroll") for( int k=0; k<5; k++ )
+    a5.v[k] = lin2( c1, qp<2,2,2,0>( pm.v[k] ), c2, qp<1,1,0,3>( pm.v[k] ) );
+  fe const a = fe_join5( a5 );
+  fe b;
+  _Pragma("unroll") for( int k=0; k<10; k++ ) b.v[k] = vsel( mD, (i32)((u32)a.v[k] << sh), qrow.v[k] );
+  fe5 const m = fe_mul_half5( a, b, H );
+  i32 s0 = neg ? -1 : 1;
+  i32 x = isD ? (qd == 1 ? -1 : (qd == 3 ? 0 : 1)) : (qd >= 2 ? 1 : 0);
+  i32 y = isD ? ((qd & 1) ? 1 : -1)               : (qd <= 1 ? 2 : (qd == 2 ? -1 : 1));
+  i32 z = isD ? (qd == 0 ? 0 : (qd == 2 ? -1 : 1)) : (qd == 0 ? s0 : (qd == 1 ? -s0 : 0));
+  asm( "" : "+v"(x), "+v"(y), "+v"(z) );
+  fe5 c5;
+  _Pragma("unroll") for( int k=0; k<5; k++ )
+    c5.v[k] = lin3( x, qp<1,1,0,0>( m.v[k] ), y, qp<2,2,1,1>( m.v[k] ), z, qp<3,3,2,2>( m.v[k] ) );
+  C = fe_join5( c5 );
 }
 
 __device__ __forceinline__ fe
@@ -1159,13 +1284,20 @@ k_dsm8( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
   fe C = (qd == 2) ? fe_zero() : fe_one();   /* identity: own coordinate (Z, T, X, Y)[q] = (1, 1, 0, 1) */
 
   for( ;; ) {
+#if FD_DSM8_SPLIT
+    fe5 pm5 = quad8_p3_ownc5( C, H );          /* q0 u.Z, q1 u.Y, q2 u.X, q3 u.T (split limbs) */
+#else
     fe pm = quad8_p3_ownc( C, H );              /* q0 u.Z, q1 u.Y, q2 u.X, q3 u.T */
+#endif
 
     bool fin = (ph == PH_FIN);
     /* each lane parks its own p1p1->p3 product in its row of entry 0 of the
        signature's Ai table (no ADD op reads it any more); the compare runs
        once after the loop */
     if( __any( fin ) ) {
+#if FD_DSM8_SPLIT
+      fe const pm = fe_join5( pm5 );           /* all 8 lanes of a signature finish together */
+#endif
       if( fin ) {
         int4 * d_ = (int4 *)(Ail + qd*12);
         d_[0] = make_int4( pm.v[0], pm.v[1], pm.v[2], pm.v[3] );
@@ -1178,7 +1310,11 @@ k_dsm8( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
 
     bool isD = (ph == PH_DBL);
     u64 mD = __builtin_amdgcn_ballot_w64( isD );
+#if FD_DSM8_SPLIT
+    quad8_body_ownc5( C, pm5, qrow, isD, qneg, mD, qd, H );
+#else
     quad8_body_ownc( C, pm, qrow, isD, qneg, mD, qd, H );
+#endif
 
     /* the event just executed is consumed; the next op follows from the
        event heads (an event at position p means a digit at p).  Branch-free:

@@ -14,7 +14,7 @@ for i, l in enumerate(s):
     m = re.match(r"^_Z(\d+)(\w+):", l)
     if m:
         starts[m.group(2)[:int(m.group(1))]] = i
-for k in ("k_prep", "k_decomp", "k_dsm", "k_dsm4"):
+for k in ("k_prep", "k_decomp", "k_dsm", "k_dsm4", "k_dsm8"):
     i = starts[k]
     j = next(n for n in range(i, len(s)) if "s_endpgm" in s[n])
     body = s[i:j]
@@ -24,7 +24,7 @@ for k in ("k_prep", "k_decomp", "k_dsm", "k_dsm4"):
     occ += " scratch " + re.search(r"; ScratchSize: (\d+)", meta).group(1)
     ins = [l.split()[0] for l in body if l.startswith("\t") and not l.strip().startswith(";") and not l.strip().startswith(".")]
     print("%-9s vgpr %s occ %s  static instrs %d" % (k, vg, occ, len(ins)))
-    if k in ("k_dsm", "k_dsm4"):
+    if k in ("k_dsm", "k_dsm4", "k_dsm8"):
         # largest loop: any label with a backward branch to it, farthest back-edge wins
         labs = {}
         for n in range(len(body)):
