@@ -66,10 +66,12 @@ int fd_amd_launch_digits_dense( uint32_t n, void const * d_ws, uint16_t * d_dig,
 
 /* 1 when a batch of n takes the latency kernels (k_front + k_dsm8/k_dsm4). */
 int fd_amd_uses_latency_path( uint32_t n, int dsm_mode );
-/* dsm_mode for one of several concurrent batches (the streaming tile):
-   k_dsm4 up to fd_ed25519_amd_set_small_batch_max, else k_dsm; never k_dsm8,
-   whose doubled wave count oversubscribes the SIMDs when batches overlap. */
-int fd_amd_batch_dsm_mode( uint32_t n );
+/* dsm_mode for one of several concurrent batches (the streaming tile, up to
+   4 in flight): k_dsm8 while four of its largest batches fit one wave per
+   SIMD (cap at most a quarter of fd_ed25519_amd_set_latency_batch_max), k_dsm4 up to
+   fd_ed25519_amd_set_small_batch_max, else k_dsm.  cap: the largest batch
+   the caller will have in flight. */
+int fd_amd_batch_dsm_mode( uint32_t n, uint32_t cap );
 
 /* d_off[i] -= lo for every nonempty message (0 for empty ones). */
 int fd_amd_launch_rebase_off( uint32_t n, uint32_t * d_off, uint32_t const * d_sz, uint32_t lo, hipStream_t stream );

@@ -2016,9 +2016,14 @@ fd_ed25519_amd_set_latency_batch_max( unsigned long n ) {
   g_dsm8_max = n > 0xFFFFFFFFUL ? 0xFFFFFFFFu : (u32)n;
 }
 
+/* the streaming tile keeps up to 4 batches in flight: k_dsm8 when four of
+   its largest batches (cap) still fit one wave per SIMD (cap <= g_dsm8_max
+   / 4), k_dsm4 up to g_dsm4_max, k_dsm beyond.  Deciding per batch size
+   instead lets k_dsm8's partial batches oversubscribe the SIMDs beside full
+   k_dsm4 ones (profiles/r02_tile_dsm8_ab.txt) */
 int
-fd_amd_batch_dsm_mode( uint32_t n ) {
-  return n <= g_dsm4_max ? 2 : 1;
+fd_amd_batch_dsm_mode( uint32_t n, uint32_t cap ) {
+  return cap <= g_dsm8_max / 4u ? 3 : n <= g_dsm4_max ? 2 : 1;
 }
 
 int

@@ -293,9 +293,12 @@ tile_launch( fd_verify_amd_tile_t * t, int k, ulong n, bool txn, uint8_t const *
      switching batches of >= 4096/8192 to the 1-lane kernel while others were
      in flight lowered the saturated rate at every batch_max and doubled
      latency; the in-flight work (4 x batch_max) is too small for the 1-lane
-     kernel to fill the GPU.  Not the 8-lane k_dsm8 either: with 4 batches in
-     flight its doubled wave count oversubscribes the SIMDs. */
-  int mode = fd_amd_batch_dsm_mode( (uint32_t)(txn ? ts.nsig : n) );
+     kernel to fill the GPU.  The 8-lane k_dsm8 only when batch_max <= 2048:
+     four of its batches then still fit one wave per SIMD (batch_max 256:
+     p50 650 -> 589 us; above, its doubled wave count oversubscribes the
+     SIMDs; profiles/r02_tile_dsm8_ab.txt).  Transaction batches carry up to
+     12 signatures per frag and keep the size rule. */
+  int mode = fd_amd_batch_dsm_mode( (uint32_t)(txn ? ts.nsig : n), txn ? 0xFFFFFFFFu : (uint32_t)t->batch_max );
   if( txn ) {
     ulong nsig = ts.nsig;
     if( fd_amd_launch_txn_parse( (uint32_t)n, ts.d_mir, s->d_toff, s->d_tsz, s->d_fp, NULL, 0, m_tbase,
