@@ -40,16 +40,11 @@ import time
 
 import numpy as np
 
-# The streaming tile keeps 4 GPU batches in flight on 4 HIP streams, and
-# only streams on distinct hardware queues run concurrently.  HIP maps
-# streams onto at most GPU_MAX_HW_QUEUES queues per process; with the
-# default 4, or with 8 once the bench's earlier engines have created and
-# destroyed their streams, the tile's 4 streams landed on 2 queues (kernel
-# trace: Queue_Id 3/4 only; 0.92 M frags/s at batch 256 vs 1.63 M with 16,
-# profiles/r02_tile_queues.txt).  16 (read at HIP runtime init, before any
-# device call) keeps them apart; the pool's limit is 32.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+# HIP's hardware-queue count is left as the process finds it (the box
+# default is 4, HIP's own): the streaming tile runs one persistent kernel on
+# one stream, and the resident batches use --streams (3) streams.  The value
+# in effect is reported in the JSON line (config.hip_hw_queues).
+HW_QUEUES = os.environ.get("GPU_MAX_HW_QUEUES", "default (4)")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -94,6 +89,11 @@ def parse():
     ap.add_argument("--workload", choices=("sigs", "txn"), default="sigs",
                     help="sigs: configs[1] (default bench line); txn: configs[3] multi-signer transactions")
     ap.add_argument("--stream-frags", type=int, default=1 << 20, help="frags per streaming-tile run")
+    ap.add_argument("--no-host-fed", action="store_true",
+                    help="skip the all-rank registered-host-memory pass (host_fed_node)")
+    ap.add_argument("--multi-engine", action="store_true",
+                    help="one process drives --gpus devices through the native multi-device engine "
+                         "(fd_ed25519_amd_multi_verify_soa) on host buffers; prints its own JSON line")
     return ap.parse_args()
 
 
@@ -399,6 +399,63 @@ def stream_rows(local, pub, sig, off, sz, blob, args):
             "rows": rows}
 
 
+# ---------------------------------------------------------------- multi-engine
+
+def run_multi_engine(args):
+    """One process, --gpus devices, the native multi-device engine
+    (fd_ed25519_amd_multi_*): one engine and one NUMA-bound host thread per
+    device, a host SoA batch of gpus x n signatures split into contiguous
+    shards per step (weak scaling: n per device).  PCIe-inclusive by
+    construction -- the shape of a host that feeds every GPU of the node from
+    one process.  FD_AMD_DEVICE_MAP=mod maps more engines than GPUs onto the
+    visible ones (rehearsal on a one-GPU box)."""
+    from firedancer_amd import ed25519, hip
+    ndev = hip.device_count()
+    if not ndev:
+        raise SystemExit("bench.py: no HIP device")
+    g = args.gpus
+    if g > ndev and os.environ.get("FD_AMD_DEVICE_MAP") != "mod":
+        raise SystemExit("bench.py --multi-engine: %d GPUs asked, %d visible" % (g, ndev))
+    devices = [d % ndev for d in range(g)]
+    n = args.n
+    pub1, sig1, off1, sz1, blob1 = make_workload(n, args.msg_sz, 1000)
+    ref = ed25519.Engine(device=0, batch_max=1 << 17, blob_max=(1 << 17) * args.msg_sz)
+    err1 = ref.verify_soa(pub1, sig1, off1, sz1, blob1)
+    ref.close()
+    pub = np.concatenate([pub1] * g)
+    sig = np.concatenate([sig1] * g)
+    sz = np.concatenate([sz1] * g)
+    off = np.concatenate([off1.astype(np.int64) + k * blob1.size for k in range(g)]).astype(np.uint32)
+    blob = np.concatenate([blob1] * g)
+    chunk = 1 << 17
+    m = ed25519.MultiEngine(devices, batch_max=chunk, blob_max=chunk * args.msg_sz)
+    try:
+        for _ in range(max(1, args.warmup)):
+            err = m.verify_soa(pub, sig, off, sz, blob)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            err = m.verify_soa(pub, sig, off, sz, blob)
+        dt = time.perf_counter() - t0
+    finally:
+        m.close()
+    nodes = [ed25519.device_numa_node(d) for d in sorted(set(devices))]
+    print(json.dumps({
+        "metric": METRIC, "value": g * n * args.steps / dt, "unit": "verifies/s", "n_gpus": g,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": DTYPE,
+        "data": "synthetic: fresh random keypairs and messages (one 2^20 batch repeated per device), host SoA buffers",
+        "mode": "multi_engine",
+        "config": {"workload": "configs[1] shape, %d x %d signatures from host memory per step" % (g, n),
+                   "devices": devices, "sigs_per_gpu_per_step": n, "msg_sz": args.msg_sz, "chunk": chunk,
+                   "parallelism": "multi-engine %d" % g, "hip_hw_queues": HW_QUEUES,
+                   "device_map": os.environ.get("FD_AMD_DEVICE_MAP", "identity")},
+        "numa_nodes": nodes,
+        "verdicts_match_single_engine": bool(all(np.array_equal(err[k * n:(k + 1) * n], err1) for k in range(g))),
+        "path": "host SoA -> fd_ed25519_amd_multi_verify_soa: per device one NUMA-bound thread, pinned staging (2 "
+                "chunks in flight) -> H2D -> kernels -> mapped verdicts",
+    }))
+
+
 # ---------------------------------------------------------------- configs[1]
 
 def main():
@@ -421,13 +478,19 @@ def main():
             os.close(saved)
 
     from firedancer_amd import ed25519, hip
+    from firedancer_amd.shard import bind_to_device_node
 
+    if args.multi_engine:
+        return run_multi_engine(args)
     ndev = hip.device_count()
     if os.environ.get("FD_AMD_DEVICE_MAP") == "mod" and ndev:   # rehearsal: more ranks than GPUs
         local = local % ndev
     if ndev <= local:
         raise SystemExit("bench.py: no HIP device %d visible" % local)
     hip.set_device(local)
+    # this rank's host thread(s) on its GPU's NUMA node, as the reference
+    # pins each verify tile to a core next to its input link
+    numa = bind_to_device_node(local)
 
     if args.workload == "txn":
         return run_txn(args, rank, world, dist)
@@ -496,6 +559,41 @@ def main():
     stream.synchronize()
     st = d_stats.to_array(np.uint32, 3 * n).reshape(3, n)
 
+    # host-fed node throughput: every rank at once verifies its batch from
+    # registered host memory (fd_ed25519_amd_verify_soa_registered: each
+    # chunk's planes and message window DMA'd, no host copy), the shape of a
+    # node whose GPUs are fed from host memory, PCIe included; max-over-ranks
+    # time.  Never the headline value.
+    host_fed = None
+    if not args.no_host_fed:
+        chunk, reps = 1 << 17, 3
+        eng = ed25519.Engine(device=local, batch_max=chunk, blob_max=chunk * args.msg_sz)
+        reg = ed25519.RegisteredPlanes(pub, sig, off, sz, blob)
+        rerr = np.zeros(n, np.int8)
+        eng.verify_soa_registered(reg[0], reg[1], reg[2], reg[3], reg[4], rerr)
+        if dist:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            eng.verify_soa_registered(reg[0], reg[1], reg[2], reg[3], reg[4], rerr)
+        dt_rank = time.perf_counter() - t1
+        reg.close()
+        eng.close()
+        ok = float(np.array_equal(rerr, err))
+        if dist:
+            from firedancer_amd.shard import max_over_ranks
+            dt_max = max_over_ranks(dt_rank)
+        else:
+            dt_max = dt_rank
+        ok_all, sum_rate = gather_sum(dist, [ok, n * reps / dt_rank])
+        host_fed = {"verifies_per_s": world * n * reps / dt_max, "sum_of_rank_rates": sum_rate,
+                    "per_rank_sigs": n, "chunk": chunk, "passes": reps,
+                    "h2d_gb_per_s_node": world * n * reps * (104 + args.msg_sz) / dt_max / 1e9,
+                    "verdicts_match_resident": ok_all == world,
+                    "path": "every rank at once: registered caller SoA (fd_ed25519_amd_host_register once) -> DMA "
+                            "of each chunk's planes and message window, no host copy -> kernels; rank bound to its "
+                            "GPU's NUMA node; value = all ranks' signatures / max-over-ranks time"}
+
     if rank != 0:
         return
     total = n * args.steps * world
@@ -514,7 +612,10 @@ def main():
         "data": "synthetic: fresh random keypairs and messages, signed on the GPU (k_sign), inputs resident in HBM",
         "config": {"workload": "configs[1]: 1xMI355X batch of 2^20 single-signer sigs, 200-byte messages",
                    "sigs_per_gpu_per_step": n, "msg_sz": args.msg_sz, "parallelism": "shard%d" % world,
-                   "streams": ns},
+                   "streams": ns, "hip_hw_queues": HW_QUEUES,
+                   "device_map": os.environ.get("FD_AMD_DEVICE_MAP", "identity")},
+        "numa_rank0": numa,
+        "host_fed_node": host_fed,
         "stage_ms": {"k_prep": stage_ms[0], "k_decomp": stage_ms[1], "k_dsm": stage_ms[2],
                      "note": "one batch alone on one stream (HIP events), after the timed region"},
         "verdicts": {"ok": int((err == 0).sum()), "rejected": int((err != 0).sum())},
@@ -582,14 +683,6 @@ def main():
         for _ in range(reps):
             herr = eng.verify_soa(pub, sig, off, sz, blob)
         dt = (time.perf_counter() - t1) / reps
-        reg = ed25519.RegisteredPlanes(pub, sig, off, sz, blob)
-        rerr = np.zeros(n, np.int8)
-        eng.verify_soa_registered(reg[0], reg[1], reg[2], reg[3], reg[4], rerr)
-        t1 = time.perf_counter()
-        for _ in range(reps):
-            eng.verify_soa_registered(reg[0], reg[1], reg[2], reg[3], reg[4], rerr)
-        dt_reg = (time.perf_counter() - t1) / reps
-        reg.close()
         eng.close()
         h2d_gbs = hip.h2d_bandwidth()
         per_sig = 104 + args.msg_sz
@@ -598,11 +691,9 @@ def main():
                            "pcie_bound_verifies_per_s": h2d_gbs * 1e9 / per_sig,
                            "verdicts_match_resident": bool((herr == err).all()),
                            "path": "host SoA -> pinned packed staging (2 chunks in flight) -> H2D -> kernels -> D2H"}
-        out["host_soa_registered"] = {"verifies_per_s": n / dt_reg, "chunk": chunk,
-                                      "h2d_gb_per_s": n * per_sig / dt_reg / 1e9,
-                                      "verdicts_match_resident": bool((rerr == err).all()),
-                                      "path": "caller planes registered once (fd_ed25519_amd_host_register) -> DMA "
-                                              "of each chunk's planes and message window, no host copy -> kernels"}
+        if host_fed:
+            out["host_soa_registered"] = {"verifies_per_s": host_fed["verifies_per_s"] / world,
+                                          "note": "rank 0's share of host_fed_node (every rank ran it at once)"}
     if world == 1 and not args.no_stream:
         out["stream_tile"] = stream_rows(local, pub, sig, off, sz, blob, args)
     if world == 1 and not args.no_cpu:

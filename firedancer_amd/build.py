@@ -20,7 +20,7 @@ LIB = os.path.join(PKG, "libfd_ed25519_amd.so")
 ARCH = os.environ.get("FD_AMD_ARCH", "gfx950")
 
 SOURCES = ["fd_ed25519_kernels.hip", "fd_txn_kernels.hip", "fd_ed25519_sign.hip", "fd_ed25519_engine.cpp", "fd_ed25519_multi.cpp", "fd_ed25519_host.cpp",
-           "fd_verify_tile.cpp"]
+           "fd_verify_tile.cpp", "fd_numa.cpp"]
 HEADERS = ["fd_ed25519_dev.h", "fd_ed25519_kernels.h", "../../include/fd_ed25519_amd.h", "../../include/fd_txn_amd.h", "../../include/fd_tango_amd.h", "fd_ed25519_engine.h",
            "../../tools/gen_consts.py"]
 

@@ -136,9 +136,14 @@ fd_amd_engine_new( int device, ulong batch_max, ulong blob_max, int nslot ) {
   fd_ed25519_amd_t * e = (fd_ed25519_amd_t *)calloc( 1, sizeof(fd_ed25519_amd_t) );
   if( !e ) return NULL;
   e->device = device; e->cap = batch_max; e->blob_cap = blob_max; e->nslot = nslot;
-  for( int k=0; k<nslot; k++ ) {
-    if( slot_alloc( &e->slot[k], batch_max, blob_max ) ) { fd_ed25519_amd_delete( e ); return NULL; }
-  }
+  /* the pinned staging on the GPU's NUMA node (the thread's own policy is
+     restored afterwards; fd_numa.cpp) */
+  int pmode = 0; unsigned long pmask[16];
+  int pnode = fd_amd_numa_prefer_begin( device, &pmode, pmask );
+  int bad = 0;
+  for( int k=0; k<nslot && !bad; k++ ) bad = slot_alloc( &e->slot[k], batch_max, blob_max );
+  if( pnode >= 0 ) fd_amd_numa_prefer_end( pmode, pmask );
+  if( bad ) { fd_ed25519_amd_delete( e ); return NULL; }
   return e;
 }
 
@@ -174,12 +179,18 @@ int
 fd_amd_slot_drain( slot_t * s ) {
   if( !s->busy ) return FD_ED25519_AMD_OK;
   HIPCHK( hipEventSynchronize( s->done ) );
-  if( s->out   ) memcpy( s->out,   s->h_err,  s->n );
-  if( s->t_out ) memcpy( s->t_out, s->h_terr, s->t_n );
-  if( s->s_out ) memcpy( s->s_out, s->h_err,  s->s_n );
+  /* k_dsmp's hang guard marks every verdict of its launch (k_fin) */
+  bool fault = ( s->chk_err  && s->h_err[0] == (int8_t)FD_AMD_VERDICT_DEVICE ) ||
+               ( s->chk_terr && memchr( s->h_terr, (uint8_t)FD_AMD_VERDICT_DEVICE, s->chk_terr ) );
+  if( fault ) fprintf( stderr, "fd_ed25519_amd: the pooled double-scalar multiply hit its step guard\n" );
+  else {
+    if( s->out   ) memcpy( s->out,   s->h_err,  s->n );
+    if( s->t_out ) memcpy( s->t_out, s->h_terr, s->t_n );
+    if( s->s_out ) memcpy( s->s_out, s->h_err,  s->s_n );
+  }
   s->out = s->t_out = s->s_out = NULL;
   s->busy = 0;
-  return FD_ED25519_AMD_OK;
+  return fault ? FD_ED25519_AMD_ERR_DEVICE : FD_ED25519_AMD_OK;
 }
 
 /* Error exit of a batch call: wait for every chunk still in flight and
@@ -212,6 +223,7 @@ fd_amd_slot_launch_packed( slot_t * s, ulong n, ulong blob_sz, schar * out ) {
   HIPCHK( slot_out( s, s->h_err, s->d_err, n ) );
   HIPCHK( hipEventRecord( s->done, s->stream ) );
   s->out = out; s->n = n; s->busy = 1; s->want_tag = 0;
+  s->chk_err = n; s->chk_terr = 0;
   return FD_ED25519_AMD_OK;
 }
 
@@ -256,6 +268,7 @@ fd_amd_slot_launch_txn( slot_t * s, ulong c, ulong nslot, ulong blob_sz, schar *
   HIPCHK( hipEventRecord( s->done, s->stream ) );
   s->t_out = t_out; s->t_n = c;
   s->s_out = nslot ? s_out : NULL; s->s_n = nslot;
+  s->chk_err = (s_out && nslot) ? nslot : 0; s->chk_terr = c;
   s->busy = 1;
   return FD_ED25519_AMD_OK;
 }
@@ -406,11 +419,24 @@ fd_ed25519_amd_host_unregister( void * base ) {
   return hipHostUnregister( base ) == hipSuccess ? FD_ED25519_AMD_OK : FD_ED25519_AMD_ERR_DEVICE;
 }
 
+/* [p, p+sz) lies in ONE registration: its first and its last byte are
+   registered host memory and map to device addresses sz-1 apart (two
+   adjacent registrations map to unrelated device ranges).  The latency
+   path reads the planes in place, so a plane registered only in part must
+   be refused here, not faulted on by the GPU. */
 static bool
-host_registered( void const * p ) {
+host_registered( void const * p, ulong sz ) {
   hipPointerAttribute_t a;
   if( hipPointerGetAttributes( &a, p ) != hipSuccess ) { (void)hipGetLastError(); return false; }
-  return a.type == hipMemoryTypeHost;
+  if( a.type != hipMemoryTypeHost ) return false;
+  if( sz <= 1UL ) return true;
+  void const * q = (uchar const *)p + (sz - 1UL);
+  if( hipPointerGetAttributes( &a, q ) != hipSuccess ) { (void)hipGetLastError(); return false; }
+  if( a.type != hipMemoryTypeHost ) return false;
+  void * dp = NULL, * dq = NULL;
+  if( hipHostGetDevicePointer( &dp, (void *)p, 0 ) != hipSuccess ||
+      hipHostGetDevicePointer( &dq, (void *)q, 0 ) != hipSuccess ) { (void)hipGetLastError(); return false; }
+  return (ulong)((uchar const *)dq - (uchar const *)dp) == sz - 1UL;
 }
 
 /* One chunk straight from registered caller memory: the pub/sig/off/sz
@@ -431,6 +457,7 @@ slot_launch_dma( slot_t * s, ulong c, uchar const * pub, uchar const * sig, uint
   HIPCHK( slot_out( s, s->h_err, s->d_err, c ) );
   HIPCHK( hipEventRecord( s->done, s->stream ) );
   s->out = out; s->n = c; s->busy = 1; s->want_tag = 0;
+  s->chk_err = c; s->chk_terr = 0;
   return FD_ED25519_AMD_OK;
 }
 
@@ -443,8 +470,8 @@ fd_ed25519_amd_verify_soa_registered( fd_ed25519_amd_t * e, ulong n, uchar const
     if( msg_sz[i] && ((ulong)msg_off[i] + msg_sz[i] > blob_sz || !blob || msg_sz[i] > e->blob_cap) )
       return FD_ED25519_AMD_ERR_INVAL;
   if( !n ) return FD_ED25519_AMD_OK;
-  if( !host_registered( pub ) || !host_registered( sig ) || !host_registered( msg_off ) || !host_registered( msg_sz ) ||
-      (blob && blob_sz && !host_registered( blob )) )
+  if( !host_registered( pub, 32UL*n ) || !host_registered( sig, 64UL*n ) || !host_registered( msg_off, 4UL*n ) ||
+      !host_registered( msg_sz, 4UL*n ) || (blob && blob_sz && !host_registered( blob, blob_sz )) )
     return FD_ED25519_AMD_ERR_INVAL;
   if( hipSetDevice( e->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
   int rc = FD_ED25519_AMD_OK;
@@ -463,6 +490,7 @@ fd_ed25519_amd_verify_soa_registered( fd_ed25519_amd_t * e, ulong n, uchar const
     if( slot_out( s, s->h_err, s->d_err, n ) != hipSuccess || hipEventRecord( s->done, s->stream ) != hipSuccess )
       return engine_quiesce( e, FD_ED25519_AMD_ERR_DEVICE );
     s->out = err; s->n = n; s->busy = 1; s->want_tag = 0;
+    s->chk_err = n; s->chk_terr = 0;
     if( (rc = fd_amd_slot_drain( s )) ) return engine_quiesce( e, rc );
     return FD_ED25519_AMD_OK;
   }

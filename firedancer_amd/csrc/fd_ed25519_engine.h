@@ -27,6 +27,7 @@ struct slot_t {
   schar *    out;
   ulong      n;
   int        busy;
+  ulong      chk_err, chk_terr;   /* verdict bytes the launch writes to h_err / h_terr (checked for FD_AMD_VERDICT_DEVICE) */
   /* transaction front end (allocated on first use): per-transaction
      payload offset/size, footprint, signature-slot base, verdict; per-slot
      skip plane */
@@ -48,6 +49,12 @@ struct fd_ed25519_amd {
   int    nslot;      /* 2 for the batch API (double buffering); the tile uses more */
   slot_t slot[FD_AMD_SLOT_MAX];
 };
+
+/* NUMA placement (fd_numa.cpp): bind the calling thread to the device's
+   node (CPUs + preferred memory), or prefer it only while allocating. */
+int  fd_amd_numa_bind_thread( int device );
+int  fd_amd_numa_prefer_begin( int device, int * saved_mode, unsigned long * saved_mask /* 16 words */ );
+void fd_amd_numa_prefer_end( int saved_mode, unsigned long const * saved_mask );
 
 /* An engine with `nslot` in-flight slots (2..FD_AMD_SLOT_MAX). */
 fd_ed25519_amd_t * fd_amd_engine_new( int device, ulong batch_max, ulong blob_max, int nslot );

@@ -23,6 +23,10 @@ int fd_amd_launch_verify( uint32_t n, uint8_t const * d_pub, uint8_t const * d_s
                           uint32_t const * d_sz, uint8_t const * d_blob, int8_t * d_err, void * d_ws,
                           hipStream_t stream, int want_stats, hipEvent_t const * ev /* 4 or NULL */,
                           int8_t const * d_skip = NULL, int dsm_mode = 0 );
+/* Verdict byte that marks every signature of a launch whose k_dsmp hang
+   guard tripped (never a reference code): the host calls turn it into
+   FD_ED25519_AMD_ERR_DEVICE. */
+#define FD_AMD_VERDICT_DEVICE (-128)
 /* dsm_mode: 0 = by batch size (fd_ed25519_amd_set_latency_batch_max,
    fd_ed25519_amd_set_small_batch_max), 1 = the throughput path (k_prep,
    k_decomp, k_dsm), 2 = k_front + k_dsm4, 3 = k_front + k_dsm8. */
@@ -58,6 +62,57 @@ int fd_amd_launch_sign( uint32_t n, uint8_t const * d_prv, uint32_t const * d_of
 int fd_amd_launch_tile_gather( uint32_t n, uint32_t const * d_meta, uint8_t const * d_src, uint8_t * d_out,
                                uint8_t * d_mir, uint32_t stride, int txn, uint8_t * d_pub, uint8_t * d_sig,
                                uint32_t * d_off, uint32_t * d_sz, hipStream_t stream );
+
+/* Streaming tile, persistent consumer (k_tile_persist).  One launch per
+   tile run; its waves take chunk descriptors the tile's host thread
+   publishes in mapped host memory and verify them, so the GPU never drains
+   between hand-offs and the tile needs one stream (one hardware queue).
+
+   ring entry (host -> GPU): the frag's chunk in the source region, its
+   output frame's chunk (zero-copy: the GPU writes the verified bytes
+   there), its size.  Entry of ring index j at ent[j & mask]. */
+typedef struct { uint32_t src_chunk, out_chunk, sz, pad; } fd_amd_tile_ent_t;
+/* chunk descriptor (host -> GPU): ring entries [first, first + count),
+   count <= 64 | FD_AMD_TILE_LAT (8 lanes per signature) */
+typedef struct { uint64_t first; uint32_t count; uint32_t pad; } fd_amd_tile_desc_t;
+#define FD_AMD_TILE_LAT (0x80000000u)
+/* result (GPU -> host): word = (j + 1) << 8 | (uint8_t)verdict, stored
+   after tag and after the frag's output bytes (system-scope release), so a
+   host that sees word's index also sees the rest. */
+typedef struct { uint64_t tag, word; } fd_amd_tile_res_t;
+/* host-written control words, each on its own 64-B line */
+typedef struct {
+  uint64_t head;  uint64_t pad0[7];   /* chunk descriptors [.., head) are published to the GPU */
+  uint64_t beat;  uint64_t pad1[7];   /* host heartbeat: the kernel's watchdog */
+  uint32_t stop;  uint32_t kerr;  uint64_t pad2[7];   /* stop: exit once drained; kerr: set by the kernel on a watchdog exit */
+} fd_amd_tile_hctl_t;
+/* device control block (zeroed by the host before each launch) */
+#define FD_AMD_TILE_MIRRORS (8)
+typedef struct { uint64_t w; uint64_t pad[7]; } fd_amd_tile_mirror_t;
+typedef struct {
+  uint64_t             ticket;  uint64_t pad0[7];   /* next chunk ticket (one atomic add per chunk) */
+  fd_amd_tile_mirror_t mw[FD_AMD_TILE_MIRRORS];     /* per XCD: descriptor head | heartbeat << 48 | err << 62 | stop << 63 */
+  uint64_t             stat[4];                     /* chunks in latency mode, in throughput mode; frags in each */
+  uint64_t             prof[8];                     /* debug (args.prof): summed ticks gather, front, DSM, results, wait, fence */
+} fd_amd_tile_dctl_t;
+typedef struct {
+  fd_amd_tile_hctl_t *       hctl;     /* device address of the mapped control words */
+  fd_amd_tile_ent_t const *  ent;      /* device address of the mapped ring */
+  fd_amd_tile_desc_t const * desc;     /* device address of the mapped chunk descriptors (same size as the ring) */
+  fd_amd_tile_res_t *        res;      /* device address of the mapped results */
+  uint64_t                   mask;     /* ring size - 1 (power of 2) */
+  uint8_t const *            src;      /* frag source region (mapped): input dcache (zero-copy) or the output frames */
+  uint8_t *                  out;      /* output frames (mapped) to fill, or NULL (copy mode: the host filled them) */
+  fd_amd_tile_dctl_t *       dctl;
+  uint8_t *                  scratch;  /* per-wave scratch, fd_amd_tile_scratch_stride() bytes apart */
+  uint64_t                   watchdog; /* s_memrealtime ticks (100 MHz) without a host heartbeat before the kernel gives up */
+  uint32_t                   prof;     /* debug: sum per-phase time stamps into dctl->prof */
+  uint32_t                   dbg;      /* A/B only: 8 read frags from src_dev, 16 no output-frame writes */
+  uint8_t const *            src_dev;  /* A/B only: a device copy of the source region */
+} fd_amd_tile_args_t;
+size_t fd_amd_tile_scratch_stride( void );
+/* waves: grid size (wave 0 is the scout that mirrors the host words) */
+int fd_amd_launch_tile_persist( fd_amd_tile_args_t const * a, uint32_t waves, hipStream_t stream );
 
 /* Dense slide digits of the last call on workspace d_ws (debug): u16
    [n][256] (low byte h digit, high byte s digit) rebuilt from the event

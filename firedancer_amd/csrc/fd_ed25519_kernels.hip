@@ -47,11 +47,13 @@ typedef uint16_t u16;
 /* ------------------------------------------------------------------ */
 /* workspace                                                            */
 
-static inline size_t ws_al( size_t x ) { return (x + 255UL) & ~(size_t)255UL; }
+__host__ __device__ constexpr size_t ws_al( size_t x ) { return (x + 255UL) & ~(size_t)255UL; }
 
-ws_layout_t
-fd_amd_ws_layout( size_t n ) {
-  ws_layout_t L;
+/* constexpr so that a kernel with a fixed N (k_tile_persist, N = 64) folds
+   every plane offset into an immediate */
+__host__ __device__ constexpr ws_layout_t
+ws_layout_const( size_t n ) {
+  ws_layout_t L = {};
   size_t N = (n + 63UL) & ~(size_t)63UL; if( !N ) N = 64;
   size_t o = 0;
   L.N   = N;
@@ -65,9 +67,14 @@ fd_amd_ws_layout( size_t n ) {
   L.tag = o; o = ws_al( o + 8UL*N );
   L.ds  = o; o = ws_al( o + 2UL*N );
   L.init = o; o = ws_al( o + 16UL*N );        /* uint4 [N]: k_dsmp op-stream start (k_ai) */
-  L.ctr  = o; o = ws_al( o + 4UL );            /* u32: k_dsmp work counter (zeroed by k_ai) */
+  L.ctr  = o; o = ws_al( o + 16UL );          /* u32 k_dsmp work counter (zeroed by k_ai) | u32 k_dsmp guard flag */
   L.total = o;
   return L;
+}
+
+ws_layout_t
+fd_amd_ws_layout( size_t n ) {
+  return ws_layout_const( n );
 }
 
 /* ------------------------------------------------------------------ */
@@ -388,6 +395,25 @@ ge_to_cached( fe & cZ, fe & cYmX, fe & cYpX, fe & cT2d, p3 const & u ) {
    (table/fd_ed25519_ge_bi_precomp_avx.c:30-112 lane order). */
 __constant__ static i32 const BI_TABLE[8][3][10] = FD_AMD_BI_PRECOMP;   /* rows y+x, y-x, 2dxy */
 
+/* The base-point table in the Ai slab's row layout (rows [Z = 1 | Y-X |
+   Y+X | 2dT] x 12 limbs, 10 used): an ADD-A row comes from the signature's
+   Ai slab, an ADD-B row from here, with the same three 16-B loads through
+   one generic pointer.  Filled by the wave before the DSM bodies run. */
+__device__ __forceinline__ void
+bi12_fill( i32 (* __restrict__ bi12)[48] ) {
+  for( int k=threadIdx.x & 63; k<8*48; k+=64 ) {
+    int e = k / 48, c = (k % 48) / 12, l = k % 12;
+    i32 v = 0;
+    if( l < 10 ) {
+      if( c == 0 ) v = (l == 0);
+      else if( c == 1 ) v = BI_TABLE[e][1][l];
+      else if( c == 2 ) v = BI_TABLE[e][0][l];
+      else v = BI_TABLE[e][2][l];
+    }
+    bi12[e][k % 48] = v;
+  }
+}
+
 /* Branch-free per-lane select: v_cndmask_b32 on a wave lane mask (ballot).
    Plain ?: on the op-stream selects lets LLVM re-form divergent branches
    around the field muls (both sides then run with copies in between). */
@@ -439,20 +465,8 @@ struct evq {
 __device__ __forceinline__ void
 dsm_lane_body( u32 i, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats,
                i32 (* __restrict__ bi)[48], u64 (* __restrict__ evl)[33] ) {
-  /* the base-point table in the Ai slab's row layout (rows [Z = 1 | Y-X |
-     Y+X | 2dT] x 12 limbs), so ADD-A and ADD-B operands load alike */
-  for( int k=threadIdx.x; k<8*48; k+=64 ) {
-    int e = k / 48, c = (k % 48) / 12, l = k % 12;
-    i32 v;
-    if( l >= 10 ) v = 0;
-    else if( c == 0 ) v = (l == 0);                    /* Z = 1 */
-    else if( c == 1 ) v = BI_TABLE[e][1][l];           /* Y-X */
-    else if( c == 2 ) v = BI_TABLE[e][0][l];           /* Y+X */
-    else v = BI_TABLE[e][2][l];                        /* 2dxy */
-    bi[e][k % 48] = v;
-  }
-  __syncthreads();
-
+  /* bi: the base-point table in the Ai slab's row layout (bi12_fill), so
+     ADD-A and ADD-B operands load alike */
   bool act = (i < n) && (err[i] == 1);
   if( act && (ws[L.ds + 2u*i] | ws[L.ds + 2u*i + 1u]) ) { err[i] = (i8)-2; act = false; }   /* A or R undecodable */
   size_t N = L.N;
@@ -654,6 +668,8 @@ __global__ void __launch_bounds__(64)
 k_dsm( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats ) {
   __shared__ __attribute__((aligned(16))) i32 bi[8][48];
   __shared__ u64 evl[64][33];
+  bi12_fill( bi );
+  __syncthreads();
   dsm_lane_body( blockIdx.x * 64u + threadIdx.x, n, err, ws, L, want_stats, bi, evl );
 }
 
@@ -985,11 +1001,9 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
  * f_i * g_{2c+h-i} with that column's reference factors (x2 when i and j are
  * odd, x19 when i + j >= 10, on the wrapped int32 pre-multiples).  The five
  * 64-bit column sums are swapped between the two lanes with DPP
- * row_shl/row_shr 4 under bank masks, and both lanes finish the reference
- * carry chain (fe_carry_b on pre-biased sums): the same limbs as fe_mul. */
-#ifndef FD_DSM8_SPLIT
-#define FD_DSM8_SPLIT 1
-#endif
+ * row_shl/row_shr 4 under bank masks, and the pair finishes the reference
+ * carry chain on pre-biased sums, each lane running one of its two
+ * interleaved runs (fe_mul_half5): the same limbs as fe_mul. */
 struct half_t { u64 mH; i32 shF; i64 bias; i64 m4, k5; u32 shz, mo0; i32 bo0; };
 __device__ __forceinline__ half_t half_ctx( int hh ) {
   half_t H;
@@ -1015,35 +1029,9 @@ __device__ __forceinline__ u32 half_from_hi( u32 v ) {   /* h = 0 lanes read lan
   return (u32)__builtin_amdgcn_update_dpp( (int)v, (int)v, 0x104, 0xf, 0x5, false );
 }
 
-__device__ __forceinline__ fe
-fe_mul_half( fe const & F, fe const & G, half_t const & H ) {
-  i32 gs[9], g19[10], f2[10];
-  _Pragma("unroll") for( int j=0; j<9; j++ ) gs[j] = vsel( H.mH, G.v[j+1], G.v[j] );
-  _Pragma("unroll") for( int j=1; j<9; j++ ) g19[j] = wmul( gs[j], 19 );
-  g19[9] = vsel( H.mH, G.v[0], wmul( G.v[9], 19 ) );
-  _Pragma("unroll") for( int i=1; i<10; i+=2 ) f2[i] = (i32)((u32)F.v[i] << (u32)H.shF);
-  i64 a[5];
-  _Pragma("unroll") for( int c=0; c<5; c++ ) a[c] = H.bias;
-  _Pragma("unroll") for( int i=0; i<10; i++ ) {
-    _Pragma("unroll") for( int c=0; c<5; c++ ) {
-      int j = 2*c - i;
-      i32 g = (j >= 0) ? gs[j] : g19[j + 10];
-      i32 f = (i & 1) ? f2[i] : F.v[i];
-      a[c] = mac( f, g, a[c] );
-    }
-  }
-  i64 E[5], O[5];
-  _Pragma("unroll") for( int c=0; c<5; c++ ) {
-    u32 lo = (u32)a[c], hi = (u32)((u64)a[c] >> 32);
-    E[c] = (i64)(((u64)half_from_lo( hi ) << 32) | half_from_lo( lo ));
-    O[c] = (i64)(((u64)half_from_hi( hi ) << 32) | half_from_hi( lo ));
-  }
-  return fe_carry_b( E[0], O[0], E[1], O[1], E[2], O[2], E[3], O[3], E[4], O[4] );
-}
-
-/* Split-carry form of fe_mul_half: the two lanes of a pair run the two
-   halves of the reference carry chain side by side instead of both running
-   all of it, and each returns five limbs (fe5); fe_join5 makes the full
+/* The split field mul: after the column sums, the two lanes of a pair run
+   the two halves of the reference carry chain side by side (rather than
+   both running all of it), and each returns five limbs (fe5); fe_join5 makes the full
    element when an operation needs it.  The chain of fe_carry_b is two
    interleaved runs, 0->1->2->3->(4) and 4->5->6->7->8->9->(0); in slots
    s0..s5 lane h = 0 holds h0..h4 (s5 = 0) and lane h = 1 holds h4..h9, so
@@ -1158,60 +1146,12 @@ quad8_body_ownc5( fe & C, fe5 const & pm, fe const & qrow, bool isD, bool neg, u
   C = fe_join5( c5 );
 }
 
-__device__ __forceinline__ fe
-quad8_p3_ownc( fe const & C, half_t const & H ) {
-  fe a, b;
-  _Pragma("unroll") for( int k=0; k<10; k++ ) { a.v[k] = qp<0,0,2,2>( C.v[k] ); b.v[k] = qp<1,3,1,3>( C.v[k] ); }
-  return fe_mul_half( a, b, H );
-}
-
+/* k_dsm8's body for lane gt of the launch (signature gt >> 3); bi12 filled
+   (bi12_fill), evl: 8 event rows of 33 words for the wave's 8 signatures.
+   Also the streaming tile's latency chunks (k_tile_persist). */
 __device__ __forceinline__ void
-quad8_body_ownc( fe & C, fe const & pm, fe const & qrow, bool isD, bool neg, u64 mD, int qd, half_t const & H ) {
-  /* operand a = c1*P1 + c2*P2 with P1 = quad_perm(2,2,2,0) -> X X X Z and
-     P2 = quad_perm(1,1,0,3) -> Y Y Z T:  DBL a = [X+Y, Y, X, Z],
-     ADD a = [X+Y, Y-X, Z, T];  b = DBL ? a << (q==3) : qrow */
-  i32 c1 = (qd == 0) ? 1 : (qd == 1) ? (isD ? 0 : -1) : (isD ? 1 : 0);
-  i32 c2 = (qd <= 1 || !isD) ? 1 : 0;
-  i32 sh = (qd == 3) ? 1 : 0;
-  asm( "" : "+v"(c1), "+v"(c2) );
-  fe a, b;
-  _Pragma("unroll") for( int k=0; k<10; k++ ) {
-    i32 av = lin2( c1, qp<2,2,2,0>( pm.v[k] ), c2, qp<1,1,0,3>( pm.v[k] ) );
-    a.v[k] = av;
-    b.v[k] = vsel( mD, (i32)((u32)av << sh), qrow.v[k] );
-  }
-  fe m = fe_mul_half( a, b, H );
-  i32 s0 = neg ? -1 : 1;
-  i32 x = isD ? (qd == 1 ? -1 : (qd == 3 ? 0 : 1)) : (qd >= 2 ? 1 : 0);
-  i32 y = isD ? ((qd & 1) ? 1 : -1)               : (qd <= 1 ? 2 : (qd == 2 ? -1 : 1));
-  i32 z = isD ? (qd == 0 ? 0 : (qd == 2 ? -1 : 1)) : (qd == 0 ? s0 : (qd == 1 ? -s0 : 0));
-  asm( "" : "+v"(x), "+v"(y), "+v"(z) );   /* opaque: keep full v_mad_i64_i32 (no small-range rewrites) */
-  _Pragma("unroll") for( int k=0; k<10; k++ )
-    C.v[k] = lin3( x, qp<1,1,0,0>( m.v[k] ), y, qp<2,2,1,1>( m.v[k] ), z, qp<3,3,2,2>( m.v[k] ) );
-}
-
-
-__global__ void __launch_bounds__(64)
-k_dsm8( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats ) {
-  /* the base-point table in the Ai slab's row layout (rows [Z = 1 | Y-X |
-     Y+X | 2dT] x 12 limbs): an ADD-A row comes from the signature's Ai slab,
-     an ADD-B row from here, with the same three 16-B loads through one
-     generic pointer */
-  __shared__ __attribute__((aligned(16))) i32 bi12[8][48];
-  for( int k=threadIdx.x; k<8*48; k+=64 ) {
-    int e = k / 48, c = (k % 48) / 12, l = k % 12;
-    i32 v = 0;
-    if( l < 10 ) {
-      if( c == 0 ) v = (l == 0);
-      else if( c == 1 ) v = BI_TABLE[e][1][l];
-      else if( c == 2 ) v = BI_TABLE[e][0][l];
-      else v = BI_TABLE[e][2][l];
-    }
-    bi12[e][k % 48] = v;
-  }
-  __syncthreads();
-
-  u32 gt = blockIdx.x * 64u + threadIdx.x;
+dsm8_body( u32 gt, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats,
+           i32 (* __restrict__ bi12)[48], u64 (* __restrict__ evl)[33] ) {
   u32 i = gt >> 3;
   int qd = (int)(threadIdx.x & 3u);
   int hh = (int)((threadIdx.x >> 2) & 1u);            /* which half of every field mul this lane computes */
@@ -1266,8 +1206,7 @@ k_dsm8( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
   int ph  = act ? (p >= 0 ? PH_DBL : PH_FIN) : PH_DONE;
   evq eva, evb;                                      /* digit events of h and s */
   {
-    __shared__ u64 evl[8][33];                       /* one row per signature of the wave */
-    u64 * row = evl[threadIdx.x >> 3];
+    u64 * row = evl[(threadIdx.x & 63u) >> 3];       /* one row per signature of the wave */
     u32 ne = act ? ((u32 const *)(ws + L.evn))[ii] : 0u;
     u32 wa = ((ne & 0xffu) + 3u) >> 2, wb = (((ne >> 8) & 0xffu) + 3u) >> 2;
     for( u32 k=threadIdx.x & 7u; k<wa; k+=8u ) row[k]       = dg[k];   /* the 8 lanes copy the row together */
@@ -1284,20 +1223,14 @@ k_dsm8( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
   fe C = (qd == 2) ? fe_zero() : fe_one();   /* identity: own coordinate (Z, T, X, Y)[q] = (1, 1, 0, 1) */
 
   for( ;; ) {
-#if FD_DSM8_SPLIT
     fe5 pm5 = quad8_p3_ownc5( C, H );          /* q0 u.Z, q1 u.Y, q2 u.X, q3 u.T (split limbs) */
-#else
-    fe pm = quad8_p3_ownc( C, H );              /* q0 u.Z, q1 u.Y, q2 u.X, q3 u.T */
-#endif
 
     bool fin = (ph == PH_FIN);
     /* each lane parks its own p1p1->p3 product in its row of entry 0 of the
        signature's Ai table (no ADD op reads it any more); the compare runs
        once after the loop */
     if( __any( fin ) ) {
-#if FD_DSM8_SPLIT
       fe const pm = fe_join5( pm5 );           /* all 8 lanes of a signature finish together */
-#endif
       if( fin ) {
         int4 * d_ = (int4 *)(Ail + qd*12);
         d_[0] = make_int4( pm.v[0], pm.v[1], pm.v[2], pm.v[3] );
@@ -1310,11 +1243,7 @@ k_dsm8( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
 
     bool isD = (ph == PH_DBL);
     u64 mD = __builtin_amdgcn_ballot_w64( isD );
-#if FD_DSM8_SPLIT
     quad8_body_ownc5( C, pm5, qrow, isD, qneg, mD, qd, H );
-#else
-    quad8_body_ownc( C, pm, qrow, isD, qneg, mD, qd, H );
-#endif
 
     /* the event just executed is consumed; the next op follows from the
        event heads (an event at position p means a digit at p).  Branch-free:
@@ -1374,6 +1303,15 @@ k_dsm8( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
   }
 }
 
+__global__ void __launch_bounds__(64)
+k_dsm8( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats ) {
+  __shared__ __attribute__((aligned(16))) i32 bi12[8][48];
+  __shared__ u64 evl[8][33];
+  bi12_fill( bi12 );
+  __syncthreads();
+  dsm8_body( blockIdx.x * 64u + threadIdx.x, n, err, ws, L, want_stats, bi12, evl );
+}
+
 /* ------------------------------------------------------------------ */
 /* Pooled DSM for large batches: k_ai -> k_dsmp -> k_fin.
  *
@@ -1431,7 +1369,7 @@ k_ai( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L ) {
     }
   }
   u32 i = blockIdx.x * 64u + threadIdx.x;
-  if( i == 0u ) *(u32 *)(ws + L.ctr) = 0u;
+  if( i == 0u ) { ((u32 *)(ws + L.ctr))[0] = 0u; ((u32 *)(ws + L.ctr))[1] = 0u; }   /* work counter, guard flag */
   bool act = (i < n) && (err[i] == 1);
   if( act && (ws[L.ds + 2u*i] | ws[L.ds + 2u*i + 1u]) ) { err[i] = (i8)-2; act = false; }
   size_t N = L.N;
@@ -1556,7 +1494,7 @@ __device__ __forceinline__ u32 lane_rank( u64 m ) {   /* set bits of m below thi
    new classes return to the masks through each slot's owner lane (s & 63),
    which pulls the processing lane's verdict with ds_bpermute. */
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
-k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
+k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
   constexpr u32 P = FD_POOL_P;
   static_assert( P >= 64 && P <= 128, "pool: each lane owns slots l and l + 64" );
   __shared__ int4  s_t[10][P];   /* p1p1 state [X | Y | Z | T], 16-B column r of slot s at [r][s]:
@@ -1576,8 +1514,13 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
   u32 * ctr = (u32 *)(ws + L.ctr);   /* next unclaimed signature, shared by all waves */
   bool more = true;                  /* wave-uniform: the counter has not passed n */
   /* hang guard: every step advances at least one op of at most 448 per
-     signature, and a wave can claim at most all n signatures */
-  u64 const iter_max = ((u64)n + 2u*P) * 448u;
+     signature, and a wave can claim at most all n signatures.  A wave that
+     reaches it raises the launch's guard flag: k_fin then marks every
+     verdict FD_AMD_VERDICT_DEVICE and the host call fails with
+     FD_ED25519_AMD_ERR_DEVICE (iter_cap: a debug cap, ~0 normally). */
+  u64 iter_max = ((u64)n + 2u*P) * 448u;
+  if( iter_cap < iter_max ) iter_max = iter_cap;
+  bool guard = true;
 #ifdef FD_POOL_DEBUG
   u32 dbg_steps = 0, dbg_lanes = 0, dbg_add = 0, dbg_idle = 0;
 #endif
@@ -1617,7 +1560,7 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
       nD = (u32)(__builtin_popcountll( mD0 ) + __builtin_popcountll( mD1 ));
     }
     if( !(nD + nA) ) {
-      if( !more ) break;   /* pool empty, nothing left to take */
+      if( !more ) { guard = false; break; }   /* pool empty, nothing left to take */
       continue;
     }
 
@@ -1812,6 +1755,7 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L ) {
     mD0 |= S0 & d0; mA0 |= S0 & x0 & ~d0;                       /* OP_AA / OP_AB: below OP_EMPTY, not OP_D */
     mD1 |= S1 & d1; mA1 |= S1 & x1 & ~d1;
   }
+  if( guard && l == 0u ) atomicOr( (u32 *)(ws + L.ctr) + 1, 1u );
 #ifdef FD_POOL_DEBUG
   if( l == 0u ) { atomicAdd( &g_pool_dbg[0], dbg_steps ); atomicAdd( &g_pool_dbg[1], dbg_lanes ); atomicAdd( &g_pool_dbg[2], dbg_add ); atomicAdd( &g_pool_dbg[3], dbg_idle ); }
   if( l == 0u && w < 8192u ) { g_pool_dbg_t[w][0] = dbg_t0; g_pool_dbg_t[w][1] = dbg_te; g_pool_dbg_t[w][2] = wall_clock64(); g_pool_dbg_t[w][3] = dbg_sa | (dbg_la << 32); }
@@ -1840,6 +1784,7 @@ k_fin( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
   u32 i = blockIdx.x * 64u + threadIdx.x;
   if( i >= n ) return;
   size_t N = L.N;
+  if( ((u32 const *)(ws + L.ctr))[1] ) { err[i] = (i8)FD_AMD_VERDICT_DEVICE; return; }   /* k_dsmp's guard tripped */
   bool act = err[i] == 1;
   int top = ((int const *)(ws + L.top))[i];
   if( act ) {
@@ -1915,6 +1860,258 @@ fd_amd_launch_tile_gather( uint32_t n, uint32_t const * d_meta, uint8_t const * 
 }
 
 /* ------------------------------------------------------------------ */
+/* k_tile_persist: the streaming tile's persistent consumer.
+ *
+ * The reference verify tile (src/app/frank/load/fd_frank_verify_synth_load.c:
+ * 219-437) verifies one frag per call on one core; N tiles scale it.  Here
+ * one launch per tile run holds every wave slot of the GPU (one single-wave
+ * workgroup per slot) and verifies what the tile's host thread hands over
+ * through mapped host memory: the frags' ring entries, and CHUNK
+ * descriptors {first ring index, count, mode} that the host cuts from each
+ * hand-off (mode: 8 lanes per signature while the GPU is lightly loaded,
+ * for latency; 1 lane per signature under load, for throughput).
+ *
+ *   wave 0 (scout)   the only poller of host memory: it mirrors the host's
+ *                    descriptor head, its stop request and a heartbeat into
+ *                    one word per XCD (device memory, one line each);
+ *   waves 1..        take a TICKET (one atomic add per chunk, never
+ *                    retried), wait on their XCD's mirror word until
+ *                    descriptor `ticket` exists, read it, and verify the
+ *                    chunk alone: copy the frags in (and, zero-copy, out to
+ *                    their output frames), k_prep's body, k_decomp's body,
+ *                    then k_dsm8's body or k_dsm's body, then verdict + tag
+ *                    to the mapped result ring, released after a
+ *                    system-scope fence so the host sees them in full.
+ *
+ * Contention is what this layout avoids: a first version let every idle
+ * wave load the shared head and CAS a claim counter; 2000 waves on one
+ * line made every atomic take ~20 us and stalled the CUs' memory pipelines
+ * (every phase, the DSM loop included, ran 8-10x slow).  Now each chunk
+ * costs one atomic add, and a waiting wave polls its XCD's mirror with a
+ * back-off proportional to how far its ticket is from the head.  Every
+ * spin is bounded: the scout flags an error after `watchdog` ticks without
+ * a host heartbeat, a waiting wave exits after `watchdog` ticks with an
+ * unchanged mirror word, so the grid always drains.
+ *
+ * Same bodies as the batch kernels, same workspace layout (one N = 64
+ * workspace per wave): identical limbs and verdicts. */
+
+#define TILE_FRAME (1408u)   /* FD_VERIFY_AMD_FRAME_SZ */
+
+__device__ __forceinline__ u64 ld_sys64( u64 const * p ) { return __hip_atomic_load( (u64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
+__device__ __forceinline__ u32 ld_sys32( u32 const * p ) { return __hip_atomic_load( (u32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
+__device__ __forceinline__ void st_sys64( u64 * p, u64 v ) { __hip_atomic_store( p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
+__device__ __forceinline__ void st_sys32( u32 * p, u32 v ) { __hip_atomic_store( p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
+__device__ __forceinline__ u64 ld_dev64( u64 const * p ) { return __hip_atomic_load( (u64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
+__device__ __forceinline__ void st_dev64( u64 * p, u64 v ) { __hip_atomic_store( p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
+__device__ __forceinline__ u64 rfl64( u64 v ) {
+  return ((u64)(u32)__builtin_amdgcn_readfirstlane( (int)(u32)(v >> 32) ) << 32) | (u32)__builtin_amdgcn_readfirstlane( (int)(u32)v );
+}
+
+/* mirror word: descriptor head | scout heartbeat << 48 | err << 62 | stop << 63 */
+#define TILE_MW_HEAD(w)  ((w) & ((1UL << 48) - 1UL))
+#define TILE_MW_ERR      (1UL << 62)
+#define TILE_MW_STOP     (1UL << 63)
+
+/* per-wave scratch: an N = 64 workspace, then the chunk's frames and planes */
+struct tile_scratch_t { size_t mir, pub, sig, off, sz, err, total; };
+__host__ __device__ constexpr tile_scratch_t tile_scratch_layout( void ) {
+  tile_scratch_t S = {}; size_t o = ws_al( ws_layout_const( 64 ).total );
+  S.mir = o; o = ws_al( o + 64UL*TILE_FRAME );
+  S.pub = o; o = ws_al( o + 64UL*32UL );
+  S.sig = o; o = ws_al( o + 64UL*64UL );
+  S.off = o; o = ws_al( o + 64UL*4UL );
+  S.sz  = o; o = ws_al( o + 64UL*4UL );
+  S.err = o; o = ws_al( o + 64UL );
+  S.total = o;
+  return S;
+}
+
+size_t fd_amd_tile_scratch_stride( void ) { return tile_scratch_layout().total; }
+
+/* The scout (wave 0, lane 0): host words -> the XCDs' mirror words. */
+__device__ __noinline__ void
+tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog ) {
+  u64 word = ld_dev64( &D->mw[0].w ), lastb = ~0UL, beat = 0UL;
+  u64 tb = __builtin_amdgcn_s_memrealtime(), tpub = tb;
+  for( ;; ) {
+    u64 h = ld_sys64( &H->head ), b = ld_sys64( &H->beat );
+    u32 st = ld_sys32( &H->stop );
+    u64 now = __builtin_amdgcn_s_memrealtime();
+    if( b != lastb ) { lastb = b; tb = now; }
+    bool dead = now - tb > watchdog;
+    if( dead ) st_sys32( &H->kerr, 1u );
+    /* the heartbeat field advances at most every 10 us (it only keeps the
+       waiting waves' own watchdog quiet) */
+    if( now - tpub > 1000UL && now - tb < 1000UL ) { beat++; tpub = now; }
+    u64 w = (h & ((1UL << 48) - 1UL)) | ((beat & 0x3fffUL) << 48) | (dead ? TILE_MW_ERR : 0UL) | (st ? TILE_MW_STOP : 0UL);
+    if( w != word ) {
+      word = w;
+      _Pragma("unroll") for( int x=0; x<FD_AMD_TILE_MIRRORS; x++ ) st_dev64( &D->mw[x].w, w );
+    }
+    if( st || dead ) break;
+    __builtin_amdgcn_s_sleep( 2 );
+  }
+}
+
+/* Verify ring entries [c0, c0 + k) (k <= 64) on this wave. */
+__device__ __forceinline__ void
+tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __restrict__ scr, ws_layout_t L,
+            tile_scratch_t const & S, i32 (* __restrict__ bi)[48], u64 (* __restrict__ evl)[33], u64 * pt ) {
+  /* pt (debug, A.prof): s_memrealtime ticks spent in gather, prep + decomp,
+     DSM, results; wave-uniform values */
+  u64 ts = A.prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
+# define TILE_STAMP( k_ ) do { if( A.prof ) { u64 t_ = __builtin_amdgcn_s_memrealtime(); pt[k_] += t_ - ts; ts = t_; } } while(0)
+  /* opaque per chunk: otherwise the compiler hoists every per-lane address
+     of the bodies out of the persistent loop and spills them */
+  {
+    __attribute__((address_space(1))) u8 * g = (__attribute__((address_space(1))) u8 *)scr;
+    asm volatile( "" : "+s"(g) );
+    scr = (u8 *)g;     /* still known global: global, not flat, accesses */
+  }
+  u32 l = threadIdx.x;
+  asm volatile( "" : "+v"(l) );
+  u8 * ws = scr; u8 * mir = scr + S.mir; u8 * pub = scr + S.pub; u8 * sig = scr + S.sig;
+  u32 * off = (u32 *)(scr + S.off); u32 * sz = (u32 *)(scr + S.sz); i8 * err = (i8 *)(scr + S.err);
+
+  /* 1. the chunk's ring entries, lane q holds entry q (host memory: system-scope loads) */
+  u32 e_src = 0u, e_out = 0u, e_sz = 96u;
+  if( l < k ) {
+    u64 const * ep = (u64 const *)(A.ent + ((c0 + l) & A.mask));
+    u64 w0 = ld_sys64( ep ), w1 = ld_sys64( ep + 1 );
+    e_src = (u32)w0; e_out = (u32)(w0 >> 32); e_sz = (u32)w1;
+  }
+  /* 2. copy the frags in: four frags per round, 16 lanes each, up to six
+        16-B words per lane issued before any is stored (frames <= 1328 B =
+        83 words; frames are chunk-aligned, so every 16-B word is whole) */
+  {
+    u32 const g = l >> 4, j = l & 15u;
+    for( u32 q0 = 0; q0 < k; q0 += 4u ) {
+      u32 const q = q0 + g;
+      u32 const src = (u32)__shfl( (int)e_src, (int)(q & 63u) );
+      u32 const oc  = (u32)__shfl( (int)e_out, (int)(q & 63u) );
+      u32 const fs  = (u32)__shfl( (int)e_sz,  (int)(q & 63u) );
+      u32 const nv  = q < k ? (fs + 15u) >> 4 : 0u;
+      uint4 const * s = (uint4 const *)(((A.dbg & 8u) ? A.src_dev : A.src) + ((size_t)src << 6));
+      uint4 v[6];
+      _Pragma("unroll") for( int r=0; r<6; r++ ) {
+        u32 w = j + 16u*(u32)r;
+        v[r] = w < nv ? s[w] : make_uint4( 0u, 0u, 0u, 0u );
+      }
+      uint4 * m = (uint4 *)(mir + (size_t)(q & 63u) * TILE_FRAME);
+      uint4 * o = (A.out && !(A.dbg & 16u)) ? (uint4 *)(A.out + ((size_t)oc << 6)) : (uint4 *)0;
+      _Pragma("unroll") for( int r=0; r<6; r++ ) {
+        u32 w = j + 16u*(u32)r;
+        if( w < nv ) { m[w] = v[r]; if( o ) o[w] = v[r]; }
+      }
+      if( q < k ) {
+        if( j < 2u )      ((uint4 *)(pub + 32u*q))[j]      = v[0];
+        else if( j < 6u ) ((uint4 *)(sig + 64u*q))[j - 2u] = v[0];
+      }
+    }
+    if( l < k ) { off[l] = l * TILE_FRAME + 96u; sz[l] = e_sz - 96u; }
+  }
+  __syncthreads();
+  TILE_STAMP( 0 );
+  /* 3. the verify pipeline on the chunk (k_prep, k_decomp, k_dsm8 / k_dsm bodies) */
+  prep_body( l, k, pub, sig, off, sz, mir, err, ws, L, (i8 const *)0 );
+  __syncthreads();
+  decomp_body( l, k, pub, sig, err, ws, L, true );                 /* points 0..63: signatures 0..31 */
+  if( k > 32u ) decomp_body( l + 64u, k, pub, sig, err, ws, L, true );
+  __syncthreads();
+  TILE_STAMP( 1 );
+  if( eight ) dsm8_body( l, k, err, ws, L, 0, bi, evl );
+  else        dsm_lane_body( l, k, err, ws, L, 0, bi, evl );
+  __syncthreads();
+  TILE_STAMP( 2 );
+  /* 4. results: tags (and, zero-copy, the output frames above) first, one
+        system-scope release, then the words the host polls */
+  u64 idx = c0 + l;
+  fd_amd_tile_res_t * r = A.res + (idx & A.mask);
+  if( l < k ) st_sys64( &r->tag, ((u64 const *)(ws + L.tag))[l] );
+  __builtin_amdgcn_fence( __ATOMIC_RELEASE, "" );
+  asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
+  if( l < k ) st_sys64( &r->word, ((idx + 1UL) << 8) | (u64)(u8)err[l] );
+  TILE_STAMP( 3 );
+# undef TILE_STAMP
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_tile_persist( fd_amd_tile_args_t A ) {
+  constexpr ws_layout_t    L = ws_layout_const( 64 );   /* every plane offset an immediate */
+  constexpr tile_scratch_t S = tile_scratch_layout();
+  __shared__ __attribute__((aligned(16))) i32 bi[8][48];
+  __shared__ u64 evl[64][33];
+  fd_amd_tile_dctl_t * D = A.dctl;
+  u32 const l = threadIdx.x;
+  if( blockIdx.x == 0u ) {
+    if( l == 0u ) tile_scout( D, A.hctl, A.watchdog );
+    return;
+  }
+  bi12_fill( bi );
+  __syncthreads();
+  /* this wave's mirror word: its XCD's (HW_REG_XCC_ID) */
+  u32 const xcc = __builtin_amdgcn_s_getreg( 20 | (0 << 6) | (3 << 11) ) % FD_AMD_TILE_MIRRORS;
+  u64 const * mw = &D->mw[xcc].w;
+  u8 * scr = A.scratch + (size_t)blockIdx.x * S.total;
+  u64 n8 = 0, n64 = 0, f8 = 0, f64 = 0;
+  u64 pt[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };   /* debug (A.prof): gather, front, DSM, results, wait, fence, -, - */
+  for( ;; ) {
+    u64 t = 0;
+    if( l == 0u ) t = atomicAdd( (unsigned long long *)&D->ticket, 1ULL );
+    t = rfl64( t );
+    /* wait for descriptor t: poll the mirror, backing off with the
+       distance to the head (the next in line polls every ~0.2 us) */
+    u64 t0 = __builtin_amdgcn_s_memrealtime(), tw = t0, last = ~0UL;
+    bool go = false;
+    for( ;; ) {
+      u64 const w = rfl64( l == 0u ? ld_dev64( mw ) : 0UL );
+      if( TILE_MW_HEAD( w ) > t ) { go = true; break; }
+      if( w & (TILE_MW_ERR | TILE_MW_STOP) ) break;
+      u64 const now = __builtin_amdgcn_s_memrealtime();
+      if( w != last ) { last = w; tw = now; }
+      else if( now - tw > A.watchdog ) break;       /* no scout (or host) for that long: give up */
+      u64 const d = t - TILE_MW_HEAD( w );
+      u32 const nap = d < 2UL ? 1u : d < 64UL ? (u32)d : 64u;
+      for( u32 z = 0; z < nap; z++ ) __builtin_amdgcn_s_sleep( 4 );
+    }
+    if( A.prof ) pt[4] += __builtin_amdgcn_s_memrealtime() - t0;
+    if( !go ) break;
+    /* descriptor t (host memory): { first ring index, count | latency mode << 31 } */
+    u64 c = 0, cm = 0;
+    if( l == 0u ) {
+      u64 const * dp = (u64 const *)(A.desc + (t & A.mask));
+      c = ld_sys64( dp ); cm = ld_sys64( dp + 1 );
+    }
+    c = rfl64( c ); cm = rfl64( cm );
+    u32 const take = (u32)cm & 0x7fffffffu;
+    bool const e8 = ((u32)cm >> 31) != 0u;
+    /* the frames were written by the host (copy mode) or the producer
+       (zero-copy) into host memory: drop this CU's stale lines first */
+    u64 const tf = A.prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
+    __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "" );
+    asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
+    if( A.prof ) pt[5] += __builtin_amdgcn_s_memrealtime() - tf;
+    if( take && take <= 64u ) tile_chunk( A, c, take, e8, scr, L, S, bi, evl, pt );
+    if( e8 ) { n8++; f8 += take; } else { n64++; f64 += take; }
+  }
+  if( l == 0u ) {
+    atomicAdd( (unsigned long long *)&D->stat[0], (unsigned long long)n8 );
+    atomicAdd( (unsigned long long *)&D->stat[1], (unsigned long long)n64 );
+    atomicAdd( (unsigned long long *)&D->stat[2], (unsigned long long)f8 );
+    atomicAdd( (unsigned long long *)&D->stat[3], (unsigned long long)f64 );
+    if( A.prof ) { _Pragma("unroll") for( int q=0; q<8; q++ ) atomicAdd( (unsigned long long *)&D->prof[q], (unsigned long long)pt[q] ); }
+  }
+}
+
+int
+fd_amd_launch_tile_persist( fd_amd_tile_args_t const * a, uint32_t waves, hipStream_t stream ) {
+  if( waves < 2u ) return -1;
+  hipLaunchKernelGGL( k_tile_persist, dim3(waves), dim3(64), 0, stream, *a );
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+/* ------------------------------------------------------------------ */
 /* launch                                                               */
 
 /* debug: dense u16 [n][256] digits from the event lists */
@@ -1981,6 +2178,12 @@ fd_amd_launch_copy_out( void * d_dst, void const * d_src, size_t n, hipStream_t 
 static volatile u32 g_dsm4_max = 16384u;
 static volatile u32 g_dsm8_max = 8192u;
 static volatile u32 g_pool_min = 1u << 19;   /* k_dsmp from 2^19 signatures (pooled A/B) */
+static volatile u64 g_pool_iter_cap = ~0UL;   /* debug: cap on k_dsmp's step loop (its hang guard) */
+
+extern "C" void
+fd_ed25519_amd_debug_set_pool_iter_cap( unsigned long cap ) {
+  g_pool_iter_cap = cap ? cap : ~0UL;
+}
 
 extern "C" void
 fd_ed25519_amd_set_pool_batch_min( unsigned long n ) {
@@ -2055,7 +2258,7 @@ fd_amd_launch_verify( u32 n, u8 const * d_pub, u8 const * d_sig, u32 const * d_o
     if( ev ) (void)hipEventRecord( ev[2], stream );
     if( pooled ) {
       hipLaunchKernelGGL( k_ai,   dim3(nb),    dim3(64), 0, stream, n, d_err, ws, L );
-      hipLaunchKernelGGL( k_dsmp, dim3(pool_waves( n )), dim3(64), 0, stream, n, ws, L );
+      hipLaunchKernelGGL( k_dsmp, dim3(pool_waves( n )), dim3(64), 0, stream, n, ws, L, (u64)g_pool_iter_cap );
       hipLaunchKernelGGL( k_fin,  dim3(nb),    dim3(64), 0, stream, n, d_err, ws, L, want_stats );
     } else {
       hipLaunchKernelGGL( k_dsm,  dim3(nb),    dim3(64), 0, stream, n, d_err, ws, L, want_stats );

@@ -42,8 +42,18 @@ fd_ed25519_amd_shard_range( ulong n, ulong ndev, ulong r, ulong * lo, ulong * hi
   *hi = (ulong)(((unsigned __int128)n * (r + 1UL)) / ndev);
 }
 
+/* Engine r's thread: bound to its device's NUMA node (CPUs and memory,
+   fd_numa.cpp), it creates the engine there (so the pinned staging it
+   fills is node-local), then serves batches. */
 static void
-worker( fd_ed25519_amd_multi_t * m, ulong r ) {
+worker( fd_ed25519_amd_multi_t * m, ulong r, int device, ulong batch_max, ulong blob_max ) {
+  (void)fd_amd_numa_bind_thread( device );
+  fd_ed25519_amd_t * e = fd_ed25519_amd_new( device, batch_max, blob_max );
+  {
+    std::lock_guard<std::mutex> lk( m->mu );
+    m->eng[r] = e;
+    if( !--m->pending ) m->cv_done.notify_all();
+  }
   ulong seen = 0;
   for( ;; ) {
     std::function<int( ulong )> job;
@@ -88,7 +98,7 @@ fd_ed25519_amd_multi_delete( fd_ed25519_amd_multi_t * m ) {
   }
   m->cv_go.notify_all();
   for( auto & t : m->th ) if( t.joinable() ) t.join();
-  for( auto * e : m->eng ) fd_ed25519_amd_delete( e );
+  for( auto * e : m->eng ) if( e ) fd_ed25519_amd_delete( e );
   delete m;
 }
 
@@ -98,12 +108,14 @@ fd_ed25519_amd_multi_new( int const * devices, ulong ndev, ulong batch_max, ulon
   fd_ed25519_amd_multi_t * m = new fd_ed25519_amd_multi_t();
   m->ndev = ndev;
   m->rc.assign( ndev, 0 );
-  for( ulong r=0; r<ndev; r++ ) {
-    fd_ed25519_amd_t * e = fd_ed25519_amd_new( devices[r], batch_max, blob_max );
-    if( !e ) { fd_ed25519_amd_multi_delete( m ); return NULL; }
-    m->eng.push_back( e );
+  m->eng.assign( ndev, NULL );
+  m->pending = ndev;
+  for( ulong r=0; r<ndev; r++ ) m->th.emplace_back( worker, m, r, devices[r], batch_max, blob_max );
+  {
+    std::unique_lock<std::mutex> lk( m->mu );
+    m->cv_done.wait( lk, [&]{ return !m->pending; } );
   }
-  for( ulong r=0; r<ndev; r++ ) m->th.emplace_back( worker, m, r );
+  for( ulong r=0; r<ndev; r++ ) if( !m->eng[r] ) { fd_ed25519_amd_multi_delete( m ); return NULL; }
   return m;
 }
 

@@ -176,7 +176,25 @@ struct fd_verify_amd_tile {
   ulong              frame_cnt;
   std::vector<ulong> frame_pub;  /* out seq of the frag a frame last carried (FRAME_FREE: none) */
   ulong              frame_next, frame_retired;
+  ulong              out_seq_end;   /* out seq after the last run's last publish (a run continuing it keeps frame_pub) */
   tile_slot_t        ts[FD_AMD_SLOT_MAX];
+  /* persistent consumer (PUB_SIG_MSG framing, k_tile_persist) */
+  hipStream_t          pst;
+  hipEvent_t           pdone;
+  fd_amd_tile_hctl_t * hctl;  void * hctl_dev;
+  fd_amd_tile_ent_t *  ring;  void * ring_dev;
+  fd_amd_tile_desc_t * desc;  void * desc_dev;   /* chunk descriptors (same size as the ring) */
+  fd_amd_tile_res_t *  res;   void * res_dev;
+  fd_amd_tile_dctl_t * dctl;
+  uint8_t *            scratch;
+  ulong                R;          /* ring size (power of 2) */
+  ulong                window;     /* frags in flight at most (handed to the GPU, not yet published) */
+  uint32_t             waves;
+  ulong                light_frags;   /* hand-offs while fewer frags are in flight are cut into latency chunks */
+  ulong                desc_seq;      /* descriptors published, monotonic over the tile's life */
+  std::vector<pending_t> ppend;    /* per ring slot */
+  ulong                ring_seq;   /* ring index of the next frag, monotonic over the tile's life */
+  bool                 batched;    /* FD_AMD_TILE_BATCHED=1: the multi-stream batch path for every framing (A/B) */
 };
 
 extern "C" int
@@ -235,7 +253,67 @@ fd_verify_amd_tile_delete( fd_verify_amd_tile_t * t ) {
     if( t->ts[k].d_mir  ) (void)hipFree( t->ts[k].d_mir );
   }
   if( t->out_base ) (void)hipHostFree( t->out_base );
+  if( t->pst )     (void)hipStreamDestroy( t->pst );
+  if( t->pdone )   (void)hipEventDestroy( t->pdone );
+  if( t->hctl )    (void)hipHostFree( t->hctl );
+  if( t->ring )    (void)hipHostFree( t->ring );
+  if( t->desc )    (void)hipHostFree( t->desc );
+  if( t->res )     (void)hipHostFree( t->res );
+  if( t->dctl )    (void)hipFree( t->dctl );
+  if( t->scratch ) (void)hipFree( t->scratch );
   delete t;
+}
+
+static ulong
+env_ulong( char const * name, ulong dflt ) {
+  char const * v = getenv( name );
+  return ( v && *v ) ? strtoul( v, NULL, 0 ) : dflt;
+}
+
+/* The persistent consumer's resources: control words, ring and results in
+   mapped coherent host memory, the device control block, per-wave scratch.
+   Window (frags in flight): 64 x batch_max, at least 2^13, at most 2^18
+   (FD_AMD_TILE_WINDOW overrides): a larger batch_max buys throughput with
+   latency at saturation, as more batches in flight did in the batch path.
+   Waves: 8 per CU, every wave slot of a kernel at 2 waves per SIMD
+   (FD_AMD_TILE_WAVES overrides, e.g. to share a GPU between tiles). */
+static int
+tile_persist_alloc( fd_verify_amd_tile_t * t ) {
+  ulong W = t->batch_max >= (1UL << 12) ? (1UL << 18) : std::max( 64UL * t->batch_max, 1UL << 13 );
+  W = env_ulong( "FD_AMD_TILE_WINDOW", W );
+  if( W > t->frame_cnt ) W = t->frame_cnt;
+  if( !W ) return FD_ED25519_AMD_ERR_INVAL;
+  ulong R = 1UL; while( R < W ) R <<= 1;
+  int cus = 0;
+  if( hipDeviceGetAttribute( &cus, hipDeviceAttributeMultiprocessorCount, t->eng->device ) != hipSuccess || cus <= 0 ) cus = 256;
+  ulong waves = env_ulong( "FD_AMD_TILE_WAVES", 8UL * (ulong)cus );
+  if( waves < 2UL || waves > 65536UL ) return FD_ED25519_AMD_ERR_INVAL;
+  t->window = W; t->R = R; t->waves = (uint32_t)waves;
+  /* latency chunks (8 frags, 8 lanes per signature) while at most one such
+     chunk per SIMD is in flight: 8 x 4 x CUs frags */
+  t->light_frags = env_ulong( "FD_AMD_TILE_LIGHT_FRAGS", 32UL * (ulong)cus );
+  unsigned const hf = hipHostMallocMapped | hipHostMallocCoherent;
+  if( hipStreamCreateWithFlags( &t->pst, hipStreamNonBlocking ) != hipSuccess ||
+      hipEventCreateWithFlags( &t->pdone, hipEventDisableTiming ) != hipSuccess ||
+      hipHostMalloc( (void **)&t->hctl, sizeof(fd_amd_tile_hctl_t), hf ) != hipSuccess ||
+      hipHostGetDevicePointer( &t->hctl_dev, t->hctl, 0 ) != hipSuccess ||
+      hipHostMalloc( (void **)&t->ring, R * sizeof(fd_amd_tile_ent_t), hf ) != hipSuccess ||
+      hipHostGetDevicePointer( &t->ring_dev, t->ring, 0 ) != hipSuccess ||
+      hipHostMalloc( (void **)&t->desc, R * sizeof(fd_amd_tile_desc_t), hf ) != hipSuccess ||
+      hipHostGetDevicePointer( &t->desc_dev, t->desc, 0 ) != hipSuccess ||
+      hipHostMalloc( (void **)&t->res, R * sizeof(fd_amd_tile_res_t), hf ) != hipSuccess ||
+      hipHostGetDevicePointer( &t->res_dev, t->res, 0 ) != hipSuccess ||
+      hipMalloc( (void **)&t->dctl, sizeof(fd_amd_tile_dctl_t) ) != hipSuccess ||
+      hipMalloc( (void **)&t->scratch, waves * fd_amd_tile_scratch_stride() ) != hipSuccess )
+    return FD_ED25519_AMD_ERR_DEVICE;
+  memset( t->hctl, 0, sizeof(fd_amd_tile_hctl_t) );
+  memset( t->ring, 0, R * sizeof(fd_amd_tile_ent_t) );
+  memset( t->desc, 0, R * sizeof(fd_amd_tile_desc_t) );
+  t->desc_seq = 0UL;
+  memset( t->res,  0, R * sizeof(fd_amd_tile_res_t) );   /* word 0 never matches an index + 1 */
+  t->ppend.resize( R );
+  t->ring_seq = 0UL;
+  return FD_ED25519_AMD_OK;
 }
 
 extern "C" fd_verify_amd_tile_t *
@@ -244,7 +322,11 @@ fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong 
   int nslot = TILE_NSLOT;
   if( char const * v = getenv( "FD_AMD_TILE_NSLOT" ) ) nslot = atoi( v );
   if( nslot < 2 || nslot > FD_AMD_SLOT_MAX ) return NULL;
-  if( !out_frame_cnt ) out_frame_cnt = 4096UL + (ulong)(nslot + 1) * batch_max;
+  if( !out_frame_cnt ) {   /* the frags in flight (window, or the batch path's slots) + the staging group + the consumer's lag */
+    ulong W = batch_max >= (1UL << 12) ? (1UL << 18) : std::max( 64UL * batch_max, 1UL << 13 );
+    W = env_ulong( "FD_AMD_TILE_WINDOW", W );
+    out_frame_cnt = 4096UL + batch_max + std::max( W, (ulong)nslot * batch_max );
+  }
   if( out_frame_cnt > (0xFFFFFFFFUL / FRAME_CHUNKS) ) return NULL;   /* chunk indices are 32-bit */
   /* the engine's own staging is unused by the tile (frags reach the GPU
      through the output frames), so it is sized for a single message */
@@ -265,9 +347,12 @@ fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong 
   }
   ok = ok && hipHostMalloc( (void **)&t->out_base, out_frame_cnt * FD_VERIFY_AMD_FRAME_SZ, hipHostMallocMapped ) == hipSuccess &&
        hipHostGetDevicePointer( (void **)&t->out_dev, t->out_base, 0 ) == hipSuccess;
-  if( !ok ) { fd_verify_amd_tile_delete( t ); return NULL; }
   t->frame_cnt = out_frame_cnt;
   t->frame_pub.assign( out_frame_cnt, FRAME_FREE );
+  t->out_seq_end = ~0UL;
+  t->batched = env_ulong( "FD_AMD_TILE_BATCHED", 0UL ) != 0UL;
+  ok = ok && ( t->batched || !tile_persist_alloc( t ) );
+  if( !ok ) { fd_verify_amd_tile_delete( t ); return NULL; }
   return t;
 }
 
@@ -325,8 +410,37 @@ tile_launch( fd_verify_amd_tile_t * t, int k, ulong n, bool txn, uint8_t const *
   if( hipEventRecord( s->done, s->stream ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
   s->out = s->t_out = s->s_out = NULL;
   s->n = n; s->t_n = n; s->busy = 1;
+  s->chk_err = txn ? 0 : n; s->chk_terr = txn ? n : 0;
   return FD_ED25519_AMD_OK;
 }
+
+/* Error exit of the batch path: wait for every batch still in flight (a
+   queued k_tile_gather reads its slot's mapped metadata in place, which the
+   next run rewrites) and forget them. */
+static int
+tile_quiesce( fd_verify_amd_tile_t * t, int rc ) {
+  for( int k=0; k<t->nslot; k++ ) {
+    slot_t * s = &t->eng->slot[k];
+    if( s->busy ) (void)hipEventSynchronize( s->done );
+    s->out = s->t_out = s->s_out = NULL;
+    s->busy = 0;
+  }
+  return rc;
+}
+
+static int
+tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ulong in_depth, void const * in_chunk0,
+                  ulong in_seq0, ulong * in_fseq, fd_frag_meta_t * out_mcache, ulong out_depth, ulong out_seq0,
+                  ulong const * out_fseq, ulong frag_cnt, int const * stop, fd_verify_amd_diag_t * diag, uint * lat,
+                  ulong lat_max, uint8_t const * zc_dev, ulong zc_lim );
+
+/* The multi-stream batch path: TXN framing (and every framing under
+   FD_AMD_TILE_BATCHED=1). */
+static int
+tile_run_batched( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ulong in_depth, void const * in_chunk0,
+                  ulong in_seq0, ulong * in_fseq, fd_frag_meta_t * out_mcache, ulong out_depth, ulong out_seq0,
+                  ulong const * out_fseq, ulong frag_cnt, int const * stop, fd_verify_amd_diag_t * diag, uint * lat,
+                  ulong lat_max, uint8_t const * zc_dev, ulong zc_lim );
 
 extern "C" int
 fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ulong in_depth,
@@ -335,16 +449,45 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
                         fd_verify_amd_diag_t * diag, uint * lat, ulong lat_max ) {
   if( !t || !in_mcache || !in_depth || (in_depth & (in_depth-1UL)) || !in_chunk0 || !out_mcache || !out_depth ||
       (out_depth & (out_depth-1UL)) || !diag || (!frag_cnt && !stop) ) return FD_ED25519_AMD_ERR_INVAL;
-  fd_ed25519_amd_t * e = t->eng;
-  if( hipSetDevice( e->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  if( hipSetDevice( t->eng->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
   bool txn = t->framing == FD_VERIFY_AMD_FRAMING_TXN;
   if( txn && t->batch_max < TXN_SIG_MAX_AT_MTU ) return FD_ED25519_AMD_ERR_INVAL;
 
-  ulong const F = t->frame_cnt;
-  /* a new run starts a new output session: no frame is held for a consumer */
-  std::fill( t->frame_pub.begin(), t->frame_pub.end(), FRAME_FREE );
+  /* Output session.  A run whose out_seq0 continues the previous run's
+     output keeps the frames' publication record, so a frame a lagging
+     consumer may still read is not reused before out_fseq passes it; any
+     other out_seq0 starts a new session (a new consumer), with every frame
+     free. */
+  if( out_seq0 != t->out_seq_end ) std::fill( t->frame_pub.begin(), t->frame_pub.end(), FRAME_FREE );
   t->frame_next = t->frame_retired = 0UL;
 
+  /* zero copy: the input data region is mapped into the GPU; frags are
+     handed over as (chunk, size) and copied on the device.  zc_lim: bytes
+     of the mapped region from in_chunk0 on (a frag reaching past it is
+     refused as a bad frag, never read by the GPU). */
+  uint8_t const * zc_dev = NULL;
+  ulong zc_lim = 0UL;
+  if( t->reg_base && (uint8_t const *)in_chunk0 >= t->reg_base &&
+      (uint8_t const *)in_chunk0 < t->reg_base + t->reg_sz &&
+      t->reg_sz - (ulong)((uint8_t const *)in_chunk0 - t->reg_base) <= (1UL << 38) ) {
+    zc_dev = t->reg_dev + ((uint8_t const *)in_chunk0 - t->reg_base);
+    zc_lim = t->reg_sz - (ulong)((uint8_t const *)in_chunk0 - t->reg_base);
+  }
+  if( !txn && !t->batched )
+    return tile_run_persist( t, in_mcache, in_depth, in_chunk0, in_seq0, in_fseq, out_mcache, out_depth, out_seq0, out_fseq,
+                             frag_cnt, stop, diag, lat, lat_max, zc_dev, zc_lim );
+  return tile_run_batched( t, in_mcache, in_depth, in_chunk0, in_seq0, in_fseq, out_mcache, out_depth, out_seq0, out_fseq,
+                           frag_cnt, stop, diag, lat, lat_max, zc_dev, zc_lim );
+}
+
+static int
+tile_run_batched( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ulong in_depth, void const * in_chunk0,
+                  ulong in_seq0, ulong * in_fseq, fd_frag_meta_t * out_mcache, ulong out_depth, ulong out_seq0,
+                  ulong const * out_fseq, ulong frag_cnt, int const * stop, fd_verify_amd_diag_t * diag, uint * lat,
+                  ulong lat_max, uint8_t const * zc_dev, ulong zc_lim ) {
+  fd_ed25519_amd_t * e = t->eng;
+  bool txn = t->framing == FD_VERIFY_AMD_FRAMING_TXN;
+  ulong const F = t->frame_cnt;
   ulong in_seq = in_seq0, out_seq = out_seq0, lat_n = 0;
   int   K = t->nslot;
   int   stage = 0;                 /* slot being filled; slots are used round robin, so the */
@@ -356,14 +499,6 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
      in housekeeping, fd_fctl): diag->in_cnt and in_fseq are published per
      staging pass; out_fseq is re-read only when a cached value runs out. */
   ulong in_cnt = diag->in_cnt, out_cr = 0, cons = out_seq0, fseq_pub = ~0UL;
-
-  /* zero copy: the input data region is mapped into the GPU; frags are
-     handed over as (chunk, size) and copied on the device */
-  uint8_t const * zc_dev = NULL;
-  if( t->reg_base && (uint8_t const *)in_chunk0 >= t->reg_base &&
-      (uint8_t const *)in_chunk0 < t->reg_base + t->reg_sz &&
-      t->reg_sz - (ulong)((uint8_t const *)in_chunk0 - t->reg_base) <= (1UL << 38) )
-    zc_dev = t->reg_dev + ((uint8_t const *)in_chunk0 - t->reg_base);
 
   auto publish = [&]( int k ) -> int {
     slot_t *      s  = &e->slot[k];
@@ -405,9 +540,9 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
           arrival order: batches retire in launch order) */
     while( nfly ) {
       int r = fd_amd_slot_ready( &e->slot[oldest] );
-      if( r < 0 ) return r;
+      if( r < 0 ) return tile_quiesce( t, r );
       if( !r ) break;
-      if( (rc = publish( oldest )) ) return rc;
+      if( (rc = publish( oldest )) ) return tile_quiesce( t, rc );
       oldest = (oldest + 1) % K; nfly--;
     }
     /* producer credit: copy mode is done with a frag once it is copied;
@@ -433,7 +568,8 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
       ulong chunk = m->chunk, sz = m->sz, ctl = m->ctl, tsorig = m->tsorig;
       __atomic_thread_fence( __ATOMIC_ACQUIRE );
       if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != in_seq ) { diag->ovrn_cnt++; in_seq++; continue; }
-      if( txn ? (!sz || sz > FD_ED25519_AMD_MSG_MAX) : (sz < 96UL || sz - 96UL > FD_ED25519_AMD_MSG_MAX) ) {
+      if( (txn ? (!sz || sz > FD_ED25519_AMD_MSG_MAX) : (sz < 96UL || sz - 96UL > FD_ED25519_AMD_MSG_MAX)) ||
+          (zc_dev && (chunk << FD_CHUNK_LG_SZ) + ((sz + 63UL) & ~63UL) > zc_lim) ) {
         diag->bad_frag_cnt++; in_seq++; in_cnt++; continue;
       }
       /* reserve the next output frame: not staged or in flight, and no
@@ -493,7 +629,7 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
       ts.nsig = slots;
       ts.frame_hi = t->frame_next;
       uint8_t const * src = zc_dev ? zc_dev : t->out_dev;
-      if( (rc = tile_launch( t, stage, staged, txn, src, zc_dev ? t->out_dev : NULL )) ) return rc;
+      if( (rc = tile_launch( t, stage, staged, txn, src, zc_dev ? t->out_dev : NULL )) ) return tile_quiesce( t, rc );
       diag->batch_sig_cnt += txn ? slots : staged;
       diag->batch_cnt++;
       nfly++;
@@ -502,7 +638,246 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
   }
   __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
   if( in_fseq ) __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE );
+  t->out_seq_end = out_seq;
   return FD_ED25519_AMD_OK;
+}
+
+/* The persistent path (PUB_SIG_MSG framing).  One k_tile_persist launch
+   per run; the host thread polls, dedups and stages frags into the ring,
+   hands them over by advancing the ring head, and publishes verdicts in
+   ring order as the GPU's result words arrive.  Nothing here waits on a
+   HIP call: the GPU side is driven entirely through mapped memory.
+
+     stage   -- as the batch path (poll, dedup, reserve an output frame;
+                copy mode: copy the frag there), then write the frag's
+                ring entry
+     hand    -- advance the ring head (the GPU's claimable range): when
+                batch_max frags are staged, the input is momentarily
+                drained (greedy; with batch_wait_ns only while nothing is
+                in flight), the input ended, the window or the frames ran
+                out, or the oldest staged frag waited batch_wait_ns
+     publish -- the next frag in ring order whose result word carries its
+                index: lapped (zero copy) -> overrun, failed -> SV_FILT,
+                else fd_mcache_publish out of its output frame
+
+   The window (t->window frags handed over and not yet published) bounds
+   the GPU's work in flight; with the output frames it is the tile's
+   backpressure on the producer. */
+static int
+tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ulong in_depth, void const * in_chunk0,
+                  ulong in_seq0, ulong * in_fseq, fd_frag_meta_t * out_mcache, ulong out_depth, ulong out_seq0,
+                  ulong const * out_fseq, ulong frag_cnt, int const * stop, fd_verify_amd_diag_t * diag, uint * lat,
+                  ulong lat_max, uint8_t const * zc_dev, ulong zc_lim ) {
+  ulong const F = t->frame_cnt, mask = t->R - 1UL, W = t->window, base = t->ring_seq;
+  fd_amd_tile_hctl_t * H = t->hctl;
+
+  /* seed the control words, then launch: the kernel's ticket counter and
+     the mirrors start at this run's first descriptor */
+  ulong const dbase = t->desc_seq;
+  __atomic_store_n( &H->head, dbase, __ATOMIC_RELAXED );
+  __atomic_store_n( &H->stop, 0u, __ATOMIC_RELAXED );
+  __atomic_store_n( &H->kerr, 0u, __ATOMIC_RELAXED );
+  ulong beat = __atomic_load_n( &H->beat, __ATOMIC_RELAXED );
+  {
+    fd_amd_tile_dctl_t d0;
+    memset( &d0, 0, sizeof d0 );
+    d0.ticket = dbase;
+    for( int x=0; x<FD_AMD_TILE_MIRRORS; x++ ) d0.mw[x].w = dbase;
+    if( hipMemcpyAsync( t->dctl, &d0, sizeof d0, hipMemcpyHostToDevice, t->pst ) != hipSuccess ||
+        hipStreamSynchronize( t->pst ) != hipSuccess )
+      return FD_ED25519_AMD_ERR_DEVICE;
+  }
+  fd_amd_tile_args_t A;
+  memset( &A, 0, sizeof A );
+  A.hctl = (fd_amd_tile_hctl_t *)t->hctl_dev;
+  A.ent  = (fd_amd_tile_ent_t const *)t->ring_dev;
+  A.desc = (fd_amd_tile_desc_t const *)t->desc_dev;
+  A.res  = (fd_amd_tile_res_t *)t->res_dev;
+  A.mask = mask;
+  A.src  = zc_dev ? zc_dev : t->out_dev;
+  A.out  = zc_dev ? t->out_dev : NULL;
+  A.dctl = t->dctl;
+  A.scratch = t->scratch;
+  A.watchdog = 500000000UL;   /* 5 s of s_memrealtime (100 MHz) without a heartbeat */
+  A.prof = (uint32_t)env_ulong( "FD_AMD_TILE_DEBUG", 0UL );
+  A.dbg  = (uint32_t)env_ulong( "FD_AMD_TILE_DBG", 0UL );
+  void * src_dev = NULL;
+  if( A.dbg & 8u ) {   /* A/B: frags read from a device copy of the source region (taken now: pre-placed frags only) */
+    ulong bytes = zc_dev ? zc_lim : t->frame_cnt * FD_VERIFY_AMD_FRAME_SZ;
+    if( hipMalloc( &src_dev, bytes ) != hipSuccess ||
+        hipMemcpy( src_dev, zc_dev ? (void const *)in_chunk0 : (void const *)t->out_base, bytes, hipMemcpyHostToDevice ) != hipSuccess )
+      return FD_ED25519_AMD_ERR_DEVICE;
+    A.src_dev = (uint8_t const *)src_dev;
+  }
+  if( fd_amd_launch_tile_persist( &A, t->waves, t->pst ) || hipEventRecord( t->pdone, t->pst ) != hipSuccess ) {
+    (void)hipStreamSynchronize( t->pst );
+    return FD_ED25519_AMD_ERR_DEVICE;
+  }
+
+  ulong in_seq = in_seq0, out_seq = out_seq0, lat_n = 0;
+  ulong staged = base, handed = base, pubd = base, hand_t0 = 0UL;
+  ulong in_cnt = diag->in_cnt, out_cr = 0, cons = out_seq0, fseq_pub = ~0UL;
+  ulong idle = 0UL;
+  int   rc = FD_ED25519_AMD_OK;
+  uchar const * in_chunk0b = (uchar const *)in_chunk0;
+
+  for( ;; ) {
+    __atomic_store_n( &H->beat, ++beat, __ATOMIC_RELAXED );
+    bool progress = false;
+
+    /* 1. publish in ring order */
+    while( pubd != handed ) {
+      fd_amd_tile_res_t const * r = t->res + (pubd & mask);
+      ulong w = __atomic_load_n( &r->word, __ATOMIC_ACQUIRE );
+      if( (w >> 8) != pubd + 1UL ) break;
+      pending_t const & m = t->ppend[pubd & mask];
+      pubd++; progress = true;
+      t->frame_retired = m.frame + 1UL;
+      /* zero copy: the GPU read the frag some time before now; if its mcache
+         line has been lapped since, the producer may have rewritten it */
+      if( zc_dev && __atomic_load_n( &in_mcache[ m.seq & (in_depth-1UL) ].seq, __ATOMIC_ACQUIRE ) != m.seq ) {
+        diag->ovrn_cnt++;
+        continue;
+      }
+      if( (schar)(uchar)(w & 0xffUL) ) { diag->sv_filt_cnt++; diag->sv_filt_sz += m.sz; continue; }
+      ulong tag = r->tag;   /* the verify's SHA-512 tag (dedup tile) */
+      if( out_fseq && (long)(out_seq - out_cr) >= 0 ) {   /* credit check against the slowest consumer */
+        out_cr = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) + out_depth;
+        if( (long)(out_seq - out_cr) >= 0 ) {
+          diag->backp_cnt++;
+          do {
+            __atomic_store_n( &H->beat, ++beat, __ATOMIC_RELAXED );
+            out_cr = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) + out_depth;
+          } while( (long)(out_seq - out_cr) >= 0 );
+        }
+      }
+      ulong f = m.frame % F;
+      t->frame_pub[f] = out_seq;
+      uint tspub = fd_verify_amd_tickcount();
+      fd_mcache_publish( out_mcache, out_depth, out_seq, tag, f * FRAME_CHUNKS, m.sz, m.ctl, m.tsorig, tspub );
+      if( lat && lat_n < lat_max ) lat[lat_n++] = tspub - m.tsorig;
+      out_seq++; diag->out_cnt++; diag->out_sz += m.sz;
+    }
+    /* producer credit: copy mode is done with a frag once it is copied,
+       zero copy once it is published (or dropped) */
+    if( in_fseq ) {
+      ulong rel = ( !zc_dev || pubd == staged ) ? in_seq : t->ppend[pubd & mask].seq;
+      if( rel != fseq_pub ) { __atomic_store_n( in_fseq, rel, __ATOMIC_RELEASE ); fseq_pub = rel; }
+    }
+    bool done_in = frag_cnt ? (in_seq - in_seq0 >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
+    if( done_in && pubd == staged ) break;
+
+    /* 2. stage */
+    bool idle_in = false, full = false;
+    while( !done_in && staged - handed < t->batch_max ) {
+      if( frag_cnt && in_seq - in_seq0 >= frag_cnt ) break;
+      if( staged - pubd >= W ) { full = true; break; }
+      fd_frag_meta_t const * m = in_mcache + (in_seq & (in_depth-1UL));
+      ulong seq_found = __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE );
+      long  d = (long)(seq_found - in_seq);
+      if( d < 0 ) { idle_in = true; break; }                             /* not yet published */
+      if( d > 0 ) { diag->ovrn_cnt += (ulong)d; in_seq = seq_found; continue; }   /* overrun: resync */
+      ulong chunk = m->chunk, sz = m->sz, ctl = m->ctl, tsorig = m->tsorig;
+      __atomic_thread_fence( __ATOMIC_ACQUIRE );
+      if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != in_seq ) { diag->ovrn_cnt++; in_seq++; continue; }
+      if( sz < 96UL || sz - 96UL > FD_ED25519_AMD_MSG_MAX ||
+          (zc_dev && (chunk << FD_CHUNK_LG_SZ) + ((sz + 63UL) & ~63UL) > zc_lim) ) {
+        diag->bad_frag_cnt++; in_seq++; in_cnt++; continue;
+      }
+      /* reserve the next output frame: not in flight, and no longer read
+         by a consumer that honours flow control */
+      ulong fr = t->frame_next, f = fr % F;
+      if( fr - t->frame_retired >= F ) { full = true; break; }
+      if( out_fseq && t->frame_pub[f] != FRAME_FREE && (long)(t->frame_pub[f] - cons) >= 0 ) {
+        cons = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE );
+        if( (long)(t->frame_pub[f] - cons) >= 0 ) { diag->backp_cnt++; full = true; break; }
+      }
+      uchar const * p = (uchar const *)fd_chunk_to_laddr_const( in_chunk0b, chunk );
+      if( !zc_dev ) {
+        /* copy mode: the frame is the tile's copy; a frag lapped while it
+           was copied is dropped (speculative read, then seq re-check) */
+        uint8_t * dst = t->out_base + f * FD_VERIFY_AMD_FRAME_SZ;
+        memcpy( dst, p, sz );
+        __atomic_thread_fence( __ATOMIC_ACQUIRE );
+        if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != in_seq ) { diag->ovrn_cnt++; in_seq++; continue; }
+        p = dst;
+      }
+      in_seq++; in_cnt++;
+      ulong ha_tag; memcpy( &ha_tag, p + 32, 8 );                        /* first 8 signature bytes */
+      if( t->tc.insert( ha_tag ) ) { diag->ha_filt_cnt++; diag->ha_filt_sz += sz; continue; }
+      t->frame_pub[f] = FRAME_FREE;
+      t->frame_next++;
+      fd_amd_tile_ent_t * en = t->ring + (staged & mask);
+      en->src_chunk = zc_dev ? (uint32_t)chunk : (uint32_t)(f * FRAME_CHUNKS);
+      en->out_chunk = (uint32_t)(f * FRAME_CHUNKS);
+      en->sz        = (uint32_t)sz;
+      t->ppend[staged & mask] = pending_t{ in_seq - 1UL, fr, (ushort)sz, (ushort)ctl, (uint)tsorig };
+      if( staged == handed && t->wait_ns ) hand_t0 = now_ns();
+      staged++; progress = true;
+    }
+    __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
+    if( in_fseq && !zc_dev && in_seq != fseq_pub ) { __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE ); fseq_pub = in_seq; }
+    done_in = frag_cnt ? (in_seq - in_seq0 >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
+
+    /* 3. hand over: cut [handed, staged) into chunks -- 8-frag latency
+          chunks while few frags are in flight, 64-frag throughput chunks
+          under load -- and publish their descriptors (x86 stores are
+          ordered: entries and descriptors are visible before the head) */
+    if( staged != handed ) {
+      bool greedy = idle_in && (!t->wait_ns || handed == pubd);
+      if( staged - handed >= t->batch_max || full || greedy || done_in ||
+          (t->wait_ns && now_ns() - hand_t0 >= t->wait_ns) ) {
+        bool lat_mode = handed - pubd < t->light_frags;
+        ulong K = lat_mode ? 8UL : 64UL, ds = t->desc_seq;
+        for( ulong c = handed; c < staged; c += K, ds++ ) {
+          fd_amd_tile_desc_t * dd = t->desc + (ds & mask);
+          dd->first = c;
+          dd->count = (uint32_t)std::min( K, staged - c ) | (lat_mode ? FD_AMD_TILE_LAT : 0u);
+        }
+        t->desc_seq = ds;
+        __atomic_store_n( &H->head, ds, __ATOMIC_RELEASE );
+        diag->batch_cnt++; diag->batch_sig_cnt += staged - handed;
+        handed = staged; progress = true;
+      }
+    }
+
+    /* 4. an idle tile checks now and then that the kernel is still there */
+    if( progress ) idle = 0UL;
+    else if( ++idle >= 4096UL ) {
+      idle = 0UL;
+      hipError_t q = hipEventQuery( t->pdone );
+      if( q != hipErrorNotReady ) {
+        fprintf( stderr, "fd_verify_amd_tile_run: the tile kernel exited early (%s, watchdog %u)\n",
+                 hipGetErrorString( q ), __atomic_load_n( &H->kerr, __ATOMIC_ACQUIRE ) );
+        rc = FD_ED25519_AMD_ERR_DEVICE;
+        break;
+      }
+    }
+  }
+
+  /* stop: the waves exit once nothing is left to claim */
+  __atomic_store_n( &H->stop, 1u, __ATOMIC_RELEASE );
+  if( hipEventSynchronize( t->pdone ) != hipSuccess ) rc = FD_ED25519_AMD_ERR_DEVICE;
+  if( src_dev ) (void)hipFree( src_dev );
+  ulong st[4] = { 0, 0, 0, 0 };
+  if( hipMemcpy( st, t->dctl->stat, sizeof st, hipMemcpyDeviceToHost ) != hipSuccess ) rc = FD_ED25519_AMD_ERR_DEVICE;
+  if( __atomic_load_n( &H->kerr, __ATOMIC_ACQUIRE ) ) rc = FD_ED25519_AMD_ERR_DEVICE;
+  if( env_ulong( "FD_AMD_TILE_DEBUG", 0UL ) ) {   /* per-phase wave time (k_tile_persist, args.prof) */
+    ulong pf[8];
+    if( hipMemcpy( pf, t->dctl->prof, sizeof pf, hipMemcpyDeviceToHost ) == hipSuccess ) {
+      double w = (double)(t->waves - 1U) * 1e5;   /* ticks are 10 ns: per-wave ms */
+      fprintf( stderr, "tile debug: per-wave ms  gather %.2f front %.2f dsm %.2f results %.2f wait %.2f fence %.2f"
+               "  (chunks %lu latency + %lu throughput)\n", pf[0]/w, pf[1]/w, pf[2]/w, pf[3]/w, pf[4]/w, pf[5]/w,
+               st[0], st[1] );
+    }
+  }
+  diag->gpu_chunk_lat_cnt += st[0]; diag->gpu_chunk_thr_cnt += st[1];
+  diag->gpu_frag_lat_cnt  += st[2]; diag->gpu_frag_thr_cnt  += st[3];
+  t->ring_seq = staged;
+  __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
+  if( in_fseq ) __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE );
+  t->out_seq_end = out_seq;
+  return rc;
 }
 
 /* ------------------------------------------------------------------ */
@@ -655,5 +1030,7 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   out[4] = diag.batch_cnt ? (double)diag.batch_sig_cnt / (double)diag.batch_cnt : 0.0;
   out[5] = (double)diag.out_cnt; out[6] = (double)diag.sv_filt_cnt; out[7] = (double)diag.ovrn_cnt;
   out[8] = (double)mism; out[9] = (double)checked;
+  out[10] = (double)diag.gpu_chunk_lat_cnt; out[11] = (double)diag.gpu_chunk_thr_cnt;
+  out[12] = (double)diag.gpu_frag_lat_cnt;  out[13] = (double)diag.gpu_frag_thr_cnt;
   return FD_ED25519_AMD_OK;
 }

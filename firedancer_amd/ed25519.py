@@ -82,6 +82,8 @@ def lib():
     L.fd_ed25519_amd_set_latency_batch_max.restype = None
     L.fd_ed25519_amd_set_pool_batch_min.argtypes = [ul]
     L.fd_ed25519_amd_set_pool_batch_min.restype = None
+    L.fd_ed25519_amd_debug_set_pool_iter_cap.argtypes = [ul]
+    L.fd_ed25519_amd_debug_set_pool_iter_cap.restype = None
     L.fd_verify_amd_tile_new.argtypes = [i, ul, ul, ul, ul]
     L.fd_verify_amd_tile_new.restype = vp
     L.fd_verify_amd_tile_out_chunk0.argtypes = [vp]
@@ -455,6 +457,21 @@ def set_latency_batch_max(n):
 def set_pool_batch_min(n):
     """Throughput batches of at least n signatures use the pooled kernel (k_dsmp)."""
     lib().fd_ed25519_amd_set_pool_batch_min(int(n))
+
+
+VERDICT_DEVICE = -128   # FD_ED25519_AMD_VERDICT_DEVICE: k_dsmp's step guard tripped
+
+
+def device_numa_node(device):
+    """fd_ed25519_amd_device_numa_node: the NUMA node of HIP device `device` (-1 unknown)."""
+    f = lib().fd_ed25519_amd_device_numa_node
+    f.restype = ctypes.c_int
+    return int(f(int(device)))
+
+
+def debug_set_pool_iter_cap(cap):
+    """Debug: cap k_dsmp's step guard at `cap` steps per wave (0 restores it)."""
+    lib().fd_ed25519_amd_debug_set_pool_iter_cap(int(cap))
 
 
 def select_dsm_kernel(name):

@@ -13,6 +13,8 @@ Two ways to run N GPUs:
     (fd_ed25519_amd_multi_*, ed25519.MultiEngine), one engine and one
     persistent host thread per device.
 """
+import os
+
 import numpy as np
 
 
@@ -48,3 +50,36 @@ def _slice_soa(pub, sig, off, sz, blob, lo, hi):
     start, end = int(o.min()), int((o + s).max())
     return (pub[lo:hi], sig[lo:hi], (o - start).astype(np.uint32), sz[lo:hi],
             np.ascontiguousarray(blob[start:max(end, start + 1)]))
+
+
+def parse_cpulist(text):
+    """sysfs cpulist ("0-3,8,10-11") -> sorted list of CPU ids."""
+    cpus = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        cpus.extend(range(int(a), int(b or a) + 1))
+    return cpus
+
+
+def bind_to_device_node(device, sysfs="/sys"):
+    """Pin this process to the CPUs of `device`'s NUMA node that it may use
+    (the reference pins each tile to a core next to its link,
+    src/app/frank/fd_frank_main.c:118-143).  Returns {"numa_node", "cpus"}
+    (cpus: how many the process is now bound to, 0 = left unchanged).
+    FD_ED25519_AMD_NUMA=0 leaves the affinity alone."""
+    from . import ed25519
+    node = int(ed25519.device_numa_node(device))
+    out = {"numa_node": node, "cpus": 0}
+    if node < 0 or os.environ.get("FD_ED25519_AMD_NUMA") == "0":
+        return out
+    try:
+        cpus = parse_cpulist(open(os.path.join(sysfs, "devices/system/node/node%d/cpulist" % node)).read())
+    except (OSError, ValueError):
+        return out
+    want = sorted(set(cpus) & os.sched_getaffinity(0))
+    if want:
+        os.sched_setaffinity(0, want)
+        out["cpus"] = len(want)
+    return out

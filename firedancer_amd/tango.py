@@ -16,7 +16,8 @@ assert FRAG_META.itemsize == 32
 CHUNK_LG_SZ = 6
 CHUNK_SZ = 64
 DIAG_FIELDS = ("in_cnt", "ha_filt_cnt", "ha_filt_sz", "sv_filt_cnt", "sv_filt_sz", "out_cnt", "out_sz",
-               "ovrn_cnt", "backp_cnt", "batch_cnt", "batch_sig_cnt", "bad_frag_cnt")
+               "ovrn_cnt", "backp_cnt", "batch_cnt", "batch_sig_cnt", "bad_frag_cnt", "gpu_chunk_lat_cnt",
+               "gpu_chunk_thr_cnt", "gpu_frag_lat_cnt", "gpu_frag_thr_cnt")
 
 
 def _aligned(nbytes, align=64):
@@ -125,7 +126,7 @@ def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, bl
     """fd_verify_amd_bench_stream: producer (rate frags/s, 0 = saturate) -> tile -> consumer; returns
     dict(frags_per_s, p50_ns, p99_ns, p999_ns, mean_batch, published, sv_filt, ovrn, mismatches, checked).
     With expect_err/expect_tag (per pool entry) the consumer checks every published frag."""
-    out = (ctypes.c_double * 10)()
+    out = (ctypes.c_double * 14)()
     p = [np.ascontiguousarray(a) for a in (pub, sig, msg_off, msg_sz, blob)]
     ee = np.ascontiguousarray(expect_err, np.int8) if expect_err is not None else None
     et = np.ascontiguousarray(expect_tag, np.uint64) if expect_tag is not None else None
@@ -141,5 +142,5 @@ def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, bl
     if rc:
         raise ed25519.EngineError("fd_verify_amd_bench_stream rc=%d" % rc)
     keys = ("frags_per_s", "p50_ns", "p99_ns", "p999_ns", "mean_batch", "published", "sv_filt", "ovrn", "mismatches",
-            "checked")
+            "checked", "gpu_chunks_lat", "gpu_chunks_thr", "gpu_frags_lat", "gpu_frags_thr")
     return dict(zip(keys, list(out)))

@@ -202,6 +202,22 @@ fd_ed25519_amd_multi_ndev( fd_ed25519_amd_multi_t const * multi );
 void
 fd_ed25519_amd_shard_range( ulong n, ulong ndev, ulong r, ulong * lo, ulong * hi );
 
+/* NUMA placement.  Each multi-engine thread binds itself to its device's
+   NUMA node (the node's CPUs it may use, and the node as its preferred
+   memory) before creating its engine, so the pinned staging it fills is
+   node-local; a single engine prefers the device's node while it allocates
+   its staging and leaves the caller's thread as it was.
+   FD_ED25519_AMD_NUMA=0 turns both off.  The node of a device:
+   hipDeviceGetPCIBusId -> /sys/bus/pci/devices/<bdf>/numa_node (-1 when
+   unknown).  fd_ed25519_amd_sysfs_numa reads that file and the node's
+   cpulist under any sysfs root: node (-1 if unknown) and up to cpus_max
+   CPUs; returns the CPU count, -1 on an unreadable or malformed tree. */
+int
+fd_ed25519_amd_device_numa_node( int device );
+
+int
+fd_ed25519_amd_sysfs_numa( char const * sysfs_root, char const * pci_bdf, int * node, int * cpus, int cpus_max );
+
 /* fd_ed25519_amd_verify_soa over the engines (same arguments and
    verdicts; err[i] for every i).  Returns the first engine error, if any. */
 int
@@ -311,6 +327,17 @@ fd_ed25519_amd_set_latency_batch_max( ulong n );
 
 void
 fd_ed25519_amd_set_pool_batch_min( ulong n );
+
+/* k_dsmp bounds its step loop (a hang guard: every step advances at least
+   one op of a signature's bounded op stream).  If a launch ever reaches the
+   bound, every verdict of that launch is set to FD_ED25519_AMD_VERDICT_DEVICE
+   (never a reference code) and the host batch calls return
+   FD_ED25519_AMD_ERR_DEVICE instead of verdicts; device-resident callers
+   (fd_ed25519_amd_verify_dev) see the marker in d_err.  Debug: cap the
+   bound at `cap` steps per wave (0 restores it), to exercise that path. */
+#define FD_ED25519_AMD_VERDICT_DEVICE (-128)
+void
+fd_ed25519_amd_debug_set_pool_iter_cap( ulong cap );
 
 /* Library version / build string. */
 char const *

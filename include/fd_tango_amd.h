@@ -97,9 +97,13 @@ typedef struct {
   ulong out_sz;
   ulong ovrn_cnt;      /* input frags lost to producer overrun (skipped, or lapped before the tile was done) */
   ulong backp_cnt;     /* times the output was backpressured */
-  ulong batch_cnt;     /* GPU batches launched */
-  ulong batch_sig_cnt; /* signatures in those batches */
-  ulong bad_frag_cnt;  /* frags too short / too long to carry a signature */
+  ulong batch_cnt;     /* GPU batches launched (persistent path: hand-offs to the GPU) */
+  ulong batch_sig_cnt; /* signatures in those batches (persistent path: frags handed over) */
+  ulong bad_frag_cnt;  /* frags too short / too long to carry a signature, or (zero copy) reaching past the mapped region */
+  ulong gpu_chunk_lat_cnt;   /* persistent path: chunks the GPU verified 8 lanes per signature (latency mode) */
+  ulong gpu_chunk_thr_cnt;   /* ... 1 lane per signature (throughput mode) */
+  ulong gpu_frag_lat_cnt;    /* frags in those chunks */
+  ulong gpu_frag_thr_cnt;
 } fd_verify_amd_diag_t;
 
 typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
@@ -248,8 +252,10 @@ fd_verify_amd_tickcount( void );
    out[5] = frags published, out[6] = frags dropped by verification
    (SV_FILT), out[7] = overrun frags, out[8] = check mismatches (published
    frags that fail a check, plus frags that should have been published and
-   were not, overrun ones excepted), out[9] = frags checked.  Returns 0 or
-   an error code. */
+   were not, overrun ones excepted), out[9] = frags checked, out[10..13] =
+   the persistent path's GPU chunks in latency / throughput mode and the
+   frags in each (0 on the batch path).  out holds 14 doubles.  Returns 0
+   or an error code. */
 #define FD_VERIFY_AMD_BENCH_ZERO_COPY (1)
 #define FD_VERIFY_AMD_BENCH_WRITE     (2)
 #define FD_VERIFY_AMD_BENCH_LAP       (4)

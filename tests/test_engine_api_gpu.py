@@ -115,3 +115,62 @@ def test_registered_batches_equal_staged(engine, golden):
         r.close()
     with pytest.raises(ed25519.EngineError):
         engine.verify_soa_registered(golden.pub, golden.sig, golden.msg_off, golden.msg_sz, golden.blob)
+
+
+def test_pooled_step_guard_is_reported_as_a_device_error(golden):
+    """k_dsmp's hang guard (a bound on its step loop): capped through the
+    debug entry point so that it trips, the batch call fails with
+    FD_ED25519_AMD_ERR_DEVICE instead of returning verdicts computed from
+    unfinished signatures, the device API sees FD_ED25519_AMD_VERDICT_DEVICE
+    in every verdict, and with the cap lifted the same engine is exact."""
+    from firedancer_amd import ed25519, hip
+    eng = ed25519.Engine(device=0, batch_max=4096, blob_max=4096 * 1232)
+    try:
+        ed25519.select_dsm_kernel("k_dsmp")
+        ed25519.debug_set_pool_iter_cap(10)
+        with pytest.raises(ed25519.EngineError):
+            eng.verify_soa(golden.pub, golden.sig, golden.msg_off, golden.msg_sz, golden.blob)
+        n = len(golden)
+        bufs = [hip.DeviceBuffer.from_array(a) for a in (golden.pub, golden.sig, golden.msg_off, golden.msg_sz,
+                                                          golden.blob)]
+        d_err, d_ws = hip.DeviceBuffer(n), hip.DeviceBuffer(ed25519.workspace_footprint(n))
+        st = hip.Stream()
+        ed25519.verify_dev(n, *[b.ptr for b in bufs], d_err.ptr, d_ws.ptr, st.handle)
+        st.synchronize()
+        assert (d_err.to_array(np.int8, n) == ed25519.VERDICT_DEVICE).all()
+        ed25519.debug_set_pool_iter_cap(0)
+        err = eng.verify_soa(golden.pub, golden.sig, golden.msg_off, golden.msg_sz, golden.blob)
+        assert np.array_equal(err, golden.expect)
+    finally:
+        ed25519.debug_set_pool_iter_cap(0)
+        ed25519.select_dsm_kernel("default")
+        eng.close()
+
+
+def test_registered_plane_must_be_registered_to_its_end(golden):
+    """A plane whose first page is registered but whose tail is not is
+    refused (ERR_INVAL) before anything launches, instead of being read in
+    place past the registered range by the latency path; the engine's next
+    call is exact."""
+    from firedancer_amd import ed25519
+    n = 512
+    raw = np.zeros(32 * n + 8192, np.uint8)
+    o = (-raw.ctypes.data) % 4096
+    pub = raw[o:o + 32 * n]                           # page-aligned, 4 pages
+    pub[:] = golden.pub[:n].reshape(-1)
+    ed25519.host_register(pub[:4096])                 # only its first page
+    r = _Registered(golden.sig[:n], golden.msg_off[:n], golden.msg_sz[:n], golden.blob)
+    eng = ed25519.Engine(device=0, batch_max=n, blob_max=n * 1232)
+    try:
+        with pytest.raises(ed25519.EngineError):
+            eng.verify_soa_registered(pub.reshape(n, 32), r[0], r[1], r[2], r[3])
+        p2 = _Registered(golden.pub[:n])
+        try:
+            err = eng.verify_soa_registered(p2[0], r[0], r[1], r[2], r[3])
+            assert np.array_equal(err, golden.expect[:n])
+        finally:
+            p2.close()
+    finally:
+        eng.close()
+        r.close()
+        ed25519.host_unregister(pub[:4096])
