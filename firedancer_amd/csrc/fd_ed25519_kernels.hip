@@ -1482,6 +1482,23 @@ pool_store_ts( PTR s, u32 stride, p1p1 const & t ) {
 #endif
 
 
+/* Rank -> processing lane.  A step's state loads are ds_read_b128 at the
+   selected slots, whose bank quad is the slot mod 16, served in four
+   16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32);
+   its stores ds_write_b128 in 8-lane groups by slot mod 8.  Consecutive
+   ranks are ~1.75 slots apart (64 of 112 selected), so rank = lane put many
+   slots of one residue into a group.  Rank r on lane 16 (r & 3) + (r >> 2)
+   spaces a group's ranks ~4 apart (~7 slots, odd: distinct residues). */
+#ifndef FD_POOL_PERM
+#define FD_POOL_PERM 0
+#endif
+__device__ __forceinline__ u32 pool_lane( u32 r ) {
+  return FD_POOL_PERM ? (((r & 3u) << 4) | ((r >> 2) & 15u)) : (r & 63u);
+}
+__device__ __forceinline__ u32 pool_rank( u32 l ) {   /* inverse of pool_lane on 0..63 */
+  return FD_POOL_PERM ? (((l & 15u) << 2) | (l >> 4)) : l;
+}
+
 __device__ __forceinline__ u32 lane_rank( u64 m ) {   /* set bits of m below this lane */
   return __builtin_amdgcn_mbcnt_hi( (u32)(m >> 32), __builtin_amdgcn_mbcnt_lo( (u32)m, 0u ) );
 }
@@ -1508,6 +1525,7 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
   u64 const valid1 = (P >= 128u) ? ~0UL : ((1UL << (P - 64u)) - 1UL);   /* slots 64.. that exist */
 
   u64 mD0 = 0, mD1 = 0, mA0 = 0, mA1 = 0;
+  u32 const lrank = pool_rank( l );   /* the selection rank this lane processes */
 #ifdef FD_POOL_DEBUG
   u64 dbg_t0 = wall_clock64(), dbg_te = 0; bool dbg_after = false; u64 dbg_sa = 0, dbg_la = 0;
 #endif
@@ -1626,11 +1644,12 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
     dbg_steps++; dbg_lanes += nsel; dbg_add += mixed;
     if( dbg_after ) { dbg_sa++; dbg_la += nsel; }
 #endif
-    bool live = l < nsel;
-    /* slot of rank l: each selected slot's owner writes it at its rank (the
-       wave's LDS accesses complete in order: no barrier for a one-wave group) */
-    if( in0 ) s_list[rk0] = l;
-    if( in1 ) s_list[rk1] = l + 64u;
+    bool live = lrank < nsel;
+    /* slot of each rank, at the lane that processes it: each selected
+       slot's owner writes it (the wave's LDS accesses complete in order: no
+       barrier for a one-wave group) */
+    if( in0 ) s_list[pool_lane( rk0 )] = l;
+    if( in1 ) s_list[pool_lane( rk1 )] = l + 64u;
     __builtin_amdgcn_wave_barrier();
     u32 s = live ? s_list[l] : 0u;
     uint4 m = s_m[s];
@@ -1748,8 +1767,8 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
       }
     }
     /* the slots' new classes, at their owner lanes */
-    u32 v0 = (u32)__builtin_amdgcn_ds_bpermute( (int)(rk0 << 2), (int)nop );
-    u32 v1 = (u32)__builtin_amdgcn_ds_bpermute( (int)((rk1 & 63u) << 2), (int)nop );
+    u32 v0 = (u32)__builtin_amdgcn_ds_bpermute( (int)(pool_lane( rk0 ) << 2), (int)nop );
+    u32 v1 = (u32)__builtin_amdgcn_ds_bpermute( (int)(pool_lane( rk1 ) << 2), (int)nop );
     u64 const d0 = __builtin_amdgcn_ballot_w64( v0 == OP_D ), d1 = __builtin_amdgcn_ballot_w64( v1 == OP_D );
     u64 const x0 = __builtin_amdgcn_ballot_w64( v0 < OP_EMPTY ), x1 = __builtin_amdgcn_ballot_w64( v1 < OP_EMPTY );
     mD0 |= S0 & d0; mA0 |= S0 & x0 & ~d0;                       /* OP_AA / OP_AB: below OP_EMPTY, not OP_D */
