@@ -107,12 +107,15 @@ typedef struct {
   uint8_t *                  scratch;  /* per-wave scratch, fd_amd_tile_scratch_stride() bytes apart */
   uint64_t                   watchdog; /* s_memrealtime ticks (100 MHz) without a host heartbeat before the kernel gives up */
   uint32_t                   prof;     /* debug: sum per-phase time stamps into dctl->prof */
-  uint32_t                   dbg;      /* A/B only: 8 read frags from src_dev, 16 no output-frame writes */
+  uint32_t                   dbg;      /* A/B only: 8 read frags from src_dev, 16 no output-frame writes, 32 agent-scope acquire, 64 no acquire, 128 no release fence */
   uint8_t const *            src_dev;  /* A/B only: a device copy of the source region */
 } fd_amd_tile_args_t;
 size_t fd_amd_tile_scratch_stride( void );
 /* waves: grid size (wave 0 is the scout that mirrors the host words) */
 int fd_amd_launch_tile_persist( fd_amd_tile_args_t const * a, uint32_t waves, hipStream_t stream );
+
+/* measurement aid: the chunk pipeline alone, every argument in device memory */
+int fd_amd_launch_tile_synth( fd_amd_tile_args_t const * a, uint32_t waves, uint32_t iters, int eight, hipStream_t stream );
 
 /* Dense slide digits of the last call on workspace d_ws (debug): u16
    [n][256] (low byte h digit, high byte s digit) rebuilt from the event

@@ -1482,23 +1482,6 @@ pool_store_ts( PTR s, u32 stride, p1p1 const & t ) {
 #endif
 
 
-/* Rank -> processing lane.  A step's state loads are ds_read_b128 at the
-   selected slots, whose bank quad is the slot mod 16, served in four
-   16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32);
-   its stores ds_write_b128 in 8-lane groups by slot mod 8.  Consecutive
-   ranks are ~1.75 slots apart (64 of 112 selected), so rank = lane put many
-   slots of one residue into a group.  Rank r on lane 16 (r & 3) + (r >> 2)
-   spaces a group's ranks ~4 apart (~7 slots, odd: distinct residues). */
-#ifndef FD_POOL_PERM
-#define FD_POOL_PERM 0
-#endif
-__device__ __forceinline__ u32 pool_lane( u32 r ) {
-  return FD_POOL_PERM ? (((r & 3u) << 4) | ((r >> 2) & 15u)) : (r & 63u);
-}
-__device__ __forceinline__ u32 pool_rank( u32 l ) {   /* inverse of pool_lane on 0..63 */
-  return FD_POOL_PERM ? (((l & 15u) << 2) | (l >> 4)) : l;
-}
-
 __device__ __forceinline__ u32 lane_rank( u64 m ) {   /* set bits of m below this lane */
   return __builtin_amdgcn_mbcnt_hi( (u32)(m >> 32), __builtin_amdgcn_mbcnt_lo( (u32)m, 0u ) );
 }
@@ -1525,7 +1508,6 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
   u64 const valid1 = (P >= 128u) ? ~0UL : ((1UL << (P - 64u)) - 1UL);   /* slots 64.. that exist */
 
   u64 mD0 = 0, mD1 = 0, mA0 = 0, mA1 = 0;
-  u32 const lrank = pool_rank( l );   /* the selection rank this lane processes */
 #ifdef FD_POOL_DEBUG
   u64 dbg_t0 = wall_clock64(), dbg_te = 0; bool dbg_after = false; u64 dbg_sa = 0, dbg_la = 0;
 #endif
@@ -1644,12 +1626,11 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
     dbg_steps++; dbg_lanes += nsel; dbg_add += mixed;
     if( dbg_after ) { dbg_sa++; dbg_la += nsel; }
 #endif
-    bool live = lrank < nsel;
-    /* slot of each rank, at the lane that processes it: each selected
-       slot's owner writes it (the wave's LDS accesses complete in order: no
-       barrier for a one-wave group) */
-    if( in0 ) s_list[pool_lane( rk0 )] = l;
-    if( in1 ) s_list[pool_lane( rk1 )] = l + 64u;
+    bool live = l < nsel;
+    /* slot of rank l: each selected slot's owner writes it at its rank (the
+       wave's LDS accesses complete in order: no barrier for a one-wave group) */
+    if( in0 ) s_list[rk0] = l;
+    if( in1 ) s_list[rk1] = l + 64u;
     __builtin_amdgcn_wave_barrier();
     u32 s = live ? s_list[l] : 0u;
     uint4 m = s_m[s];
@@ -1767,8 +1748,8 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
       }
     }
     /* the slots' new classes, at their owner lanes */
-    u32 v0 = (u32)__builtin_amdgcn_ds_bpermute( (int)(pool_lane( rk0 ) << 2), (int)nop );
-    u32 v1 = (u32)__builtin_amdgcn_ds_bpermute( (int)(pool_lane( rk1 ) << 2), (int)nop );
+    u32 v0 = (u32)__builtin_amdgcn_ds_bpermute( (int)(rk0 << 2), (int)nop );
+    u32 v1 = (u32)__builtin_amdgcn_ds_bpermute( (int)((rk1 & 63u) << 2), (int)nop );
     u64 const d0 = __builtin_amdgcn_ballot_w64( v0 == OP_D ), d1 = __builtin_amdgcn_ballot_w64( v1 == OP_D );
     u64 const x0 = __builtin_amdgcn_ballot_w64( v0 < OP_EMPTY ), x1 = __builtin_amdgcn_ballot_w64( v1 < OP_EMPTY );
     mD0 |= S0 & d0; mA0 |= S0 & x0 & ~d0;                       /* OP_AA / OP_AB: below OP_EMPTY, not OP_D */
@@ -1950,7 +1931,8 @@ size_t fd_amd_tile_scratch_stride( void ) { return tile_scratch_layout().total; 
 
 /* The scout (wave 0, lane 0): host words -> the XCDs' mirror words. */
 __device__ __noinline__ void
-tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog ) {
+tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog, u32 dbg ) {
+  u64 tmw = 0UL;
   u64 word = ld_dev64( &D->mw[0].w ), lastb = ~0UL, beat = 0UL;
   u64 tb = __builtin_amdgcn_s_memrealtime(), tpub = tb;
   for( ;; ) {
@@ -1964,8 +1946,8 @@ tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog ) {
        waiting waves' own watchdog quiet) */
     if( now - tpub > 1000UL && now - tb < 1000UL ) { beat++; tpub = now; }
     u64 w = (h & ((1UL << 48) - 1UL)) | ((beat & 0x3fffUL) << 48) | (dead ? TILE_MW_ERR : 0UL) | (st ? TILE_MW_STOP : 0UL);
-    if( w != word ) {
-      word = w;
+    if( w != word && ( !(dbg & 512u) || now - tmw > 2000UL || (w & (TILE_MW_ERR | TILE_MW_STOP)) ) ) {
+      word = w; tmw = now;
       _Pragma("unroll") for( int x=0; x<FD_AMD_TILE_MIRRORS; x++ ) st_dev64( &D->mw[x].w, w );
     }
     if( st || dead ) break;
@@ -2048,7 +2030,7 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __rest
   u64 idx = c0 + l;
   fd_amd_tile_res_t * r = A.res + (idx & A.mask);
   if( l < k ) st_sys64( &r->tag, ((u64 const *)(ws + L.tag))[l] );
-  __builtin_amdgcn_fence( __ATOMIC_RELEASE, "" );
+  if( !(A.dbg & 128u) ) __builtin_amdgcn_fence( __ATOMIC_RELEASE, "" );
   asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
   if( l < k ) st_sys64( &r->word, ((idx + 1UL) << 8) | (u64)(u8)err[l] );
   TILE_STAMP( 3 );
@@ -2064,7 +2046,7 @@ k_tile_persist( fd_amd_tile_args_t A ) {
   fd_amd_tile_dctl_t * D = A.dctl;
   u32 const l = threadIdx.x;
   if( blockIdx.x == 0u ) {
-    if( l == 0u ) tile_scout( D, A.hctl, A.watchdog );
+    if( l == 0u ) tile_scout( D, A.hctl, A.watchdog, A.dbg );
     return;
   }
   bi12_fill( bi );
@@ -2091,7 +2073,7 @@ k_tile_persist( fd_amd_tile_args_t A ) {
       if( w != last ) { last = w; tw = now; }
       else if( now - tw > A.watchdog ) break;       /* no scout (or host) for that long: give up */
       u64 const d = t - TILE_MW_HEAD( w );
-      u32 const nap = d < 2UL ? 1u : d < 64UL ? (u32)d : 64u;
+      u32 const nap = (A.dbg & 256u) ? 64u : d < 2UL ? 1u : d < 64UL ? (u32)d : 64u;
       for( u32 z = 0; z < nap; z++ ) __builtin_amdgcn_s_sleep( 4 );
     }
     if( A.prof ) pt[4] += __builtin_amdgcn_s_memrealtime() - t0;
@@ -2108,7 +2090,9 @@ k_tile_persist( fd_amd_tile_args_t A ) {
     /* the frames were written by the host (copy mode) or the producer
        (zero-copy) into host memory: drop this CU's stale lines first */
     u64 const tf = A.prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
-    __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "" );
+    if( A.dbg & 64u )      { /* A/B: no acquire */ }
+    else if( A.dbg & 32u ) __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "agent" );
+    else                   __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "" );
     asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
     if( A.prof ) pt[5] += __builtin_amdgcn_s_memrealtime() - tf;
     if( take && take <= 64u ) tile_chunk( A, c, take, e8, scr, L, S, bi, evl, pt );
@@ -2121,6 +2105,48 @@ k_tile_persist( fd_amd_tile_args_t A ) {
     atomicAdd( (unsigned long long *)&D->stat[3], (unsigned long long)f64 );
     if( A.prof ) { _Pragma("unroll") for( int q=0; q<8; q++ ) atomicAdd( (unsigned long long *)&D->prof[q], (unsigned long long)pt[q] ); }
   }
+}
+
+/* Measurement aid: k_tile_persist's chunk pipeline without the host
+   hand-off (no tickets, no polling, nothing in mapped memory): wave w runs
+   `iters` chunks of k ring entries, [(w iters + it) k, +k), with every
+   argument in device memory (fd_amd_tile_synth, tools/tile_synth.py). */
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_tile_synth( fd_amd_tile_args_t A, u32 iters, u32 eight ) {
+  constexpr ws_layout_t    L = ws_layout_const( 64 );
+  constexpr tile_scratch_t S = tile_scratch_layout();
+  __shared__ __attribute__((aligned(16))) i32 bi[8][48];
+  __shared__ u64 evl[64][33];
+  bi12_fill( bi );
+  __syncthreads();
+  u64 pt[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
+  u32 const k = eight ? 8u : 64u;
+  if( A.hctl && blockIdx.x == gridDim.x - 1u ) {
+    /* A/B: a scout-like wave polling the host control words until the
+       others are done (bounded by the watchdog) */
+    if( threadIdx.x == 0u ) {
+      u64 const t0 = __builtin_amdgcn_s_memrealtime();
+      u64 acc = 0;
+      while( __hip_atomic_load( (u64 *)&A.dctl->stat[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ) < (u64)(gridDim.x - 1u) &&
+             __builtin_amdgcn_s_memrealtime() - t0 < A.watchdog ) {
+        acc += ld_sys64( &A.hctl->head ) + ld_sys64( &A.hctl->beat ) + ld_sys32( &A.hctl->stop );
+        __builtin_amdgcn_s_sleep( 2 );
+      }
+      A.dctl->stat[1] = acc;
+    }
+    return;
+  }
+  u8 * scr = A.scratch + (size_t)blockIdx.x * S.total;
+  for( u32 it = 0; it < iters; it++ )
+    tile_chunk( A, ((u64)blockIdx.x * iters + it) * k, k, eight != 0u, scr, L, S, bi, evl, pt );
+  if( A.hctl && threadIdx.x == 0u ) atomicAdd( (unsigned long long *)&A.dctl->stat[0], 1ULL );
+}
+
+int
+fd_amd_launch_tile_synth( fd_amd_tile_args_t const * a, uint32_t waves, uint32_t iters, int eight, hipStream_t stream ) {
+  if( !waves || !iters ) return -1;
+  hipLaunchKernelGGL( k_tile_synth, dim3(waves), dim3(64), 0, stream, *a, iters, (u32)(eight != 0) );
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int

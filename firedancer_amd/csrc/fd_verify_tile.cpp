@@ -345,7 +345,8 @@ fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong 
          hipMalloc( (void **)&s.d_mir, batch_max * FD_VERIFY_AMD_FRAME_SZ + 64UL ) == hipSuccess;
     s.pend.resize( batch_max ); s.ich.resize( batch_max ); s.fsz.resize( batch_max ); s.tb.resize( batch_max + 1UL );
   }
-  ok = ok && hipHostMalloc( (void **)&t->out_base, out_frame_cnt * FD_VERIFY_AMD_FRAME_SZ, hipHostMallocMapped ) == hipSuccess &&
+  unsigned const of = hipHostMallocMapped | ( env_ulong( "FD_AMD_TILE_OUT_COHERENT", 0UL ) ? hipHostMallocCoherent : 0u );
+  ok = ok && hipHostMalloc( (void **)&t->out_base, out_frame_cnt * FD_VERIFY_AMD_FRAME_SZ, of ) == hipSuccess &&
        hipHostGetDevicePointer( (void **)&t->out_dev, t->out_base, 0 ) == hipSuccess;
   t->frame_cnt = out_frame_cnt;
   t->frame_pub.assign( out_frame_cnt, FRAME_FREE );
@@ -499,6 +500,11 @@ tile_run_batched( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
      in housekeeping, fd_fctl): diag->in_cnt and in_fseq are published per
      staging pass; out_fseq is re-read only when a cached value runs out. */
   ulong in_cnt = diag->in_cnt, out_cr = 0, cons = out_seq0, fseq_pub = ~0UL;
+  /* debug (FD_AMD_TILE_DEBUG): host TSC ticks in retire+publish, staging,
+     launch, and spinning with every slot in flight */
+  bool const hdbg = env_ulong( "FD_AMD_TILE_DEBUG", 0UL ) != 0UL;
+  ulong hpt[4] = { 0, 0, 0, 0 }, hspin = 0, ht = hdbg ? __rdtsc() : 0UL, ht0 = ht, hns0 = hdbg ? now_ns() : 0UL, hin0 = in_cnt;
+# define HSTAMP( k_ ) do { if( hdbg ) { ulong t_ = __rdtsc(); hpt[k_] += t_ - ht; ht = t_; } } while(0)
 
   auto publish = [&]( int k ) -> int {
     slot_t *      s  = &e->slot[k];
@@ -545,6 +551,7 @@ tile_run_batched( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       if( (rc = publish( oldest )) ) return tile_quiesce( t, rc );
       oldest = (oldest + 1) % K; nfly--;
     }
+    HSTAMP( 0 );
     /* producer credit: copy mode is done with a frag once it is copied;
        zero copy only once the batch holding it has retired */
     if( in_fseq ) {
@@ -553,7 +560,7 @@ tile_run_batched( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     }
     bool done_in = frag_cnt ? (in_seq - in_seq0 >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
     if( done_in && !staged && !nfly ) break;
-    if( nfly == K ) continue;      /* every slot in flight: the staging slot is busy */
+    if( nfly == K ) { hspin++; HSTAMP( 3 ); continue; }   /* every slot in flight: the staging slot is busy */
 
     /* 2. stage input frags into the free slot */
     tile_slot_t & ts = t->ts[stage];
@@ -614,6 +621,7 @@ tile_run_batched( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
     if( in_fseq && !zc_dev && in_seq != fseq_pub ) { __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE ); fseq_pub = in_seq; }
     done_in = frag_cnt ? (in_seq - in_seq0 >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
+    HSTAMP( 1 );
 
     /* 3. adaptive launch (a free slot exists here): full batch, input
           momentarily drained (greedy: under light load batches stay small
@@ -635,6 +643,14 @@ tile_run_batched( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       nfly++;
       stage = (stage + 1) % K; staged = 0; slots = 0;
     }
+    HSTAMP( 2 );
+  }
+# undef HSTAMP
+  if( hdbg ) {
+    double const tot = (double)(__rdtsc() - ht0);
+    fprintf( stderr, "tile debug (batch path, host): publish %.1f%% stage %.1f%% launch %.1f%% all-slots-busy %.1f%% (%lu spins), "
+             "%.1f ns/frag\n", 100.0*(double)hpt[0]/tot, 100.0*(double)hpt[1]/tot, 100.0*(double)hpt[2]/tot,
+             100.0*(double)hpt[3]/tot, hspin, (double)(now_ns() - hns0) / (double)(in_cnt - hin0 + 1UL) );
   }
   __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
   if( in_fseq ) __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE );
@@ -877,6 +893,81 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
   if( in_fseq ) __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE );
   t->out_seq_end = out_seq;
+  return rc;
+}
+
+/* ------------------------------------------------------------------ */
+/* Measurement aid (tools/tile_synth.py): k_tile_persist's chunk pipeline
+   on frags already in device memory, without the host hand-off.  frames:
+   nframes frames of FD_VERIFY_AMD_FRAME_SZ bytes (pub | sig | msg), fsz
+   their sizes; ring entry j takes frame j % nframes.  out_ms: the launch's
+   time; verdict: per entry the verdict, or 99 if its result word is
+   missing. */
+/* where (flags): 1 ring entries, 2 results, 4 frames in mapped coherent
+   host memory, 8 frames in mapped non-coherent host memory, 16 one more
+   wave polling mapped host control words meanwhile (the scout's load) */
+extern "C" int
+fd_amd_tile_synth( int device, uint32_t waves, uint32_t iters, int eight, uint32_t dbg, uint32_t where,
+                   uint8_t const * frames, uint32_t nframes, uint32_t const * fsz, double * out_ms, int8_t * verdict ) {
+  if( !frames || !nframes || !fsz || !out_ms || !verdict || !waves || !iters || waves > 65536u || iters > 4096u ) return FD_ED25519_AMD_ERR_INVAL;
+  for( uint32_t f=0; f<nframes; f++ ) if( fsz[f] < 96u || fsz[f] > 96u + FD_ED25519_AMD_MSG_MAX ) return FD_ED25519_AMD_ERR_INVAL;
+  if( hipSetDevice( device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  ulong const k = eight ? 8UL : 64UL, n = (ulong)waves * iters * k;
+  ulong R = 1UL; while( R < n ) R <<= 1;
+  std::vector<fd_amd_tile_ent_t> ent( R );
+  for( ulong j=0; j<R; j++ ) ent[j] = fd_amd_tile_ent_t{ (uint32_t)((j % nframes) * FRAME_CHUNKS), 0u, fsz[j % nframes], 0u };
+  uint8_t * d_fr = NULL; fd_amd_tile_ent_t * d_ent = NULL; fd_amd_tile_res_t * d_res = NULL;
+  fd_amd_tile_dctl_t * d_ctl = NULL; uint8_t * d_scr = NULL;
+  fd_amd_tile_hctl_t * h_ctl = NULL; void * h_ctl_dev = NULL;
+  void * hm[3] = { NULL, NULL, NULL };   /* host allocations of ring, results, frames */
+  hipStream_t st = NULL; hipEvent_t e0 = NULL, e1 = NULL;
+  int rc = FD_ED25519_AMD_ERR_DEVICE;
+  std::vector<fd_amd_tile_res_t> res( R );
+  fd_amd_tile_args_t A;
+  float ms = 0.f;
+  auto halloc = [&]( int k, ulong sz, unsigned fl, void ** dev ) -> bool {
+    return hipHostMalloc( &hm[k], sz, hipHostMallocMapped | fl ) == hipSuccess && hipHostGetDevicePointer( dev, hm[k], 0 ) == hipSuccess;
+  };
+  unsigned const frfl = (where & 4u) ? hipHostMallocCoherent : hipHostMallocNonCoherent;
+  if( ( (where & 12u) ? !halloc( 2, (ulong)nframes * FD_VERIFY_AMD_FRAME_SZ, frfl, (void **)&d_fr )
+                      : hipMalloc( (void **)&d_fr, (ulong)nframes * FD_VERIFY_AMD_FRAME_SZ ) != hipSuccess ) ||
+      ( (where & 1u) ? !halloc( 0, R * sizeof(fd_amd_tile_ent_t), hipHostMallocCoherent, (void **)&d_ent )
+                     : hipMalloc( (void **)&d_ent, R * sizeof(fd_amd_tile_ent_t) ) != hipSuccess ) ||
+      ( (where & 2u) ? !halloc( 1, R * sizeof(fd_amd_tile_res_t), hipHostMallocCoherent, (void **)&d_res )
+                     : hipMalloc( (void **)&d_res, R * sizeof(fd_amd_tile_res_t) ) != hipSuccess ) ||
+      ( (where & 16u) && ( hipHostMalloc( (void **)&h_ctl, sizeof(fd_amd_tile_hctl_t), hipHostMallocMapped | hipHostMallocCoherent ) != hipSuccess ||
+                           hipHostGetDevicePointer( &h_ctl_dev, h_ctl, 0 ) != hipSuccess ) ) ||
+      hipMalloc( (void **)&d_ctl, sizeof(fd_amd_tile_dctl_t) ) != hipSuccess ||
+      hipMalloc( (void **)&d_scr, (ulong)waves * fd_amd_tile_scratch_stride() ) != hipSuccess ||
+      hipStreamCreateWithFlags( &st, hipStreamNonBlocking ) != hipSuccess ||
+      hipEventCreate( &e0 ) != hipSuccess || hipEventCreate( &e1 ) != hipSuccess ||
+      hipMemcpy( hm[2] ? hm[2] : (void *)d_fr, frames, (ulong)nframes * FD_VERIFY_AMD_FRAME_SZ, hipMemcpyDefault ) != hipSuccess ||
+      hipMemcpy( hm[0] ? hm[0] : (void *)d_ent, ent.data(), R * sizeof(fd_amd_tile_ent_t), hipMemcpyDefault ) != hipSuccess ||
+      hipMemset( hm[1] ? hm[1] : (void *)d_res, 0, R * sizeof(fd_amd_tile_res_t) ) != hipSuccess ||
+      hipMemset( d_ctl, 0, sizeof(fd_amd_tile_dctl_t) ) != hipSuccess ) goto done;
+  memset( &A, 0, sizeof A );
+  if( h_ctl ) memset( h_ctl, 0, sizeof(fd_amd_tile_hctl_t) );
+  A.ent = d_ent; A.res = d_res; A.mask = R - 1UL; A.src = d_fr; A.out = NULL; A.dctl = d_ctl; A.scratch = d_scr;
+  A.dbg = dbg & ~8u; A.hctl = (fd_amd_tile_hctl_t *)h_ctl_dev; A.watchdog = 1000000000UL;
+  if( hipEventRecord( e0, st ) != hipSuccess || fd_amd_launch_tile_synth( &A, waves + (h_ctl ? 1u : 0u), iters, eight, st ) ||
+      hipEventRecord( e1, st ) != hipSuccess || hipStreamSynchronize( st ) != hipSuccess ||
+      hipEventElapsedTime( &ms, e0, e1 ) != hipSuccess ||
+      hipMemcpy( res.data(), hm[1] ? hm[1] : (void *)d_res, R * sizeof(fd_amd_tile_res_t), hipMemcpyDefault ) != hipSuccess ) goto done;
+  *out_ms = (double)ms;
+  for( ulong j=0; j<n; j++ ) verdict[j] = (res[j].word >> 8) == j + 1UL ? (int8_t)(uint8_t)(res[j].word & 0xffUL) : (int8_t)99;
+  rc = FD_ED25519_AMD_OK;
+done:
+  if( st ) (void)hipStreamSynchronize( st );
+  if( e0 ) (void)hipEventDestroy( e0 );
+  if( e1 ) (void)hipEventDestroy( e1 );
+  if( st ) (void)hipStreamDestroy( st );
+  if( d_fr && !hm[2] ) (void)hipFree( d_fr );
+  if( d_ent && !hm[0] ) (void)hipFree( d_ent );
+  if( d_res && !hm[1] ) (void)hipFree( d_res );
+  for( int k=0; k<3; k++ ) if( hm[k] ) (void)hipHostFree( hm[k] );
+  if( h_ctl ) (void)hipHostFree( h_ctl );
+  if( d_ctl ) (void)hipFree( d_ctl );
+  if( d_scr ) (void)hipFree( d_scr );
   return rc;
 }
 
