@@ -76,10 +76,14 @@ typedef struct { uint32_t src_chunk, out_chunk, sz, pad; } fd_amd_tile_ent_t;
    count <= 64 | FD_AMD_TILE_LAT (8 lanes per signature) */
 typedef struct { uint64_t first; uint32_t count; uint32_t pad; } fd_amd_tile_desc_t;
 #define FD_AMD_TILE_LAT (0x80000000u)
-/* result (GPU -> host): word = (j + 1) << 8 | (uint8_t)verdict, stored
-   after tag and after the frag's output bytes (system-scope release), so a
-   host that sees word's index also sees the rest. */
-typedef struct { uint64_t tag, word; } fd_amd_tile_res_t;
+/* result of ring index j (GPU -> host), two arrays of R words: tag[j & mask]
+   and word[j & mask] = (j + 1) << 8 | (uint8_t)verdict, the word stored
+   after the tag and after the frag's output bytes (system-scope release),
+   so a host that sees word's index also sees the rest.  Arrays, not
+   {tag, word} records: a chunk's 64 lanes then store 512 contiguous bytes
+   per instruction (whole lines) -- interleaved 8-B stores into mapped host
+   memory held the L2 so long that every wave of the GPU slowed ~5x
+   (tools/tile_synth.py, profiles/r03_tile_persist_ab.txt). */
 /* host-written control words, each on its own 64-B line */
 typedef struct {
   uint64_t head;  uint64_t pad0[7];   /* chunk descriptors [.., head) are published to the GPU */
@@ -99,7 +103,8 @@ typedef struct {
   fd_amd_tile_hctl_t *       hctl;     /* device address of the mapped control words */
   fd_amd_tile_ent_t const *  ent;      /* device address of the mapped ring */
   fd_amd_tile_desc_t const * desc;     /* device address of the mapped chunk descriptors (same size as the ring) */
-  fd_amd_tile_res_t *        res;      /* device address of the mapped results */
+  uint64_t *                 res_tag;  /* device address of the mapped results: tags */
+  uint64_t *                 res_word; /*   and verdict words */
   uint64_t                   mask;     /* ring size - 1 (power of 2) */
   uint8_t const *            src;      /* frag source region (mapped): input dcache (zero-copy) or the output frames */
   uint8_t *                  out;      /* output frames (mapped) to fill, or NULL (copy mode: the host filled them) */
@@ -107,7 +112,7 @@ typedef struct {
   uint8_t *                  scratch;  /* per-wave scratch, fd_amd_tile_scratch_stride() bytes apart */
   uint64_t                   watchdog; /* s_memrealtime ticks (100 MHz) without a host heartbeat before the kernel gives up */
   uint32_t                   prof;     /* debug: sum per-phase time stamps into dctl->prof */
-  uint32_t                   dbg;      /* A/B only: 8 read frags from src_dev, 16 no output-frame writes, 32 agent-scope acquire, 64 no acquire, 128 no release fence */
+  uint32_t                   dbg;      /* A/B only: 8 read frags from src_dev, 16 no output-frame writes, 32 agent-scope acquire, 64 no acquire, 128 no release fence, 1024 plain result stores */
   uint8_t const *            src_dev;  /* A/B only: a device copy of the source region */
 } fd_amd_tile_args_t;
 size_t fd_amd_tile_scratch_stride( void );

@@ -2027,12 +2027,14 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __rest
   TILE_STAMP( 2 );
   /* 4. results: tags (and, zero-copy, the output frames above) first, one
         system-scope release, then the words the host polls */
-  u64 idx = c0 + l;
-  fd_amd_tile_res_t * r = A.res + (idx & A.mask);
-  if( l < k ) st_sys64( &r->tag, ((u64 const *)(ws + L.tag))[l] );
+  u64 const idx = c0 + l, j = idx & A.mask;
+  bool const plain = (A.dbg & 1024u) != 0u;
+  u64 const tg = ((u64 const *)(ws + L.tag))[l];
+  if( l < k ) { if( plain ) A.res_tag[j] = tg; else st_sys64( A.res_tag + j, tg ); }
   if( !(A.dbg & 128u) ) __builtin_amdgcn_fence( __ATOMIC_RELEASE, "" );
   asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
-  if( l < k ) st_sys64( &r->word, ((idx + 1UL) << 8) | (u64)(u8)err[l] );
+  u64 const wd = ((idx + 1UL) << 8) | (u64)(u8)err[l];
+  if( l < k ) { if( plain ) A.res_word[j] = wd; else st_sys64( A.res_word + j, wd ); }
   TILE_STAMP( 3 );
 # undef TILE_STAMP
 }

@@ -184,18 +184,25 @@ struct fd_verify_amd_tile {
   fd_amd_tile_hctl_t * hctl;  void * hctl_dev;
   fd_amd_tile_ent_t *  ring;  void * ring_dev;
   fd_amd_tile_desc_t * desc;  void * desc_dev;   /* chunk descriptors (same size as the ring) */
-  fd_amd_tile_res_t *  res;   void * res_dev;
+  uint64_t *           res;   void * res_dev;   /* results: R tags, then R verdict words */
   fd_amd_tile_dctl_t * dctl;
   uint8_t *            scratch;
   ulong                R;          /* ring size (power of 2) */
   ulong                window;     /* frags in flight at most (handed to the GPU, not yet published) */
   uint32_t             waves;
   ulong                light_frags;   /* hand-offs while fewer frags are in flight are cut into latency chunks */
+  ulong                chunk_wait_ns; /* throughput mode: longest a partial chunk waits for company */
   ulong                desc_seq;      /* descriptors published, monotonic over the tile's life */
   std::vector<pending_t> ppend;    /* per ring slot */
   ulong                ring_seq;   /* ring index of the next frag, monotonic over the tile's life */
   bool                 batched;    /* FD_AMD_TILE_BATCHED=1: the multi-stream batch path for every framing (A/B) */
 };
+
+static ulong
+env_ulong( char const * name, ulong dflt ) {
+  char const * v = getenv( name );
+  return ( v && *v ) ? strtoul( v, NULL, 0 ) : dflt;
+}
 
 extern "C" int
 fd_verify_amd_tile_register_dcache( fd_verify_amd_tile_t * t, void * base, ulong sz ) {
@@ -203,7 +210,8 @@ fd_verify_amd_tile_register_dcache( fd_verify_amd_tile_t * t, void * base, ulong
   if( hipSetDevice( t->eng->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
   if( t->reg_base ) { (void)hipHostUnregister( t->reg_base ); t->reg_base = NULL; t->reg_dev = NULL; t->reg_sz = 0; }
   uintptr_t lo = (uintptr_t)base & ~(uintptr_t)4095, hi = ((uintptr_t)base + sz + 4095) & ~(uintptr_t)4095;
-  if( hipHostRegister( (void *)lo, hi - lo, hipHostRegisterMapped ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  unsigned const rf = hipHostRegisterMapped | ( env_ulong( "FD_AMD_TILE_REG_UNCACHED", 0UL ) ? hipExtHostRegisterUncached : 0u );
+  if( hipHostRegister( (void *)lo, hi - lo, rf ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
   void * dev = NULL;
   if( hipHostGetDevicePointer( &dev, (void *)lo, 0 ) != hipSuccess ) {
     (void)hipHostUnregister( (void *)lo );
@@ -264,11 +272,6 @@ fd_verify_amd_tile_delete( fd_verify_amd_tile_t * t ) {
   delete t;
 }
 
-static ulong
-env_ulong( char const * name, ulong dflt ) {
-  char const * v = getenv( name );
-  return ( v && *v ) ? strtoul( v, NULL, 0 ) : dflt;
-}
 
 /* The persistent consumer's resources: control words, ring and results in
    mapped coherent host memory, the device control block, per-wave scratch.
@@ -292,6 +295,7 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
   /* latency chunks (8 frags, 8 lanes per signature) while at most one such
      chunk per SIMD is in flight: 8 x 4 x CUs frags */
   t->light_frags = env_ulong( "FD_AMD_TILE_LIGHT_FRAGS", 32UL * (ulong)cus );
+  t->chunk_wait_ns = env_ulong( "FD_AMD_TILE_CHUNK_WAIT_NS", 50000UL );
   unsigned const hf = hipHostMallocMapped | hipHostMallocCoherent;
   if( hipStreamCreateWithFlags( &t->pst, hipStreamNonBlocking ) != hipSuccess ||
       hipEventCreateWithFlags( &t->pdone, hipEventDisableTiming ) != hipSuccess ||
@@ -301,7 +305,7 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
       hipHostGetDevicePointer( &t->ring_dev, t->ring, 0 ) != hipSuccess ||
       hipHostMalloc( (void **)&t->desc, R * sizeof(fd_amd_tile_desc_t), hf ) != hipSuccess ||
       hipHostGetDevicePointer( &t->desc_dev, t->desc, 0 ) != hipSuccess ||
-      hipHostMalloc( (void **)&t->res, R * sizeof(fd_amd_tile_res_t), hf ) != hipSuccess ||
+      hipHostMalloc( (void **)&t->res, 2UL * R * sizeof(uint64_t), hf ) != hipSuccess ||
       hipHostGetDevicePointer( &t->res_dev, t->res, 0 ) != hipSuccess ||
       hipMalloc( (void **)&t->dctl, sizeof(fd_amd_tile_dctl_t) ) != hipSuccess ||
       hipMalloc( (void **)&t->scratch, waves * fd_amd_tile_scratch_stride() ) != hipSuccess )
@@ -310,7 +314,7 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
   memset( t->ring, 0, R * sizeof(fd_amd_tile_ent_t) );
   memset( t->desc, 0, R * sizeof(fd_amd_tile_desc_t) );
   t->desc_seq = 0UL;
-  memset( t->res,  0, R * sizeof(fd_amd_tile_res_t) );   /* word 0 never matches an index + 1 */
+  memset( t->res,  0, 2UL * R * sizeof(uint64_t) );   /* word 0 never matches an index + 1 */
   t->ppend.resize( R );
   t->ring_seq = 0UL;
   return FD_ED25519_AMD_OK;
@@ -708,7 +712,8 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   A.hctl = (fd_amd_tile_hctl_t *)t->hctl_dev;
   A.ent  = (fd_amd_tile_ent_t const *)t->ring_dev;
   A.desc = (fd_amd_tile_desc_t const *)t->desc_dev;
-  A.res  = (fd_amd_tile_res_t *)t->res_dev;
+  A.res_tag  = (uint64_t *)t->res_dev;
+  A.res_word = (uint64_t *)t->res_dev + t->R;
   A.mask = mask;
   A.src  = zc_dev ? zc_dev : t->out_dev;
   A.out  = zc_dev ? t->out_dev : NULL;
@@ -737,43 +742,70 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   int   rc = FD_ED25519_AMD_OK;
   uchar const * in_chunk0b = (uchar const *)in_chunk0;
 
+  ulong iter = 0UL;
+  /* debug (FD_AMD_TILE_DEBUG): host TSC ticks in publish, staging, hand-off and empty passes */
+  bool const hdbg = A.prof != 0u;
+  ulong hpt[3] = { 0, 0, 0 }, ht = hdbg ? __rdtsc() : 0UL, ht0 = ht, hns0 = hdbg ? now_ns() : 0UL, hin0 = in_cnt, hpass = 0;
+# define HSTAMP( k_ ) do { if( hdbg ) { ulong t_ = __rdtsc(); hpt[k_] += t_ - ht; ht = t_; } } while(0)
   for( ;; ) {
-    __atomic_store_n( &H->beat, ++beat, __ATOMIC_RELAXED );
+    /* the kernel's watchdog needs a heartbeat now and then, not every
+       pass: each store after a GPU read of the line is a cache-line
+       ownership round trip */
+    if( !(++iter & 63UL) ) __atomic_store_n( &H->beat, ++beat, __ATOMIC_RELAXED );
     bool progress = false;
 
-    /* 1. publish in ring order */
-    while( pubd != handed ) {
-      fd_amd_tile_res_t const * r = t->res + (pubd & mask);
-      ulong w = __atomic_load_n( &r->word, __ATOMIC_ACQUIRE );
-      if( (w >> 8) != pubd + 1UL ) break;
-      pending_t const & m = t->ppend[pubd & mask];
-      pubd++; progress = true;
-      t->frame_retired = m.frame + 1UL;
-      /* zero copy: the GPU read the frag some time before now; if its mcache
-         line has been lapped since, the producer may have rewritten it */
-      if( zc_dev && __atomic_load_n( &in_mcache[ m.seq & (in_depth-1UL) ].seq, __ATOMIC_ACQUIRE ) != m.seq ) {
-        diag->ovrn_cnt++;
-        continue;
-      }
-      if( (schar)(uchar)(w & 0xffUL) ) { diag->sv_filt_cnt++; diag->sv_filt_sz += m.sz; continue; }
-      ulong tag = r->tag;   /* the verify's SHA-512 tag (dedup tile) */
-      if( out_fseq && (long)(out_seq - out_cr) >= 0 ) {   /* credit check against the slowest consumer */
-        out_cr = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) + out_depth;
-        if( (long)(out_seq - out_cr) >= 0 ) {
-          diag->backp_cnt++;
-          do {
-            __atomic_store_n( &H->beat, ++beat, __ATOMIC_RELAXED );
-            out_cr = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) + out_depth;
-          } while( (long)(out_seq - out_cr) >= 0 );
-        }
-      }
-      ulong f = m.frame % F;
-      t->frame_pub[f] = out_seq;
-      uint tspub = fd_verify_amd_tickcount();
-      fd_mcache_publish( out_mcache, out_depth, out_seq, tag, f * FRAME_CHUNKS, m.sz, m.ctl, m.tsorig, tspub );
-      if( lat && lat_n < lat_max ) lat[lat_n++] = tspub - m.tsorig;
-      out_seq++; diag->out_cnt++; diag->out_sz += m.sz;
+    /* 1. publish in ring order: count the results that are in, then (zero
+          copy) check once that the oldest of them was not lapped -- lapping
+          goes in sequence order, so if its mcache line is intact now, after
+          the GPU read every frag of the pass, so are the newer ones' -- then
+          publish them with one timestamp */
+    ulong ready = 0UL;
+    while( pubd + ready != handed && ready < 4096UL ) {
+      ulong w = __atomic_load_n( t->res + t->R + ((pubd + ready) & mask), __ATOMIC_ACQUIRE );
+      if( (w >> 8) != pubd + ready + 1UL ) break;
+      ready++;
     }
+    if( ready ) {
+      progress = true;
+      bool lap_ok = true;
+      if( zc_dev ) {
+        ulong const s0 = t->ppend[pubd & mask].seq;
+        lap_ok = __atomic_load_n( &in_mcache[ s0 & (in_depth-1UL) ].seq, __ATOMIC_ACQUIRE ) == s0;
+      }
+      uint const tspub = fd_verify_amd_tickcount();
+      for( ulong end = pubd + ready; pubd != end; ) {
+        ulong const j = pubd & mask;
+        ulong const w = t->res[ t->R + j ];
+        pending_t const & m = t->ppend[j];
+        pubd++;
+        t->frame_retired = m.frame + 1UL;
+        /* zero copy: the GPU read the frag some time before now; if its
+           mcache line has been lapped since, the producer may have
+           rewritten it */
+        if( !lap_ok && __atomic_load_n( &in_mcache[ m.seq & (in_depth-1UL) ].seq, __ATOMIC_ACQUIRE ) != m.seq ) {
+          diag->ovrn_cnt++;
+          continue;
+        }
+        if( (schar)(uchar)(w & 0xffUL) ) { diag->sv_filt_cnt++; diag->sv_filt_sz += m.sz; continue; }
+        ulong tag = t->res[ j ];   /* the verify's SHA-512 tag (dedup tile) */
+        if( out_fseq && (long)(out_seq - out_cr) >= 0 ) {   /* credit check against the slowest consumer */
+          out_cr = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) + out_depth;
+          if( (long)(out_seq - out_cr) >= 0 ) {
+            diag->backp_cnt++;
+            do {
+              __atomic_store_n( &H->beat, ++beat, __ATOMIC_RELAXED );
+              out_cr = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) + out_depth;
+            } while( (long)(out_seq - out_cr) >= 0 );
+          }
+        }
+        ulong f = m.frame % F;
+        t->frame_pub[f] = out_seq;
+        fd_mcache_publish( out_mcache, out_depth, out_seq, tag, f * FRAME_CHUNKS, m.sz, m.ctl, m.tsorig, tspub );
+        if( lat && lat_n < lat_max ) lat[lat_n++] = tspub - m.tsorig;
+        out_seq++; diag->out_cnt++; diag->out_sz += m.sz;
+      }
+    }
+    HSTAMP( 0 );
     /* producer credit: copy mode is done with a frag once it is copied,
        zero copy once it is published (or dropped) */
     if( in_fseq ) {
@@ -789,6 +821,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       if( frag_cnt && in_seq - in_seq0 >= frag_cnt ) break;
       if( staged - pubd >= W ) { full = true; break; }
       fd_frag_meta_t const * m = in_mcache + (in_seq & (in_depth-1UL));
+      __builtin_prefetch( in_mcache + ((in_seq + 16UL) & (in_depth-1UL)) );
       ulong seq_found = __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE );
       long  d = (long)(seq_found - in_seq);
       if( d < 0 ) { idle_in = true; break; }                             /* not yet published */
@@ -819,8 +852,10 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
         p = dst;
       }
       in_seq++; in_cnt++;
-      ulong ha_tag; memcpy( &ha_tag, p + 32, 8 );                        /* first 8 signature bytes */
-      if( t->tc.insert( ha_tag ) ) { diag->ha_filt_cnt++; diag->ha_filt_sz += sz; continue; }
+      if( t->tc.depth ) {   /* HA dedup on the first 8 signature bytes (reads the frag: a cache miss in zero copy) */
+        ulong ha_tag; memcpy( &ha_tag, p + 32, 8 );
+        if( t->tc.insert( ha_tag ) ) { diag->ha_filt_cnt++; diag->ha_filt_sz += sz; continue; }
+      }
       t->frame_pub[f] = FRAME_FREE;
       t->frame_next++;
       fd_amd_tile_ent_t * en = t->ring + (staged & mask);
@@ -828,35 +863,55 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       en->out_chunk = (uint32_t)(f * FRAME_CHUNKS);
       en->sz        = (uint32_t)sz;
       t->ppend[staged & mask] = pending_t{ in_seq - 1UL, fr, (ushort)sz, (ushort)ctl, (uint)tsorig };
-      if( staged == handed && t->wait_ns ) hand_t0 = now_ns();
+      if( staged == handed ) hand_t0 = now_ns();
       staged++; progress = true;
     }
     __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
     if( in_fseq && !zc_dev && in_seq != fseq_pub ) { __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE ); fseq_pub = in_seq; }
     done_in = frag_cnt ? (in_seq - in_seq0 >= frag_cnt) : (__atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0);
+    HSTAMP( 1 );
 
-    /* 3. hand over: cut [handed, staged) into chunks -- 8-frag latency
-          chunks while few frags are in flight, 64-frag throughput chunks
-          under load -- and publish their descriptors (x86 stores are
-          ordered: entries and descriptors are visible before the head) */
+    /* 3. hand over: cut staged frags into chunks and publish their
+          descriptors (x86 stores are ordered: entries and descriptors are
+          visible before the head).  A chunk takes one wave whatever its
+          size, so the cut follows the load:
+            latency mode (fewer than light_frags in flight): everything
+              staged, in chunks of up to 8 frags (8 lanes per signature),
+              when the input is momentarily drained (greedy; with
+              batch_wait_ns only while nothing is in flight) or the oldest
+              waited batch_wait_ns;
+            throughput mode: whole 64-frag chunks only (1 lane per
+              signature), a remainder once its oldest frag waited
+              chunk_wait_ns -- small hand-offs under load would otherwise
+              become small chunks, each holding a wave for a full chunk's
+              time.
+          Either mode hands over everything at batch_max staged frags, when
+          the window or the frames ran out, and at the end of the input. */
     if( staged != handed ) {
-      bool greedy = idle_in && (!t->wait_ns || handed == pubd);
-      if( staged - handed >= t->batch_max || full || greedy || done_in ||
-          (t->wait_ns && now_ns() - hand_t0 >= t->wait_ns) ) {
-        bool lat_mode = handed - pubd < t->light_frags;
+      bool  const lat_mode = handed - pubd < t->light_frags;
+      ulong const waited   = now_ns() - hand_t0;
+      bool  const flush    = staged - handed >= t->batch_max || full || done_in ||
+                             (t->wait_ns && waited >= t->wait_ns) || (!lat_mode && waited >= t->chunk_wait_ns);
+      ulong upto = handed;
+      if( flush || (lat_mode && idle_in && (!t->wait_ns || handed == pubd)) ) upto = staged;
+      else if( !lat_mode ) upto = handed + ((staged - handed) & ~63UL);
+      if( upto != handed ) {
         ulong K = lat_mode ? 8UL : 64UL, ds = t->desc_seq;
-        for( ulong c = handed; c < staged; c += K, ds++ ) {
+        for( ulong c = handed; c < upto; c += K, ds++ ) {
           fd_amd_tile_desc_t * dd = t->desc + (ds & mask);
           dd->first = c;
-          dd->count = (uint32_t)std::min( K, staged - c ) | (lat_mode ? FD_AMD_TILE_LAT : 0u);
+          dd->count = (uint32_t)std::min( K, upto - c ) | (lat_mode ? FD_AMD_TILE_LAT : 0u);
         }
         t->desc_seq = ds;
         __atomic_store_n( &H->head, ds, __ATOMIC_RELEASE );
-        diag->batch_cnt++; diag->batch_sig_cnt += staged - handed;
-        handed = staged; progress = true;
+        diag->batch_cnt++; diag->batch_sig_cnt += upto - handed;
+        handed = upto; progress = true;
+        if( staged != handed ) hand_t0 = now_ns();
       }
     }
 
+    HSTAMP( 2 );
+    if( hdbg && !progress ) hpass++;
     /* 4. an idle tile checks now and then that the kernel is still there */
     if( progress ) idle = 0UL;
     else if( ++idle >= 4096UL ) {
@@ -871,6 +926,13 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     }
   }
 
+# undef HSTAMP
+  if( hdbg ) {
+    double const tot = (double)(__rdtsc() - ht0);
+    fprintf( stderr, "tile debug (persistent, host): publish %.1f%% stage %.1f%% hand-off %.1f%%, %lu empty passes, %.1f ns/frag\n",
+             100.0*(double)hpt[0]/tot, 100.0*(double)hpt[1]/tot, 100.0*(double)hpt[2]/tot, hpass,
+             (double)(now_ns() - hns0) / (double)(in_cnt - hin0 + 1UL) );
+  }
   /* stop: the waves exit once nothing is left to claim */
   __atomic_store_n( &H->stop, 1u, __ATOMIC_RELEASE );
   if( hipEventSynchronize( t->pdone ) != hipSuccess ) rc = FD_ED25519_AMD_ERR_DEVICE;
@@ -916,13 +978,13 @@ fd_amd_tile_synth( int device, uint32_t waves, uint32_t iters, int eight, uint32
   ulong R = 1UL; while( R < n ) R <<= 1;
   std::vector<fd_amd_tile_ent_t> ent( R );
   for( ulong j=0; j<R; j++ ) ent[j] = fd_amd_tile_ent_t{ (uint32_t)((j % nframes) * FRAME_CHUNKS), 0u, fsz[j % nframes], 0u };
-  uint8_t * d_fr = NULL; fd_amd_tile_ent_t * d_ent = NULL; fd_amd_tile_res_t * d_res = NULL;
+  uint8_t * d_fr = NULL; fd_amd_tile_ent_t * d_ent = NULL; uint64_t * d_res = NULL;
   fd_amd_tile_dctl_t * d_ctl = NULL; uint8_t * d_scr = NULL;
   fd_amd_tile_hctl_t * h_ctl = NULL; void * h_ctl_dev = NULL;
   void * hm[3] = { NULL, NULL, NULL };   /* host allocations of ring, results, frames */
   hipStream_t st = NULL; hipEvent_t e0 = NULL, e1 = NULL;
   int rc = FD_ED25519_AMD_ERR_DEVICE;
-  std::vector<fd_amd_tile_res_t> res( R );
+  std::vector<uint64_t> res( 2UL * R );
   fd_amd_tile_args_t A;
   float ms = 0.f;
   auto halloc = [&]( int k, ulong sz, unsigned fl, void ** dev ) -> bool {
@@ -933,8 +995,8 @@ fd_amd_tile_synth( int device, uint32_t waves, uint32_t iters, int eight, uint32
                       : hipMalloc( (void **)&d_fr, (ulong)nframes * FD_VERIFY_AMD_FRAME_SZ ) != hipSuccess ) ||
       ( (where & 1u) ? !halloc( 0, R * sizeof(fd_amd_tile_ent_t), hipHostMallocCoherent, (void **)&d_ent )
                      : hipMalloc( (void **)&d_ent, R * sizeof(fd_amd_tile_ent_t) ) != hipSuccess ) ||
-      ( (where & 2u) ? !halloc( 1, R * sizeof(fd_amd_tile_res_t), hipHostMallocCoherent, (void **)&d_res )
-                     : hipMalloc( (void **)&d_res, R * sizeof(fd_amd_tile_res_t) ) != hipSuccess ) ||
+      ( (where & 2u) ? !halloc( 1, 2UL * R * sizeof(uint64_t), hipHostMallocCoherent, (void **)&d_res )
+                     : hipMalloc( (void **)&d_res, 2UL * R * sizeof(uint64_t) ) != hipSuccess ) ||
       ( (where & 16u) && ( hipHostMalloc( (void **)&h_ctl, sizeof(fd_amd_tile_hctl_t), hipHostMallocMapped | hipHostMallocCoherent ) != hipSuccess ||
                            hipHostGetDevicePointer( &h_ctl_dev, h_ctl, 0 ) != hipSuccess ) ) ||
       hipMalloc( (void **)&d_ctl, sizeof(fd_amd_tile_dctl_t) ) != hipSuccess ||
@@ -943,18 +1005,18 @@ fd_amd_tile_synth( int device, uint32_t waves, uint32_t iters, int eight, uint32
       hipEventCreate( &e0 ) != hipSuccess || hipEventCreate( &e1 ) != hipSuccess ||
       hipMemcpy( hm[2] ? hm[2] : (void *)d_fr, frames, (ulong)nframes * FD_VERIFY_AMD_FRAME_SZ, hipMemcpyDefault ) != hipSuccess ||
       hipMemcpy( hm[0] ? hm[0] : (void *)d_ent, ent.data(), R * sizeof(fd_amd_tile_ent_t), hipMemcpyDefault ) != hipSuccess ||
-      hipMemset( hm[1] ? hm[1] : (void *)d_res, 0, R * sizeof(fd_amd_tile_res_t) ) != hipSuccess ||
+      hipMemset( hm[1] ? hm[1] : (void *)d_res, 0, 2UL * R * sizeof(uint64_t) ) != hipSuccess ||
       hipMemset( d_ctl, 0, sizeof(fd_amd_tile_dctl_t) ) != hipSuccess ) goto done;
   memset( &A, 0, sizeof A );
   if( h_ctl ) memset( h_ctl, 0, sizeof(fd_amd_tile_hctl_t) );
-  A.ent = d_ent; A.res = d_res; A.mask = R - 1UL; A.src = d_fr; A.out = NULL; A.dctl = d_ctl; A.scratch = d_scr;
+  A.ent = d_ent; A.res_tag = d_res; A.res_word = d_res + R; A.mask = R - 1UL; A.src = d_fr; A.out = NULL; A.dctl = d_ctl; A.scratch = d_scr;
   A.dbg = dbg & ~8u; A.hctl = (fd_amd_tile_hctl_t *)h_ctl_dev; A.watchdog = 1000000000UL;
   if( hipEventRecord( e0, st ) != hipSuccess || fd_amd_launch_tile_synth( &A, waves + (h_ctl ? 1u : 0u), iters, eight, st ) ||
       hipEventRecord( e1, st ) != hipSuccess || hipStreamSynchronize( st ) != hipSuccess ||
       hipEventElapsedTime( &ms, e0, e1 ) != hipSuccess ||
-      hipMemcpy( res.data(), hm[1] ? hm[1] : (void *)d_res, R * sizeof(fd_amd_tile_res_t), hipMemcpyDefault ) != hipSuccess ) goto done;
+      hipMemcpy( res.data(), hm[1] ? hm[1] : (void *)d_res, 2UL * R * sizeof(uint64_t), hipMemcpyDefault ) != hipSuccess ) goto done;
   *out_ms = (double)ms;
-  for( ulong j=0; j<n; j++ ) verdict[j] = (res[j].word >> 8) == j + 1UL ? (int8_t)(uint8_t)(res[j].word & 0xffUL) : (int8_t)99;
+  for( ulong j=0; j<n; j++ ) verdict[j] = (res[R + j] >> 8) == j + 1UL ? (int8_t)(uint8_t)(res[R + j] & 0xffUL) : (int8_t)99;
   rc = FD_ED25519_AMD_OK;
 done:
   if( st ) (void)hipStreamSynchronize( st );
