@@ -388,9 +388,10 @@ def stream_rows(local, pub, sig, off, sz, blob, args):
             row[key] = rr
         rows.append(row)
     return {"path": "producer (metadata only; frames pre-placed in the data region as a NIC would) -> in "
-                    "mcache/dcache -> verify tile (adaptive GPU batches, 4 in flight; copy: frag copied into the "
-                    "tile's output dcache and released; zero_copy: GPU copies from the mapped input region, input "
-                    "released when its batch retires) -> out mcache + tile-owned out dcache -> consumer (checks "
+                    "mcache/dcache -> verify tile (one persistent GPU kernel fed through mapped ring/descriptor "
+                    "memory, load-adaptive chunks; copy: frag copied into the tile's output dcache and released; "
+                    "zero_copy: GPU copies from the mapped input region, input released when the frag is "
+                    "published) -> out mcache + tile-owned out dcache -> consumer (checks "
                     "verdict, tag and order of every frag, bytes of every 16th); latency = scheduled send to tile publish",
             "pool": "%d signatures of %d B, %d with one message bit flipped" % (m, int(p_sz[0]), bad.size),
             "frags_per_run": args.stream_frags,

@@ -210,8 +210,7 @@ fd_verify_amd_tile_register_dcache( fd_verify_amd_tile_t * t, void * base, ulong
   if( hipSetDevice( t->eng->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
   if( t->reg_base ) { (void)hipHostUnregister( t->reg_base ); t->reg_base = NULL; t->reg_dev = NULL; t->reg_sz = 0; }
   uintptr_t lo = (uintptr_t)base & ~(uintptr_t)4095, hi = ((uintptr_t)base + sz + 4095) & ~(uintptr_t)4095;
-  unsigned const rf = hipHostRegisterMapped | ( env_ulong( "FD_AMD_TILE_REG_UNCACHED", 0UL ) ? hipExtHostRegisterUncached : 0u );
-  if( hipHostRegister( (void *)lo, hi - lo, rf ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  if( hipHostRegister( (void *)lo, hi - lo, hipHostRegisterMapped ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
   void * dev = NULL;
   if( hipHostGetDevicePointer( &dev, (void *)lo, 0 ) != hipSuccess ) {
     (void)hipHostUnregister( (void *)lo );
@@ -349,8 +348,7 @@ fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong 
          hipMalloc( (void **)&s.d_mir, batch_max * FD_VERIFY_AMD_FRAME_SZ + 64UL ) == hipSuccess;
     s.pend.resize( batch_max ); s.ich.resize( batch_max ); s.fsz.resize( batch_max ); s.tb.resize( batch_max + 1UL );
   }
-  unsigned const of = hipHostMallocMapped | ( env_ulong( "FD_AMD_TILE_OUT_COHERENT", 0UL ) ? hipHostMallocCoherent : 0u );
-  ok = ok && hipHostMalloc( (void **)&t->out_base, out_frame_cnt * FD_VERIFY_AMD_FRAME_SZ, of ) == hipSuccess &&
+  ok = ok && hipHostMalloc( (void **)&t->out_base, out_frame_cnt * FD_VERIFY_AMD_FRAME_SZ, hipHostMallocMapped ) == hipSuccess &&
        hipHostGetDevicePointer( (void **)&t->out_dev, t->out_base, 0 ) == hipSuccess;
   t->frame_cnt = out_frame_cnt;
   t->frame_pub.assign( out_frame_cnt, FRAME_FREE );

@@ -108,14 +108,26 @@ typedef struct {
 
 typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
 
-/* A tile bound to HIP device `device`, with up to 4 GPU batches in
-   flight.  batch_max: largest GPU batch.  Launch rule (adaptive): a batch
-   goes as soon as a slot is free and the input is momentarily drained
-   (light load: small batches, low latency; heavy load: every slot busy, so
-   batches grow toward batch_max).  batch_wait_ns != 0 replaces "drained"
-   by "the oldest staged frag waited batch_wait_ns" while another batch is
-   in flight (fewer, larger batches).  tcache_depth: HA dedup window (tags
-   remembered, 0 disables).
+/* A tile bound to HIP device `device`.  tcache_depth: HA dedup window
+   (tags remembered, 0 disables).
+
+   GPU side (PUB_SIG_MSG framing): ONE persistent kernel per run
+   (k_tile_persist) holds every wave slot of the GPU and verifies what the
+   tile's host thread hands over through mapped host memory -- ring entries
+   (frag chunk, output frame, size) and chunk descriptors -- on one stream,
+   so it needs one hardware queue (HIP's default GPU_MAX_HW_QUEUES = 4 is
+   enough) and the GPU never drains between hand-offs.  Hand-off rule
+   (adaptive): while fewer than 32 x CUs frags are in flight, everything
+   staged goes as soon as the input is momentarily drained, in chunks of up
+   to 8 frags verified 8 lanes per signature (latency); under load only
+   whole 64-frag chunks go, verified 1 lane per signature (throughput), a
+   partial one once its oldest frag waited 50 us.  batch_max: the most frags
+   staged before a hand-off is forced.  batch_wait_ns != 0 replaces
+   "drained" by "the oldest staged frag waited batch_wait_ns" while frags
+   are in flight.  At most 64 x batch_max (>= 2^13; 2^18 from batch_max
+   4096) frags are in flight.
+   TXN framing uses the batch path: up to 4 batches in flight, each on its
+   own stream (parse, verify, reduce per batch).
 
    Output data region.  Like the reference verify tile, which publishes
    frags out of a dcache it owns (fd_frank_verify_synth_load.c:324,409-411),
@@ -127,10 +139,6 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    that were verified.  A frame is reused only once the consumer's out_fseq
    has passed the frag it last carried (backpressure otherwise), so the
    output never changes under a consumer that honours flow control.
-   Each in-flight batch runs on its own HIP stream, and streams only
-   overlap on distinct hardware queues: run the process with
-   GPU_MAX_HW_QUEUES >= 16 (HIP's default 4 put the 4 streams on 2 queues
-   and halved the small-batch rate, profiles/r02_tile_queues.txt).
    NULL on failure. */
 #define FD_VERIFY_AMD_FRAME_SZ (1408UL)   /* 22 chunks >= 96 + FD_ED25519_AMD_MSG_MAX */
 
@@ -224,7 +232,7 @@ fd_verify_amd_tickcount( void );
    entry s % pool_n) into a private mcache/dcache -- at `rate` frags/s (open
    loop; tsorig = scheduled send time) or, with rate 0, as fast as the tile
    accepts (credit-based flow control on the tile's in_fseq) -- the tile
-   runs on `device` with 4 batches in flight, and a consumer drains the
+   runs on `device`, and a consumer drains the
    output.  Runs until frag_cnt input frags were consumed.
 
    flags: FD_VERIFY_AMD_BENCH_ZERO_COPY maps the input data region into the

@@ -170,7 +170,7 @@ def _stream_pool(seed, count, szhi=1232):
 def test_tile_producer_rewrites_wrapping_dcache(zero_copy):
     """A producer that writes every frame into a small wrapping data region
     (in_depth + 64 frames) as fast as the tile's in_fseq credit allows,
-    with 4 batches of 256 in flight: every published frag's verdict, tag,
+    at batch_max 256: every published frag's verdict, tag,
     bytes (in the tile's output dcache) and order equal the oracle's, none
     is missing, none overran."""
     from firedancer_amd import tango
@@ -201,9 +201,10 @@ def test_tile_lapping_producer_never_publishes_rewritten_frags(zero_copy):
 @pytest.mark.parametrize("zero_copy", [False, True])
 def test_tile_large_batches_vs_oracle(batch_max, zero_copy):
     """Config 5 at its large batch caps: saturated stream of fresh
-    signatures with 10 % corrupted frags through 4 in-flight batches of up
-    to batch_max; the published stream equals the oracle's accepted set, in
-    order, with the right tags and bytes."""
+    signatures with 10 % corrupted frags through the persistent consumer;
+    the published stream equals the oracle's accepted set, in order, with
+    the right tags and bytes, and under saturation most frags reach the GPU
+    in whole 64-frag throughput chunks."""
     from firedancer_amd import tango
     pub, sig, off, sz, blob, err, tag = _stream_pool(4096 + batch_max + zero_copy, 8192, 400)
     nf = 8 * batch_max + 12345
@@ -212,7 +213,8 @@ def test_tile_large_batches_vs_oracle(batch_max, zero_copy):
     want = int((err[np.arange(nf) % err.size] == 0).sum())
     assert r["mismatches"] == 0 and r["ovrn"] == 0
     assert r["checked"] == r["published"] == want and r["sv_filt"] == nf - want
-    assert r["mean_batch"] > batch_max / 8
+    assert r["gpu_frags_lat"] + r["gpu_frags_thr"] == nf
+    assert r["gpu_frags_thr"] > nf / 2 and r["gpu_frags_thr"] >= 60 * r["gpu_chunks_thr"]
 
 
 @pytest.mark.parametrize("zero_copy", [False, True])
