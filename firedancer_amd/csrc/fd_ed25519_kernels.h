@@ -22,7 +22,10 @@ ws_layout_t fd_amd_ws_layout( size_t n );
 int fd_amd_launch_verify( uint32_t n, uint8_t const * d_pub, uint8_t const * d_sig, uint32_t const * d_off,
                           uint32_t const * d_sz, uint8_t const * d_blob, int8_t * d_err, void * d_ws,
                           hipStream_t stream, int want_stats, hipEvent_t const * ev /* 4 or NULL */,
-                          int8_t const * d_skip = NULL, int dsm_mode = 0 );
+                          int8_t const * d_skip = NULL, int dsm_mode = 0, int8_t * d_out = NULL );
+/* d_out (NULL = none): on the latency path (fd_amd_uses_latency_path) the
+   last kernel also writes every verdict to d_out, e.g. mapped host memory,
+   so the caller needs no copy kernel; the throughput path ignores it. */
 /* Verdict byte that marks every signature of a launch whose k_dsmp hang
    guard tripped (never a reference code): the host calls turn it into
    FD_ED25519_AMD_ERR_DEVICE. */

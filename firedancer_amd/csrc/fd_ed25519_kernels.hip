@@ -825,7 +825,7 @@ quad_cached_row( p3 const & u, u64 m1, u64 m2 ) {
 }
 
 __global__ void __launch_bounds__(64)
-k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats ) {
+k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats, i8 * __restrict__ out ) {
   /* the base-point table in the Ai slab's row layout (see k_dsm8) */
   __shared__ __attribute__((aligned(16))) i32 bi12[8][48];
   for( int k=threadIdx.x; k<8*48; k+=64 ) {
@@ -983,6 +983,7 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
     int both = qb<0>( e01 ) & qb<1>( e01 );
     if( act && qd == 0 ) err[i] = (i8)(both ? 0 : -3);
   }
+  if( out && i < n && qd == 0 ) out[i] = err[i];   /* every verdict, straight to mapped host memory */
 
   if( want_stats && i < n && qd == 0 ) {
     u32 * st = (u32 *)(ws + L.st);
@@ -1304,12 +1305,15 @@ dsm8_body( u32 gt, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout
 }
 
 __global__ void __launch_bounds__(64)
-k_dsm8( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats ) {
+k_dsm8( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats, i8 * __restrict__ out ) {
   __shared__ __attribute__((aligned(16))) i32 bi12[8][48];
   __shared__ u64 evl[8][33];
   bi12_fill( bi12 );
   __syncthreads();
-  dsm8_body( blockIdx.x * 64u + threadIdx.x, n, err, ws, L, want_stats, bi12, evl );
+  u32 const gt = blockIdx.x * 64u + threadIdx.x;
+  dsm8_body( gt, n, err, ws, L, want_stats, bi12, evl );
+  /* every verdict, straight to mapped host memory, by the lane that wrote it */
+  if( out && (gt >> 3) < n && !(threadIdx.x & 7u) ) out[gt >> 3] = err[gt >> 3];
 }
 
 /* ------------------------------------------------------------------ */
@@ -2284,7 +2288,7 @@ fd_amd_uses_latency_path( uint32_t n, int dsm_mode ) {
 int
 fd_amd_launch_verify( u32 n, u8 const * d_pub, u8 const * d_sig, u32 const * d_off, u32 const * d_sz,
                       u8 const * d_blob, i8 * d_err, void * d_ws, hipStream_t stream, int want_stats,
-                      hipEvent_t const * ev, i8 const * d_skip, int dsm_mode ) {
+                      hipEvent_t const * ev, i8 const * d_skip, int dsm_mode, i8 * d_out ) {
   if( !n ) return 0;
   ws_layout_t L = fd_amd_ws_layout( n );
   u8 * ws = (u8 *)d_ws;
@@ -2295,8 +2299,8 @@ fd_amd_launch_verify( u32 n, u8 const * d_pub, u8 const * d_sig, u32 const * d_o
   if( small ) {   /* latency path: one front launch (hash || decompress), then k_dsm8 or k_dsm4 */
     hipLaunchKernelGGL( k_front, dim3(3u*nb), dim3(64), 0, stream, n, nb, d_pub, d_sig, d_off, d_sz, d_blob, d_err, ws, L, d_skip );
     if( ev ) { (void)hipEventRecord( ev[1], stream ); (void)hipEventRecord( ev[2], stream ); }
-    if( eight ) hipLaunchKernelGGL( k_dsm8, dim3((n + 7u)/8u), dim3(64), 0, stream, n, d_err, ws, L, want_stats );
-    else        hipLaunchKernelGGL( k_dsm4, dim3((n + 15u)/16u), dim3(64), 0, stream, n, d_err, ws, L, want_stats );
+    if( eight ) hipLaunchKernelGGL( k_dsm8, dim3((n + 7u)/8u), dim3(64), 0, stream, n, d_err, ws, L, want_stats, d_out );
+    else        hipLaunchKernelGGL( k_dsm4, dim3((n + 15u)/16u), dim3(64), 0, stream, n, d_err, ws, L, want_stats, d_out );
   } else {
     bool pooled = dsm_mode == 4 || (dsm_mode == 0 && n >= g_pool_min);
     hipLaunchKernelGGL( k_prep,   dim3(nb),    dim3(64), 0, stream, n, d_pub, d_sig, d_off, d_sz, d_blob, d_err, ws, L, d_skip );

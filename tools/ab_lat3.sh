@@ -1,7 +1,7 @@
 #!/bin/bash
 # latency A/B of library builds: GPU-only stage times at 4096 (tools/lat_floor.py) and the bench's
 # p50 rows (registered, staged, drop-in).  usage: tools/ab_lat3.sh <rounds> lib1.so lib2.so ...
-export GPU_MAX_HW_QUEUES=16
+# HIP default hardware queues
 R=$1; shift
 for r in $(seq $R); do
   for lib in "$@"; do
