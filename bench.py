@@ -89,6 +89,8 @@ def parse():
     ap.add_argument("--workload", choices=("sigs", "txn"), default="sigs",
                     help="sigs: configs[1] (default bench line); txn: configs[3] multi-signer transactions")
     ap.add_argument("--stream-frags", type=int, default=1 << 20, help="frags per streaming-tile run")
+    ap.add_argument("--txn-full-check", action="store_true",
+                    help="--workload txn: re-verify every transaction with the compiled reference (slow)")
     ap.add_argument("--no-host-fed", action="store_true",
                     help="skip the all-rank registered-host-memory pass (host_fed_node)")
     ap.add_argument("--multi-engine", action="store_true",
@@ -340,6 +342,15 @@ def run_txn(args, rank, world, dist):
             L.ref_txn_verify_batch(rej.size, _vp(payload), _vp(r_off), _vp(r_sz), _vp(r_err), nt)
             out["verdicts"]["rejected_rechecked_by_reference"] = bool(np.array_equal(r_err, terr[rej]))
             out["verdicts"]["rejected_codes"] = sorted(set(int(c) for c in terr[rej]))
+        if args.txn_full_check:
+            # every transaction of the run re-verified by the compiled
+            # reference, acceptances included (outside the timed region)
+            t1 = time.perf_counter()
+            f_err = np.zeros(toff.size, np.int8)
+            L.ref_txn_verify_batch(toff.size, _vp(payload), _vp(toff), _vp(tsz), _vp(f_err), nt)
+            out["verdicts"]["all_txns_rechecked_by_reference"] = {
+                "txns": int(toff.size), "signatures": int(tbase[-1]), "equal": bool(np.array_equal(f_err, terr)),
+                "mismatches": int((f_err != terr).sum()), "threads": nt, "seconds": time.perf_counter() - t1}
     print(json.dumps(out))
 
 

@@ -1104,6 +1104,7 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   std::thread prod( [&]() {
     pin_to( 1 );
     ulong p0 = now_ns(), cr = 0;   /* cr: first seq not covered by the cached credit */
+    uint  tnow = 0;                /* saturated: one timestamp per 32 frags (the producer must outrun the tile) */
     ulong lim = writes ? std::min( depth, D ) : depth;
     for( ulong seq=0; seq<frag_cnt; seq++ ) {
       ulong due = rate > 0.0 ? p0 + (ulong)((double)seq * 1e9 / rate) : 0UL;   /* paced: open loop */
@@ -1117,7 +1118,8 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
       if( writes ) put_frame( dcache + fr * frame, k );
       /* tsorig = the scheduled send time when paced, so producer stalls
          count as latency; the input seq when lapping (the check needs it) */
-      uint tso = lap ? (uint)seq : due ? (uint)due : fd_verify_amd_tickcount();
+      if( !due && !(seq & 31UL) ) tnow = fd_verify_amd_tickcount();
+      uint tso = lap ? (uint)seq : due ? (uint)due : tnow;
       fd_mcache_publish( in_mc.data(), depth, seq, 0UL, fr * frame_c, sz, 3UL, tso, 0UL );
     }
   } );
