@@ -1966,7 +1966,7 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __rest
   /* pt (debug, A.prof): s_memrealtime ticks spent in gather, prep + decomp,
      DSM, results; wave-uniform values */
   u64 ts = A.prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
-# define TILE_STAMP( k_ ) do { if( A.prof ) { u64 t_ = __builtin_amdgcn_s_memrealtime(); pt[k_] += t_ - ts; ts = t_; } } while(0)
+# define TILE_STAMP( k_ ) do { if( A.prof ) { u64 t_ = __builtin_amdgcn_s_memrealtime(); if( !threadIdx.x ) pt[k_] += t_ - ts; ts = t_; } } while(0)
   /* opaque per chunk: otherwise the compiler hoists every per-lane address
      of the bodies out of the persistent loop and spills them */
   {
@@ -2061,8 +2061,12 @@ k_tile_persist( fd_amd_tile_args_t A ) {
   u32 const xcc = __builtin_amdgcn_s_getreg( 20 | (0 << 6) | (3 << 11) ) % FD_AMD_TILE_MIRRORS;
   u64 const * mw = &D->mw[xcc].w;
   u8 * scr = A.scratch + (size_t)blockIdx.x * S.total;
-  u64 n8 = 0, n64 = 0, f8 = 0, f64 = 0;
-  u64 pt[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };   /* debug (A.prof): gather, front, DSM, results, wait, fence, -, - */
+  /* per-wave tallies in LDS, not registers (the DSM bodies want every VGPR):
+     [0..7] debug (A.prof) gather, front, DSM, results, wait, fence, -, -;
+     [8..11] latency chunks, throughput chunks, their frags */
+  __shared__ u64 s_tally[12];
+  if( l < 12u ) s_tally[l] = 0UL;
+  u64 * const pt = s_tally;
   for( ;; ) {
     u64 t = 0;
     if( l == 0u ) t = atomicAdd( (unsigned long long *)&D->ticket, 1ULL );
@@ -2082,7 +2086,7 @@ k_tile_persist( fd_amd_tile_args_t A ) {
       u32 const nap = (A.dbg & 256u) ? 64u : d < 2UL ? 1u : d < 64UL ? (u32)d : 64u;
       for( u32 z = 0; z < nap; z++ ) __builtin_amdgcn_s_sleep( 4 );
     }
-    if( A.prof ) pt[4] += __builtin_amdgcn_s_memrealtime() - t0;
+    if( A.prof && !l ) pt[4] += __builtin_amdgcn_s_memrealtime() - t0;
     if( !go ) break;
     /* descriptor t (host memory): { first ring index, count | latency mode << 31 } */
     u64 c = 0, cm = 0;
@@ -2100,15 +2104,12 @@ k_tile_persist( fd_amd_tile_args_t A ) {
     else if( A.dbg & 32u ) __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "agent" );
     else                   __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "" );
     asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
-    if( A.prof ) pt[5] += __builtin_amdgcn_s_memrealtime() - tf;
+    if( A.prof && !l ) pt[5] += __builtin_amdgcn_s_memrealtime() - tf;
     if( take && take <= 64u ) tile_chunk( A, c, take, e8, scr, L, S, bi, evl, pt );
-    if( e8 ) { n8++; f8 += take; } else { n64++; f64 += take; }
+    if( !l ) { s_tally[e8 ? 8 : 9] += 1UL; s_tally[e8 ? 10 : 11] += take; }
   }
   if( l == 0u ) {
-    atomicAdd( (unsigned long long *)&D->stat[0], (unsigned long long)n8 );
-    atomicAdd( (unsigned long long *)&D->stat[1], (unsigned long long)n64 );
-    atomicAdd( (unsigned long long *)&D->stat[2], (unsigned long long)f8 );
-    atomicAdd( (unsigned long long *)&D->stat[3], (unsigned long long)f64 );
+    _Pragma("unroll") for( int q=0; q<4; q++ ) atomicAdd( (unsigned long long *)&D->stat[q], (unsigned long long)s_tally[8 + q] );
     if( A.prof ) { _Pragma("unroll") for( int q=0; q<8; q++ ) atomicAdd( (unsigned long long *)&D->prof[q], (unsigned long long)pt[q] ); }
   }
 }

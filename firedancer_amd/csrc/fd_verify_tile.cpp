@@ -681,6 +681,28 @@ tile_run_batched( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
    The window (t->window frags handed over and not yet published) bounds
    the GPU's work in flight; with the output frames it is the tile's
    backpressure on the producer. */
+/* The persistent path's hand-off rule (tile_run_persist step 3): of the
+   staged frags [handed, staged), how far to hand over now, and in which
+   chunk mode (*lat_mode: 8-frag latency chunks, else 64-frag throughput
+   chunks).  Latency mode while fewer than light_frags frags are in flight
+   (handed - pubd): everything, as soon as the input is momentarily drained
+   (with wait_ns only while nothing is in flight).  Throughput mode: whole
+   64-frag chunks only, a remainder once its oldest frag waited
+   chunk_wait_ns.  Either mode: everything at batch_max staged, when the
+   window or the frames ran out (full), at the end of the input, or once the
+   oldest waited wait_ns (nonzero).  Pure; exported for the CPU tests. */
+extern "C" ulong
+fd_verify_amd_tile_cut( ulong staged, ulong handed, ulong pubd, ulong light_frags, ulong batch_max, ulong waited_ns,
+                        ulong wait_ns, ulong chunk_wait_ns, int idle_in, int full, int done_in, int * lat_mode ) {
+  bool const lat = handed - pubd < light_frags;
+  if( lat_mode ) *lat_mode = lat ? 1 : 0;
+  if( staged == handed ) return handed;
+  bool const flush = staged - handed >= batch_max || full || done_in || (wait_ns && waited_ns >= wait_ns) ||
+                     (!lat && waited_ns >= chunk_wait_ns);
+  if( flush || (lat && idle_in && (!wait_ns || handed == pubd)) ) return staged;
+  return lat ? handed : handed + ((staged - handed) & ~63UL);
+}
+
 static int
 tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ulong in_depth, void const * in_chunk0,
                   ulong in_seq0, ulong * in_fseq, fd_frag_meta_t * out_mcache, ulong out_depth, ulong out_seq0,
@@ -886,13 +908,9 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
           Either mode hands over everything at batch_max staged frags, when
           the window or the frames ran out, and at the end of the input. */
     if( staged != handed ) {
-      bool  const lat_mode = handed - pubd < t->light_frags;
-      ulong const waited   = now_ns() - hand_t0;
-      bool  const flush    = staged - handed >= t->batch_max || full || done_in ||
-                             (t->wait_ns && waited >= t->wait_ns) || (!lat_mode && waited >= t->chunk_wait_ns);
-      ulong upto = handed;
-      if( flush || (lat_mode && idle_in && (!t->wait_ns || handed == pubd)) ) upto = staged;
-      else if( !lat_mode ) upto = handed + ((staged - handed) & ~63UL);
+      int lat_mode;
+      ulong const upto = fd_verify_amd_tile_cut( staged, handed, pubd, t->light_frags, t->batch_max, now_ns() - hand_t0,
+                                                 t->wait_ns, t->chunk_wait_ns, idle_in, full, done_in, &lat_mode );
       if( upto != handed ) {
         ulong K = lat_mode ? 8UL : 64UL, ds = t->desc_seq;
         for( ulong c = handed; c < upto; c += K, ds++ ) {

@@ -226,6 +226,19 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t *  tile,
 uint
 fd_verify_amd_tickcount( void );
 
+/* The tile's hand-off rule (pure; what fd_verify_amd_tile_run applies to
+   its staged frags [handed, staged) with pubd the next frag to publish):
+   returns how far to hand over now; *lat_mode (may be NULL) = 1 for 8-frag
+   latency chunks (fewer than light_frags frags in flight), 0 for 64-frag
+   throughput chunks.  Latency mode hands over everything once idle_in (the
+   input is momentarily drained; with wait_ns != 0 only while nothing is in
+   flight); throughput mode whole 64-frag chunks, a remainder once
+   waited_ns >= chunk_wait_ns; both everything at batch_max staged, on full,
+   done_in, or waited_ns >= wait_ns != 0. */
+ulong
+fd_verify_amd_tile_cut( ulong staged, ulong handed, ulong pubd, ulong light_frags, ulong batch_max, ulong waited_ns,
+                        ulong wait_ns, ulong chunk_wait_ns, int idle_in, int full, int done_in, int * lat_mode );
+
 /* Streaming benchmark and end-to-end check (config 5): a producer thread
    publishes frags public_key | signature | message cyclically from the
    given pool (SoA layout of fd_ed25519_amd_verify_soa; frag s carries pool
