@@ -115,8 +115,6 @@ typedef struct {
   uint8_t *                  scratch;  /* per-wave scratch, fd_amd_tile_scratch_stride() bytes apart */
   uint64_t                   watchdog; /* s_memrealtime ticks (100 MHz) without a host heartbeat before the kernel gives up */
   uint32_t                   prof;     /* debug: sum per-phase time stamps into dctl->prof */
-  uint32_t                   dbg;      /* A/B only: 8 read frags from src_dev, 16 no output-frame writes, 32 agent-scope acquire, 64 no acquire, 128 no release fence, 1024 plain result stores */
-  uint8_t const *            src_dev;  /* A/B only: a device copy of the source region */
 } fd_amd_tile_args_t;
 size_t fd_amd_tile_scratch_stride( void );
 /* waves: grid size (wave 0 is the scout that mirrors the host words) */

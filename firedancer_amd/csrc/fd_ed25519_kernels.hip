@@ -1935,8 +1935,7 @@ size_t fd_amd_tile_scratch_stride( void ) { return tile_scratch_layout().total; 
 
 /* The scout (wave 0, lane 0): host words -> the XCDs' mirror words. */
 __device__ __noinline__ void
-tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog, u32 dbg ) {
-  u64 tmw = 0UL;
+tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog ) {
   u64 word = ld_dev64( &D->mw[0].w ), lastb = ~0UL, beat = 0UL;
   u64 tb = __builtin_amdgcn_s_memrealtime(), tpub = tb;
   for( ;; ) {
@@ -1950,8 +1949,8 @@ tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog, u32 db
        waiting waves' own watchdog quiet) */
     if( now - tpub > 1000UL && now - tb < 1000UL ) { beat++; tpub = now; }
     u64 w = (h & ((1UL << 48) - 1UL)) | ((beat & 0x3fffUL) << 48) | (dead ? TILE_MW_ERR : 0UL) | (st ? TILE_MW_STOP : 0UL);
-    if( w != word && ( !(dbg & 512u) || now - tmw > 2000UL || (w & (TILE_MW_ERR | TILE_MW_STOP)) ) ) {
-      word = w; tmw = now;
+    if( w != word ) {
+      word = w;
       _Pragma("unroll") for( int x=0; x<FD_AMD_TILE_MIRRORS; x++ ) st_dev64( &D->mw[x].w, w );
     }
     if( st || dead ) break;
@@ -1997,14 +1996,14 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __rest
       u32 const oc  = (u32)__shfl( (int)e_out, (int)(q & 63u) );
       u32 const fs  = (u32)__shfl( (int)e_sz,  (int)(q & 63u) );
       u32 const nv  = q < k ? (fs + 15u) >> 4 : 0u;
-      uint4 const * s = (uint4 const *)(((A.dbg & 8u) ? A.src_dev : A.src) + ((size_t)src << 6));
+      uint4 const * s = (uint4 const *)(A.src + ((size_t)src << 6));
       uint4 v[6];
       _Pragma("unroll") for( int r=0; r<6; r++ ) {
         u32 w = j + 16u*(u32)r;
         v[r] = w < nv ? s[w] : make_uint4( 0u, 0u, 0u, 0u );
       }
       uint4 * m = (uint4 *)(mir + (size_t)(q & 63u) * TILE_FRAME);
-      uint4 * o = (A.out && !(A.dbg & 16u)) ? (uint4 *)(A.out + ((size_t)oc << 6)) : (uint4 *)0;
+      uint4 * o = A.out ? (uint4 *)(A.out + ((size_t)oc << 6)) : (uint4 *)0;
       _Pragma("unroll") for( int r=0; r<6; r++ ) {
         u32 w = j + 16u*(u32)r;
         if( w < nv ) { m[w] = v[r]; if( o ) o[w] = v[r]; }
@@ -2032,13 +2031,11 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __rest
   /* 4. results: tags (and, zero-copy, the output frames above) first, one
         system-scope release, then the words the host polls */
   u64 const idx = c0 + l, j = idx & A.mask;
-  bool const plain = (A.dbg & 1024u) != 0u;
-  u64 const tg = ((u64 const *)(ws + L.tag))[l];
-  if( l < k ) { if( plain ) A.res_tag[j] = tg; else st_sys64( A.res_tag + j, tg ); }
-  if( !(A.dbg & 128u) ) __builtin_amdgcn_fence( __ATOMIC_RELEASE, "" );
+  if( l < k ) st_sys64( A.res_tag + j, ((u64 const *)(ws + L.tag))[l] );
+  __builtin_amdgcn_fence( __ATOMIC_RELEASE, "" );
   asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
   u64 const wd = ((idx + 1UL) << 8) | (u64)(u8)err[l];
-  if( l < k ) { if( plain ) A.res_word[j] = wd; else st_sys64( A.res_word + j, wd ); }
+  if( l < k ) st_sys64( A.res_word + j, wd );
   TILE_STAMP( 3 );
 # undef TILE_STAMP
 }
@@ -2052,7 +2049,7 @@ k_tile_persist( fd_amd_tile_args_t A ) {
   fd_amd_tile_dctl_t * D = A.dctl;
   u32 const l = threadIdx.x;
   if( blockIdx.x == 0u ) {
-    if( l == 0u ) tile_scout( D, A.hctl, A.watchdog, A.dbg );
+    if( l == 0u ) tile_scout( D, A.hctl, A.watchdog );
     return;
   }
   bi12_fill( bi );
@@ -2083,7 +2080,7 @@ k_tile_persist( fd_amd_tile_args_t A ) {
       if( w != last ) { last = w; tw = now; }
       else if( now - tw > A.watchdog ) break;       /* no scout (or host) for that long: give up */
       u64 const d = t - TILE_MW_HEAD( w );
-      u32 const nap = (A.dbg & 256u) ? 64u : d < 2UL ? 1u : d < 64UL ? (u32)d : 64u;
+      u32 const nap = d < 2UL ? 1u : d < 64UL ? (u32)d : 64u;
       for( u32 z = 0; z < nap; z++ ) __builtin_amdgcn_s_sleep( 4 );
     }
     if( A.prof && !l ) pt[4] += __builtin_amdgcn_s_memrealtime() - t0;
@@ -2100,9 +2097,7 @@ k_tile_persist( fd_amd_tile_args_t A ) {
     /* the frames were written by the host (copy mode) or the producer
        (zero-copy) into host memory: drop this CU's stale lines first */
     u64 const tf = A.prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
-    if( A.dbg & 64u )      { /* A/B: no acquire */ }
-    else if( A.dbg & 32u ) __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "agent" );
-    else                   __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "" );
+    __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "" );
     asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
     if( A.prof && !l ) pt[5] += __builtin_amdgcn_s_memrealtime() - tf;
     if( take && take <= 64u ) tile_chunk( A, c, take, e8, scr, L, S, bi, evl, pt );

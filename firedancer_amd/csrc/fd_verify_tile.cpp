@@ -741,15 +741,6 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   A.scratch = t->scratch;
   A.watchdog = 500000000UL;   /* 5 s of s_memrealtime (100 MHz) without a heartbeat */
   A.prof = (uint32_t)env_ulong( "FD_AMD_TILE_DEBUG", 0UL );
-  A.dbg  = (uint32_t)env_ulong( "FD_AMD_TILE_DBG", 0UL );
-  void * src_dev = NULL;
-  if( A.dbg & 8u ) {   /* A/B: frags read from a device copy of the source region (taken now: pre-placed frags only) */
-    ulong bytes = zc_dev ? zc_lim : t->frame_cnt * FD_VERIFY_AMD_FRAME_SZ;
-    if( hipMalloc( &src_dev, bytes ) != hipSuccess ||
-        hipMemcpy( src_dev, zc_dev ? (void const *)in_chunk0 : (void const *)t->out_base, bytes, hipMemcpyHostToDevice ) != hipSuccess )
-      return FD_ED25519_AMD_ERR_DEVICE;
-    A.src_dev = (uint8_t const *)src_dev;
-  }
   if( fd_amd_launch_tile_persist( &A, t->waves, t->pst ) || hipEventRecord( t->pdone, t->pst ) != hipSuccess ) {
     (void)hipStreamSynchronize( t->pst );
     return FD_ED25519_AMD_ERR_DEVICE;
@@ -952,7 +943,6 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   /* stop: the waves exit once nothing is left to claim */
   __atomic_store_n( &H->stop, 1u, __ATOMIC_RELEASE );
   if( hipEventSynchronize( t->pdone ) != hipSuccess ) rc = FD_ED25519_AMD_ERR_DEVICE;
-  if( src_dev ) (void)hipFree( src_dev );
   ulong st[4] = { 0, 0, 0, 0 };
   if( hipMemcpy( st, t->dctl->stat, sizeof st, hipMemcpyDeviceToHost ) != hipSuccess ) rc = FD_ED25519_AMD_ERR_DEVICE;
   if( __atomic_load_n( &H->kerr, __ATOMIC_ACQUIRE ) ) rc = FD_ED25519_AMD_ERR_DEVICE;
@@ -985,7 +975,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
    host memory, 8 frames in mapped non-coherent host memory, 16 one more
    wave polling mapped host control words meanwhile (the scout's load) */
 extern "C" int
-fd_amd_tile_synth( int device, uint32_t waves, uint32_t iters, int eight, uint32_t dbg, uint32_t where,
+fd_amd_tile_synth( int device, uint32_t waves, uint32_t iters, int eight, uint32_t where,
                    uint8_t const * frames, uint32_t nframes, uint32_t const * fsz, double * out_ms, int8_t * verdict ) {
   if( !frames || !nframes || !fsz || !out_ms || !verdict || !waves || !iters || waves > 65536u || iters > 4096u ) return FD_ED25519_AMD_ERR_INVAL;
   for( uint32_t f=0; f<nframes; f++ ) if( fsz[f] < 96u || fsz[f] > 96u + FD_ED25519_AMD_MSG_MAX ) return FD_ED25519_AMD_ERR_INVAL;
@@ -1026,7 +1016,7 @@ fd_amd_tile_synth( int device, uint32_t waves, uint32_t iters, int eight, uint32
   memset( &A, 0, sizeof A );
   if( h_ctl ) memset( h_ctl, 0, sizeof(fd_amd_tile_hctl_t) );
   A.ent = d_ent; A.res_tag = d_res; A.res_word = d_res + R; A.mask = R - 1UL; A.src = d_fr; A.out = NULL; A.dctl = d_ctl; A.scratch = d_scr;
-  A.dbg = dbg & ~8u; A.hctl = (fd_amd_tile_hctl_t *)h_ctl_dev; A.watchdog = 1000000000UL;
+  A.hctl = (fd_amd_tile_hctl_t *)h_ctl_dev; A.watchdog = 1000000000UL;
   if( hipEventRecord( e0, st ) != hipSuccess || fd_amd_launch_tile_synth( &A, waves + (h_ctl ? 1u : 0u), iters, eight, st ) ||
       hipEventRecord( e1, st ) != hipSuccess || hipStreamSynchronize( st ) != hipSuccess ||
       hipEventElapsedTime( &ms, e0, e1 ) != hipSuccess ||

@@ -23,21 +23,21 @@ for i in range(m):
 fsz = (96 + sz).astype(np.uint32)
 L = ed25519.lib()
 L.fd_amd_tile_synth.restype = ctypes.c_int
-# (waves, iters, eight, dbg, where): where 1 ring, 2 results, 4 frames (coherent), 8 frames (non-coherent)
+# (waves, iters, eight, where): where 1 ring, 2 results, 4 frames (coherent), 8 frames (non-coherent)
 # in mapped host memory, 16 a wave polling host words meanwhile
-cfgs = [(2048, 4, 0, 0, 0), (2048, 4, 0, 0, 1), (2048, 4, 0, 0, 2), (2048, 4, 0, 0, 4), (2048, 4, 0, 0, 8),
-        (2048, 4, 0, 0, 16), (2048, 4, 0, 0, 31 & ~8), (2048, 16, 1, 0, 0), (2048, 16, 1, 0, 31 & ~8)]
+cfgs = [(2048, 4, 0, 0), (2048, 4, 0, 1), (2048, 4, 0, 2), (2048, 4, 0, 4), (2048, 4, 0, 8),
+        (2048, 4, 0, 16), (2048, 4, 0, 31 & ~8), (2048, 16, 1, 0), (2048, 16, 1, 31 & ~8)]
 if len(sys.argv) > 1:
     cfgs = [tuple(int(x) for x in a.split(",")) for a in sys.argv[1:]]
-for waves, iters, eight, dbg, where in cfgs:
+for waves, iters, eight, where in cfgs:
     k = 8 if eight else 64
     n = waves * iters * k
     v = np.zeros(n, np.int8)
     ms = ctypes.c_double(0)
-    rc = L.fd_amd_tile_synth(0, waves, iters, eight, dbg, where, frames.ctypes.data_as(ctypes.c_void_p), m,
+    rc = L.fd_amd_tile_synth(0, waves, iters, eight, where, frames.ctypes.data_as(ctypes.c_void_p), m,
                              fsz.ctypes.data_as(ctypes.c_void_p), ctypes.byref(ms), v.ctypes.data_as(ctypes.c_void_p))
     if rc:
         raise SystemExit("fd_amd_tile_synth rc=%d" % rc)
-    print(json.dumps(dict(waves=waves, iters=iters, eight=eight, dbg=dbg, where=where, ms=round(ms.value, 3),
+    print(json.dumps(dict(waves=waves, iters=iters, eight=eight, where=where, ms=round(ms.value, 3),
                           ms_per_chunk=round(ms.value / iters, 3), frags_per_s=round(n / ms.value * 1e3),
                           ok=int((v == 0).sum()), bad=int((v != 0).sum()))), flush=True)
