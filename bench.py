@@ -88,7 +88,7 @@ def parse():
     ap.add_argument("--no-stream", action="store_true", help="skip the streaming-tile sweep (config 5)")
     ap.add_argument("--workload", choices=("sigs", "txn"), default="sigs",
                     help="sigs: configs[1] (default bench line); txn: configs[3] multi-signer transactions")
-    ap.add_argument("--stream-frags", type=int, default=1 << 20, help="frags per streaming-tile run")
+    ap.add_argument("--stream-frags", type=int, default=1 << 21, help="frags per streaming-tile run")
     ap.add_argument("--txn-full-check", action="store_true",
                     help="--workload txn: re-verify every transaction with the compiled reference (slow)")
     ap.add_argument("--no-host-fed", action="store_true",

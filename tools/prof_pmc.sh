@@ -4,7 +4,7 @@
 # usage: tools/prof_pmc.sh <outdir> [bench args...]
 set -o pipefail
 OUT=${1:-gpurun_out/pmc}; shift
-ARGS=${@:---sigs 1048576 --steps 2 --warmup 1 --streams 1 --no-cpu --no-latency --no-stream}
+ARGS=${@:---sigs 1048576 --steps 2 --warmup 1 --streams 1 --no-cpu --no-latency --no-stream --no-host-fed}
 export TMPDIR=/tmp
 mkdir -p $OUT
 run() { name=$1; shift; timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o p -- python3 bench.py $ARGS > $OUT/$name.log 2>&1 || { echo "pass $name failed"; exit 1; }; }
