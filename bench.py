@@ -395,7 +395,10 @@ def stream_rows(local, pub, sig, off, sz, blob, args):
                 rr["at_%d%%" % int(load * 100)] = {"offered_frags_per_s": rate, "frags_per_s": r["frags_per_s"],
                                                     "p50_us": r["p50_ns"] / 1e3, "p99_us": r["p99_ns"] / 1e3,
                                                     "mean_batch": r["mean_batch"], "sv_filt": int(r["sv_filt"]),
-                                                    "check_mismatches": int(r["mismatches"])}
+                                                    "check_mismatches": int(r["mismatches"]),
+                                                    "stalls_us": {"producer_late_max": r["producer_late_max_ns"] / 1e3,
+                                                                  "tile_pass_max": r["tile_pass_max_ns"] / 1e3,
+                                                                  "consumer_gap_max": r["consumer_gap_max_ns"] / 1e3}}
             row[key] = rr
         rows.append(row)
     return {"path": "producer (metadata only; frames pre-placed in the data region as a NIC would) -> in "

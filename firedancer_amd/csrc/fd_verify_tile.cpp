@@ -192,6 +192,7 @@ struct fd_verify_amd_tile {
   uint32_t             waves;
   ulong                light_frags;   /* hand-offs while fewer frags are in flight are cut into latency chunks */
   ulong                chunk_wait_ns; /* throughput mode: longest a partial chunk waits for company */
+  ulong                pass_max_ns;   /* longest pass of the last run's loop (stall diagnosis) */
   ulong                desc_seq;      /* descriptors published, monotonic over the tile's life */
   std::vector<pending_t> ppend;    /* per ring slot */
   ulong                ring_seq;   /* ring index of the next frag, monotonic over the tile's life */
@@ -753,7 +754,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   int   rc = FD_ED25519_AMD_OK;
   uchar const * in_chunk0b = (uchar const *)in_chunk0;
 
-  ulong iter = 0UL;
+  ulong iter = 0UL, pass_t = now_ns(), pass_max = 0UL;
   /* debug (FD_AMD_TILE_DEBUG): host TSC ticks in publish, staging, hand-off and empty passes */
   bool const hdbg = A.prof != 0u;
   ulong hpt[3] = { 0, 0, 0 }, ht = hdbg ? __rdtsc() : 0UL, ht0 = ht, hns0 = hdbg ? now_ns() : 0UL, hin0 = in_cnt, hpass = 0;
@@ -764,6 +765,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
        ownership round trip */
     if( !(++iter & 63UL) ) __atomic_store_n( &H->beat, ++beat, __ATOMIC_RELAXED );
     bool progress = false;
+    { ulong const tn = now_ns(); pass_max = std::max( pass_max, tn - pass_t ); pass_t = tn; }
 
     /* 1. publish in ring order: count the results that are in, then (zero
           copy) check once that the oldest of them was not lapped -- lapping
@@ -958,6 +960,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   diag->gpu_chunk_lat_cnt += st[0]; diag->gpu_chunk_thr_cnt += st[1];
   diag->gpu_frag_lat_cnt  += st[2]; diag->gpu_frag_thr_cnt  += st[3];
   t->ring_seq = staged;
+  t->pass_max_ns = pass_max;
   __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
   if( in_fseq ) __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE );
   t->out_seq_end = out_seq;
@@ -1086,13 +1089,16 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
 
   /* the three spinning threads (producer, tile, consumer) each get a CPU of
      their own from the process's allowed set, so the scheduler does not
-     stack them (the saturated rate otherwise varies run to run) */
+     stack them (the saturated rate otherwise varies run to run): the
+     highest-numbered allowed CPUs, away from CPU 0, which takes most of the
+     machine's interrupts (tile passes of 1-5 ms and p99 spikes were seen
+     with the tile thread on CPU 0) */
   cpu_set_t allowed, saved; CPU_ZERO( &allowed ); CPU_ZERO( &saved );
   int cpus[3] = { -1, -1, -1 }, ncpu = 0;
   bool pin = !sched_getaffinity( 0, sizeof allowed, &allowed ) && CPU_COUNT( &allowed ) >= 4;
   if( pin ) {
     saved = allowed;
-    for( int c=0; c<CPU_SETSIZE && ncpu<3; c++ ) if( CPU_ISSET( c, &allowed ) ) cpus[ncpu++] = c;
+    for( int c=CPU_SETSIZE-1; c>0 && ncpu<3; c-- ) if( CPU_ISSET( c, &allowed ) ) cpus[ncpu++] = c;
     pin = ncpu == 3;
   }
   auto pin_to = [&]( int k ) {
@@ -1106,7 +1112,7 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   std::vector<uint> lat( frag_cnt );
   fd_verify_amd_diag_t diag; memset( &diag, 0, sizeof diag );
   int tile_rc = 0;
-  ulong mism = 0, checked = 0;
+  ulong mism = 0, checked = 0, late_max = 0, gap_max = 0;
   ulong t0 = now_ns();
 
   std::thread prod( [&]() {
@@ -1116,7 +1122,11 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
     ulong lim = writes ? std::min( depth, D ) : depth;
     for( ulong seq=0; seq<frag_cnt; seq++ ) {
       ulong due = rate > 0.0 ? p0 + (ulong)((double)seq * 1e9 / rate) : 0UL;   /* paced: open loop */
-      if( due ) while( now_ns() < due ) { /* spin */ }
+      if( due ) {
+        ulong tn;
+        while( (tn = now_ns()) < due ) { /* spin */ }
+        late_max = std::max( late_max, tn - due );
+      }
       /* credit: neither the mcache line nor (when writing) the data frame
          of a frag the tile still reads is reused; refreshed only when the
          cached credit runs out */
@@ -1136,9 +1146,11 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
     ulong seq = 0, fseq = 0;   /* fseq: last value published to out_fseq (every 64 frags, or when idle) */
     ulong exp_s = 0;           /* check: next input seq that should be published */
     long  last = -1;
+    ulong tl = 0;              /* when the previous frag was seen */
     for( ;; ) {
       fd_frag_meta_t const * m = &out_mc[ seq & (out_depth-1UL) ];
       if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) == seq ) {
+        if( !(seq & 15UL) ) { ulong tn = now_ns(); if( tl ) gap_max = std::max( gap_max, tn - tl ); tl = tn; }
         if( check ) {
           ulong tag = m->sig, chunk = m->chunk, sz = m->sz, s_in;
           if( lap ) {
@@ -1180,6 +1192,7 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   if( rc ) __atomic_store_n( &in_fseq, ~0UL >> 1, __ATOMIC_RELEASE );   /* unblock the producer */
   prod.join(); cons.join();
   if( pin ) (void)pthread_setaffinity_np( pthread_self(), sizeof saved, &saved );
+  ulong const pass_max = tile->pass_max_ns;
   fd_verify_amd_tile_delete( tile );
   free( dcache );
   if( rc ) return rc;
@@ -1193,5 +1206,6 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   out[8] = (double)mism; out[9] = (double)checked;
   out[10] = (double)diag.gpu_chunk_lat_cnt; out[11] = (double)diag.gpu_chunk_thr_cnt;
   out[12] = (double)diag.gpu_frag_lat_cnt;  out[13] = (double)diag.gpu_frag_thr_cnt;
+  out[14] = (double)late_max; out[15] = (double)pass_max; out[16] = (double)gap_max;
   return FD_ED25519_AMD_OK;
 }

@@ -275,8 +275,11 @@ fd_verify_amd_tile_cut( ulong staged, ulong handed, ulong pubd, ulong light_frag
    frags that fail a check, plus frags that should have been published and
    were not, overrun ones excepted), out[9] = frags checked, out[10..13] =
    the persistent path's GPU chunks in latency / throughput mode and the
-   frags in each (0 on the batch path).  out holds 14 doubles.  Returns 0
-   or an error code. */
+   frags in each (0 on the batch path), out[14] = the paced producer's
+   largest lateness behind its schedule (ns; its stalls count as latency),
+   out[15] = the tile thread's longest pass of its run loop (ns; a stall of
+   the host thread shows here), out[16] = the consumer's longest gap between
+   two frags it saw.  out holds 17 doubles.  Returns 0 or an error code. */
 #define FD_VERIFY_AMD_BENCH_ZERO_COPY (1)
 #define FD_VERIFY_AMD_BENCH_WRITE     (2)
 #define FD_VERIFY_AMD_BENCH_LAP       (4)
