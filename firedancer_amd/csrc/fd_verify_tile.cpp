@@ -40,6 +40,7 @@
 #include <pthread.h>
 #include <vector>
 #include <atomic>
+#include <mutex>
 #include <algorithm>
 
 #include "../../include/fd_ed25519_amd.h"
@@ -193,6 +194,7 @@ struct fd_verify_amd_tile {
   ulong                light_frags;   /* hand-offs while fewer frags are in flight are cut into latency chunks */
   ulong                chunk_wait_ns; /* throughput mode: longest a partial chunk waits for company */
   ulong                pass_max_ns;   /* longest pass of the last run's loop (stall diagnosis) */
+  bool                 counted;       /* in the per-device live tile count */
   ulong                desc_seq;      /* descriptors published, monotonic over the tile's life */
   std::vector<pending_t> ppend;    /* per ring slot */
   ulong                ring_seq;   /* ring index of the next frag, monotonic over the tile's life */
@@ -245,6 +247,33 @@ fd_verify_amd_tile_out_data_sz( fd_verify_amd_tile_t * t ) {
                             p50 at every batch_max, higher saturated rate only at 16384): one wave's verify takes ~0.7 ms, so small
                             batches need several in flight to keep the GPU busy */
 
+/* Live tiles per device (process-wide): a run's persistent kernel takes
+   the wave slots of 8 x CUs / (tiles on its device), so tiles created on
+   one GPU before any of them runs share it instead of the first run
+   holding every slot (FD_AMD_TILE_WAVES fixes the count instead). */
+namespace {
+std::mutex g_tile_mu;
+int        g_tile_cnt[64];
+}
+
+static void
+tile_count( int device, int d ) {
+  if( device < 0 || device >= 64 ) return;
+  std::lock_guard<std::mutex> g( g_tile_mu );
+  g_tile_cnt[device] += d;
+}
+
+static uint32_t
+tile_run_waves( fd_verify_amd_tile_t const * t ) {
+  if( getenv( "FD_AMD_TILE_WAVES" ) ) return t->waves;
+  int n = 1;
+  if( t->eng->device >= 0 && t->eng->device < 64 ) {
+    std::lock_guard<std::mutex> g( g_tile_mu );
+    n = std::max( 1, g_tile_cnt[t->eng->device] );
+  }
+  return std::max( 2u, t->waves / (uint32_t)n );
+}
+
 extern "C" uint
 fd_verify_amd_tickcount( void ) {
   return (uint)now_ns();
@@ -253,6 +282,7 @@ fd_verify_amd_tickcount( void ) {
 extern "C" void
 fd_verify_amd_tile_delete( fd_verify_amd_tile_t * t ) {
   if( !t ) return;
+  if( t->counted ) tile_count( t->eng->device, -1 );
   (void)hipSetDevice( t->eng->device );
   fd_ed25519_amd_delete( t->eng );   /* synchronises every slot stream first */
   if( t->reg_base ) (void)hipHostUnregister( t->reg_base );
@@ -357,6 +387,7 @@ fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong 
   t->batched = env_ulong( "FD_AMD_TILE_BATCHED", 0UL ) != 0UL;
   ok = ok && ( t->batched || !tile_persist_alloc( t ) );
   if( !ok ) { fd_verify_amd_tile_delete( t ); return NULL; }
+  t->counted = true; tile_count( device, 1 );
   return t;
 }
 
@@ -742,7 +773,8 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   A.scratch = t->scratch;
   A.watchdog = 500000000UL;   /* 5 s of s_memrealtime (100 MHz) without a heartbeat */
   A.prof = (uint32_t)env_ulong( "FD_AMD_TILE_DEBUG", 0UL );
-  if( fd_amd_launch_tile_persist( &A, t->waves, t->pst ) || hipEventRecord( t->pdone, t->pst ) != hipSuccess ) {
+  uint32_t const waves = tile_run_waves( t );
+  if( fd_amd_launch_tile_persist( &A, waves, t->pst ) || hipEventRecord( t->pdone, t->pst ) != hipSuccess ) {
     (void)hipStreamSynchronize( t->pst );
     return FD_ED25519_AMD_ERR_DEVICE;
   }
@@ -951,7 +983,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   if( env_ulong( "FD_AMD_TILE_DEBUG", 0UL ) ) {   /* per-phase wave time (k_tile_persist, args.prof) */
     ulong pf[8];
     if( hipMemcpy( pf, t->dctl->prof, sizeof pf, hipMemcpyDeviceToHost ) == hipSuccess ) {
-      double w = (double)(t->waves - 1U) * 1e5;   /* ticks are 10 ns: per-wave ms */
+      double w = (double)(waves - 1U) * 1e5;   /* ticks are 10 ns: per-wave ms */
       fprintf( stderr, "tile debug: per-wave ms  gather %.2f front %.2f dsm %.2f results %.2f wait %.2f fence %.2f"
                "  (chunks %lu latency + %lu throughput)\n", pf[0]/w, pf[1]/w, pf[2]/w, pf[3]/w, pf[4]/w, pf[5]/w,
                st[0], st[1] );

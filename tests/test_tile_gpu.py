@@ -289,3 +289,43 @@ def test_tile_txn_framing_needs_room_for_a_full_transaction():
         tango.VerifyTile(0, batch_max=8, framing=tango.VerifyTile.FRAMING_TXN)
     t = tango.VerifyTile(0, batch_max=19, framing=tango.VerifyTile.FRAMING_TXN)
     t.close()
+
+
+def test_two_tiles_share_one_gpu():
+    """Two tiles created on one device before either runs split its wave
+    slots (each run's persistent kernel takes 8 x CUs / 2 waves), so their
+    runs proceed side by side from two threads; each publishes exactly the
+    oracle's accepted set, in order, with the right tags."""
+    import threading
+    from firedancer_amd import ed25519, tango
+    prv, blob, off, sz, fk, fp = _oracle.stream_inputs(5151, 6000, 0, 300, True)
+    pub, sig = ed25519.sign_batch(prv, blob, off, sz)
+    for i in np.nonzero(fk)[0]:
+        byte, bit = divmod(int(fp[i]), 8)
+        sig[i, byte % 64] ^= 1 << bit
+    msgs = [bytes(blob[off[i]:off[i] + sz[i]]) for i in range(len(sz))]
+    verdict = _oracle.verify_batch(_golden.Batch(pub, sig, off, sz, blob))
+    halves = [np.arange(0, 3000), np.arange(3000, 6000)]
+    feeds = [_feed(pub, sig, msgs, o, 4096) for o in halves]
+    outs = [tango.mcache_new(4096) for _ in halves]
+    tiles = [tango.VerifyTile(0, batch_max=1024, tcache_depth=1 << 12) for _ in halves]
+    res = [None, None]
+
+    def go(k):
+        res[k] = tiles[k].run(feeds[k][0], feeds[k][1], 0, outs[k], 0, len(halves[k]))
+
+    try:
+        th = [threading.Thread(target=go, args=(k,)) for k in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=100)
+        assert not any(t.is_alive() for t in th)
+    finally:
+        for t in tiles:
+            t.close()
+    for k, order in enumerate(halves):
+        diag, _ = res[k]
+        exp, ha, sv = _model(pub, sig, msgs, order, verdict, 1 << 12)
+        assert diag["out_cnt"] == len(exp) and diag["sv_filt_cnt"] == sv and diag["ha_filt_cnt"] == ha
+        assert [int(outs[k][o]["sig"]) for o in range(len(exp))] == [tg for _, tg in exp]
