@@ -824,6 +824,45 @@ quad_cached_row( p3 const & u, u64 m1, u64 m2 ) {
   return r;
 }
 
+/* -A and its odd multiples as cached rows on a quad (k_dsm4, k_dsm8):
+   lane q computes row q ([Z, Y-X, Y+X, 2dT]) of every entry and,
+   when wr, writes it to the signature's Ai slab Ail; the same ops as
+   ge_to_cached / ge_dbl / ge_add (k_ai), so the same limbs. */
+__device__ __forceinline__ void
+ai_table_quad( bool act, bool wr, int qd, u64 m1, u64 m2, i32 const * __restrict__ Aw, size_t N, u32 ii,
+               i32 * __restrict__ Ail ) {
+  p3 A;
+  _Pragma("unroll") for( int k=0; k<10; k++ ) {
+    A.X.v[k] = act ? Aw[(size_t)(k   )*N + ii] : 0;
+    A.Y.v[k] = act ? Aw[(size_t)(10+k)*N + ii] : (k==0);
+    A.T.v[k] = act ? Aw[(size_t)(20+k)*N + ii] : 0;
+    A.Z.v[k] = (k==0);
+  }
+  fe row = quad_cached_row( A, m1, m2 );
+# define AI_ROW4( e ) do {                                                          \
+    int4 * d_ = (int4 *)(Ail + (e)*48 + qd*12);                                     \
+    d_[0] = make_int4( row.v[0], row.v[1], row.v[2], row.v[3] );                   \
+    d_[1] = make_int4( row.v[4], row.v[5], row.v[6], row.v[7] );                   \
+    d_[2] = make_int4( row.v[8], row.v[9], 0, 0 );                                 \
+  } while(0)
+  if( wr ) AI_ROW4( 0 );
+  u64 const all = ~0UL, none = 0UL;
+  p1p1 t; fe z0 = fe_zero();
+  quad_body( t, A, z0, all, none, m1, m2 );            /* DBL(A) */
+  p3 A2; quad_p3( A2, t, m1, m2 );
+  for( int e=0; e<7; e++ ) {
+    fe R0, R1, R2, R3;
+    qgather( row, R0, R1, R2, R3 );                    /* rows Z, Y-X, Y+X, 2dT of entry e */
+    fe br;
+    _Pragma("unroll") for( int k=0; k<10; k++ ) br.v[k] = q4( m1, m2, R2.v[k], R1.v[k], R0.v[k], R3.v[k] );
+    quad_body( t, A2, br, none, none, m1, m2 );        /* A2 + Ai[e] */
+    p3 u; quad_p3( u, t, m1, m2 );
+    row = quad_cached_row( u, m1, m2 );
+    if( wr ) AI_ROW4( e+1 );
+  }
+# undef AI_ROW4
+}
+
 __global__ void __launch_bounds__(64)
 k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats, i8 * __restrict__ out ) {
   /* the base-point table in the Ai slab's row layout (see k_dsm8) */
@@ -855,39 +894,7 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
   u64 const m1 = __builtin_amdgcn_ballot_w64( qd & 1 ), m2 = __builtin_amdgcn_ballot_w64( qd & 2 );
 
   /* -A and its odd multiples (cached rows; lane q writes row q) */
-  {
-    p3 A;
-    i32 const * Aw = (i32 const *)(ws + L.A);
-    _Pragma("unroll") for( int k=0; k<10; k++ ) {
-      A.X.v[k] = act ? Aw[(size_t)(k   )*N + ii] : 0;
-      A.Y.v[k] = act ? Aw[(size_t)(10+k)*N + ii] : (k==0);
-      A.T.v[k] = act ? Aw[(size_t)(20+k)*N + ii] : 0;
-      A.Z.v[k] = (k==0);
-    }
-    fe row = quad_cached_row( A, m1, m2 );
-#   define AI_ROW4( e ) do {                                                        \
-      int4 * d_ = (int4 *)(Ail + (e)*48 + qd*12);                                   \
-      d_[0] = make_int4( row.v[0], row.v[1], row.v[2], row.v[3] );                 \
-      d_[1] = make_int4( row.v[4], row.v[5], row.v[6], row.v[7] );                 \
-      d_[2] = make_int4( row.v[8], row.v[9], 0, 0 );                               \
-    } while(0)
-    if( act ) AI_ROW4( 0 );
-    u64 const all = ~0UL, none = 0UL;
-    p1p1 t; fe z0 = fe_zero();
-    quad_body( t, A, z0, all, none, m1, m2 );            /* DBL(A) */
-    p3 A2; quad_p3( A2, t, m1, m2 );
-    for( int e=0; e<7; e++ ) {
-      fe R0, R1, R2, R3;
-      qgather( row, R0, R1, R2, R3 );                    /* rows Z, Y-X, Y+X, 2dT of entry e */
-      fe br;
-      _Pragma("unroll") for( int k=0; k<10; k++ ) br.v[k] = q4( m1, m2, R2.v[k], R1.v[k], R0.v[k], R3.v[k] );
-      quad_body( t, A2, br, none, none, m1, m2 );        /* A2 + Ai[e] */
-      p3 u; quad_p3( u, t, m1, m2 );
-      row = quad_cached_row( u, m1, m2 );
-      if( act ) AI_ROW4( e+1 );
-    }
-#   undef AI_ROW4
-  }
+  ai_table_quad( act, act, qd, m1, m2, (i32 const *)(ws + L.A), N, ii, Ail );
 
   u64 const * dg = (u64 const *)(ws + L.dig) + (size_t)ii*32u;
   int p   = act ? ((int const *)(ws + L.top))[ii] : -1;
@@ -1167,40 +1174,8 @@ dsm8_body( u32 gt, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout
   u64 const m1 = __builtin_amdgcn_ballot_w64( qd & 1 ), m2 = __builtin_amdgcn_ballot_w64( qd & 2 );
   half_t const H = half_ctx( hh );
 
-  /* -A and its odd multiples (cached rows; lane q writes row q) */
-  {
-    p3 A;
-    i32 const * Aw = (i32 const *)(ws + L.A);
-    _Pragma("unroll") for( int k=0; k<10; k++ ) {
-      A.X.v[k] = act ? Aw[(size_t)(k   )*N + ii] : 0;
-      A.Y.v[k] = act ? Aw[(size_t)(10+k)*N + ii] : (k==0);
-      A.T.v[k] = act ? Aw[(size_t)(20+k)*N + ii] : 0;
-      A.Z.v[k] = (k==0);
-    }
-    fe row = quad_cached_row( A, m1, m2 );
-#   define AI_ROW4( e ) do {                                                        \
-      int4 * d_ = (int4 *)(Ail + (e)*48 + qd*12);                                   \
-      d_[0] = make_int4( row.v[0], row.v[1], row.v[2], row.v[3] );                 \
-      d_[1] = make_int4( row.v[4], row.v[5], row.v[6], row.v[7] );                 \
-      d_[2] = make_int4( row.v[8], row.v[9], 0, 0 );                               \
-    } while(0)
-    if( act && !hh ) AI_ROW4( 0 );
-    u64 const all = ~0UL, none = 0UL;
-    p1p1 t; fe z0 = fe_zero();
-    quad_body( t, A, z0, all, none, m1, m2 );            /* DBL(A) */
-    p3 A2; quad_p3( A2, t, m1, m2 );
-    for( int e=0; e<7; e++ ) {
-      fe R0, R1, R2, R3;
-      qgather( row, R0, R1, R2, R3 );                    /* rows Z, Y-X, Y+X, 2dT of entry e */
-      fe br;
-      _Pragma("unroll") for( int k=0; k<10; k++ ) br.v[k] = q4( m1, m2, R2.v[k], R1.v[k], R0.v[k], R3.v[k] );
-      quad_body( t, A2, br, none, none, m1, m2 );        /* A2 + Ai[e] */
-      p3 u; quad_p3( u, t, m1, m2 );
-      row = quad_cached_row( u, m1, m2 );
-      if( act && !hh ) AI_ROW4( e+1 );
-    }
-#   undef AI_ROW4
-  }
+  /* -A and its odd multiples (cached rows; lane q writes row q, the h = 0 half) */
+  ai_table_quad( act, act && !hh, qd, m1, m2, (i32 const *)(ws + L.A), N, ii, Ail );
 
   u64 const * dg = (u64 const *)(ws + L.dig) + (size_t)ii*32u;
   int p   = act ? ((int const *)(ws + L.top))[ii] : -1;

@@ -112,7 +112,9 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    (tags remembered, 0 disables).
 
    GPU side (PUB_SIG_MSG framing): ONE persistent kernel per run
-   (k_tile_persist) holds every wave slot of the GPU and verifies what the
+   (k_tile_persist) holds its share of the GPU's wave slots (8 x CUs over
+   the tiles that exist on the device: create a GPU's tiles before running
+   any; FD_AMD_TILE_WAVES sets the count) and verifies what the
    tile's host thread hands over through mapped host memory -- ring entries
    (frag chunk, output frame, size) and chunk descriptors -- on one stream,
    so it needs one hardware queue (HIP's default GPU_MAX_HW_QUEUES = 4 is
