@@ -99,8 +99,9 @@ class VerifyTile:
         if rc:
             raise ed25519.EngineError("fd_verify_amd_tile_register_dcache rc=%d" % rc)
 
-    def run(self, in_mcache, in_chunk0, in_seq0, out_mcache, out_seq0, frag_cnt, lat_max=0):
-        """Consume frag_cnt input frags; returns (diag dict, latency samples).
+    def run(self, in_mcache, in_chunk0, in_seq0, out_mcache, out_seq0, frag_cnt, lat_max=0, stop=None):
+        """Consume frag_cnt input frags (frag_cnt 0: until stop, a ctypes.c_int
+        another thread sets nonzero); returns (diag dict, latency samples).
         self.in_fseq holds the tile's final producer credit."""
         diag = (ctypes.c_ulong * len(DIAG_FIELDS))()
         lat = np.zeros(max(lat_max, 1), np.uint32)
@@ -108,7 +109,8 @@ class VerifyTile:
         vp = ctypes.c_void_p
         rc = ed25519.lib().fd_verify_amd_tile_run(
             self._h, vp(in_mcache.ctypes.data), in_mcache.size, vp(in_chunk0.ctypes.data), int(in_seq0),
-            ctypes.byref(fseq), vp(out_mcache.ctypes.data), out_mcache.size, int(out_seq0), None, int(frag_cnt), None,
+            ctypes.byref(fseq), vp(out_mcache.ctypes.data), out_mcache.size, int(out_seq0), None, int(frag_cnt),
+            ctypes.byref(stop) if stop is not None else None,
             ctypes.byref(diag), vp(lat.ctypes.data) if lat_max else None, int(lat_max))
         if rc:
             raise ed25519.EngineError("fd_verify_amd_tile_run rc=%d" % rc)

@@ -329,3 +329,59 @@ def test_two_tiles_share_one_gpu():
         exp, ha, sv = _model(pub, sig, msgs, order, verdict, 1 << 12)
         assert diag["out_cnt"] == len(exp) and diag["sv_filt_cnt"] == sv and diag["ha_filt_cnt"] == ha
         assert [int(outs[k][o]["sig"]) for o in range(len(exp))] == [tg for _, tg in exp]
+
+
+@pytest.mark.parametrize("zero_copy", [False, True])
+def test_tile_runs_until_stop_and_continues(zero_copy):
+    """The deployment shape: a run with frag_cnt 0 lasts until another
+    thread raises *stop (the reference's cnc halt), publishing everything it
+    took in; a second run on the same tile continues the input and output
+    sequences (its kernel's tickets restart at the tile's descriptor count)
+    and publishes the rest in order."""
+    import ctypes
+    import threading
+    import time
+    from firedancer_amd import ed25519, tango
+    prv, blob, off, sz, fk, fp = _oracle.stream_inputs(6262, 3000, 0, 300, True)
+    pub, sig = ed25519.sign_batch(prv, blob, off, sz)
+    for i in np.nonzero(fk)[0]:
+        byte, bit = divmod(int(fp[i]), 8)
+        sig[i, byte % 64] ^= 1 << bit
+    msgs = [bytes(blob[off[i]:off[i] + sz[i]]) for i in range(len(sz))]
+    verdict = _oracle.verify_batch(_golden.Batch(pub, sig, off, sz, blob))
+    order = np.arange(len(msgs))
+    mc_in, dc, _, _, _ = _feed(pub, sig, msgs, order, 4096)
+    mc_out = tango.mcache_new(4096)
+    exp, ha, sv = _model(pub, sig, msgs, order, verdict, 0)
+    first = 1800                                   # frags the first run takes in
+    n_first = sum(1 for s_in, _ in exp if s_in < first)
+    tile = tango.VerifyTile(0, batch_max=512, tcache_depth=0)
+    if zero_copy:
+        tile.register_dcache(dc)
+    try:
+        # run 1: only the first `first` frags are visible to it (the later
+        # lines still read "never published"), stop once they are out
+        mc_hide = tango.mcache_new(4096)
+        mc_hide[:first] = mc_in[:first]
+        stop = ctypes.c_int(0)
+
+        def halt():
+            t0 = time.time()
+            while time.time() - t0 < 60:
+                if int(mc_out[(n_first - 1) % 4096]["seq"]) == n_first - 1:
+                    break
+                time.sleep(0.001)
+            stop.value = 1
+        th = threading.Thread(target=halt)
+        th.start()
+        d1, _ = tile.run(mc_hide, dc, 0, mc_out, 0, 0, stop=stop)
+        th.join()
+        assert d1["in_cnt"] == first and d1["out_cnt"] == n_first
+        # run 2: the rest, sequences continued
+        d2, _ = tile.run(mc_in, dc, first, mc_out, n_first, len(order) - first)
+        assert d2["out_cnt"] == len(exp) - n_first
+    finally:
+        tile.close()
+    assert d1["sv_filt_cnt"] + d2["sv_filt_cnt"] == sv and tile.in_fseq == len(order)
+    assert [int(mc_out[o]["seq"]) for o in range(len(exp))] == list(range(len(exp)))
+    assert [int(mc_out[o]["sig"]) for o in range(len(exp))] == [t for _, t in exp]
