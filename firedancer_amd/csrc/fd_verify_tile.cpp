@@ -106,9 +106,10 @@ struct tcache_t {
 
 struct pending_t {            /* one staged / in-flight frag */
   ulong  seq;                 /* input sequence number */
-  ulong  frame;               /* output frame reservation (monotonic; frame = frame % frame_cnt) */
+  ulong  frame;               /* output frame reservation (monotonic) */
   ushort sz, ctl;
   uint   tsorig;
+  uint   fidx;                /* frame % frame_cnt (kept incrementally: no division per frag) */
 };
 
 inline ulong mono_ns( void ) {
@@ -177,6 +178,7 @@ struct fd_verify_amd_tile {
   ulong              frame_cnt;
   std::vector<ulong> frame_pub;  /* out seq of the frag a frame last carried (FRAME_FREE: none) */
   ulong              frame_next, frame_retired;
+  ulong              frame_next_idx;   /* frame_next % frame_cnt */
   ulong              out_seq_end;   /* out seq after the last run's last publish (a run continuing it keeps frame_pub) */
   tile_slot_t        ts[FD_AMD_SLOT_MAX];
   /* persistent consumer (PUB_SIG_MSG framing, k_tile_persist) */
@@ -494,7 +496,7 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
      other out_seq0 starts a new session (a new consumer), with every frame
      free. */
   if( out_seq0 != t->out_seq_end ) std::fill( t->frame_pub.begin(), t->frame_pub.end(), FRAME_FREE );
-  t->frame_next = t->frame_retired = 0UL;
+  t->frame_next = t->frame_retired = t->frame_next_idx = 0UL;
 
   /* zero copy: the input data region is mapped into the GPU; frags are
      handed over as (chunk, size) and copied on the device.  zc_lim: bytes
@@ -564,7 +566,7 @@ tile_run_batched( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
           do out_cr = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) + out_depth; while( (long)(out_seq - out_cr) >= 0 );
         }
       }
-      ulong f = m.frame % F;
+      ulong f = m.fidx;
       t->frame_pub[f] = out_seq;
       uint tspub = fd_verify_amd_tickcount();
       fd_mcache_publish( out_mcache, out_depth, out_seq, tag, f * FRAME_CHUNKS, m.sz, m.ctl, m.tsorig, tspub );
@@ -615,7 +617,7 @@ tile_run_batched( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       }
       /* reserve the next output frame: not staged or in flight, and no
          longer read by a consumer that honours flow control */
-      ulong fr = t->frame_next, f = fr % F;
+      ulong fr = t->frame_next, f = t->frame_next_idx;
       if( fr - t->frame_retired >= F ) { full = true; break; }
       if( out_fseq && t->frame_pub[f] != FRAME_FREE && (long)(t->frame_pub[f] - cons) >= 0 ) {
         cons = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE );
@@ -644,11 +646,12 @@ tile_run_batched( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       if( (!txn || k2) && t->tc.insert( ha_tag ) ) { diag->ha_filt_cnt++; diag->ha_filt_sz += sz; continue; }
       t->frame_pub[f] = FRAME_FREE;
       t->frame_next++;
+      if( ++t->frame_next_idx == F ) t->frame_next_idx = 0UL;
       ts.ich[staged] = zc_dev ? (uint32_t)chunk : (uint32_t)(f * FRAME_CHUNKS);
       ts.fsz[staged] = (uint32_t)sz;
       ts.tb[staged]  = (uint32_t)slots;
       slots += k2;
-      ts.pend[staged] = pending_t{ in_seq - 1UL, fr, (ushort)sz, (ushort)ctl, (uint)tsorig };
+      ts.pend[staged] = pending_t{ in_seq - 1UL, fr, (ushort)sz, (ushort)ctl, (uint)tsorig, (uint)f };
       if( !staged ) { stage_t0 = now_ns(); ts.seq_lo = in_seq - 1UL; }
       staged++;
     }
@@ -843,7 +846,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
             } while( (long)(out_seq - out_cr) >= 0 );
           }
         }
-        ulong f = m.frame % F;
+        ulong f = m.fidx;
         t->frame_pub[f] = out_seq;
         fd_mcache_publish( out_mcache, out_depth, out_seq, tag, f * FRAME_CHUNKS, m.sz, m.ctl, m.tsorig, tspub );
         if( lat && lat_n < lat_max ) lat[lat_n++] = tspub - m.tsorig;
@@ -880,7 +883,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       }
       /* reserve the next output frame: not in flight, and no longer read
          by a consumer that honours flow control */
-      ulong fr = t->frame_next, f = fr % F;
+      ulong fr = t->frame_next, f = t->frame_next_idx;
       if( fr - t->frame_retired >= F ) { full = true; break; }
       if( out_fseq && t->frame_pub[f] != FRAME_FREE && (long)(t->frame_pub[f] - cons) >= 0 ) {
         cons = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE );
@@ -903,11 +906,12 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       }
       t->frame_pub[f] = FRAME_FREE;
       t->frame_next++;
+      if( ++t->frame_next_idx == F ) t->frame_next_idx = 0UL;
       fd_amd_tile_ent_t * en = t->ring + (staged & mask);
       en->src_chunk = zc_dev ? (uint32_t)chunk : (uint32_t)(f * FRAME_CHUNKS);
       en->out_chunk = (uint32_t)(f * FRAME_CHUNKS);
       en->sz        = (uint32_t)sz;
-      t->ppend[staged & mask] = pending_t{ in_seq - 1UL, fr, (ushort)sz, (ushort)ctl, (uint)tsorig };
+      t->ppend[staged & mask] = pending_t{ in_seq - 1UL, fr, (ushort)sz, (ushort)ctl, (uint)tsorig, (uint)f };
       if( staged == handed ) hand_t0 = now_ns();
       staged++; progress = true;
     }
@@ -1152,7 +1156,8 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
     ulong p0 = now_ns(), cr = 0;   /* cr: first seq not covered by the cached credit */
     uint  tnow = 0;                /* saturated: one timestamp per 32 frags (the producer must outrun the tile) */
     ulong lim = writes ? std::min( depth, D ) : depth;
-    for( ulong seq=0; seq<frag_cnt; seq++ ) {
+    ulong k = 0, fw = 0;           /* seq % pool_n, seq % D, kept incrementally (no division per frag) */
+    for( ulong seq=0; seq<frag_cnt; seq++, k = (k + 1UL == pool_n) ? 0UL : k + 1UL, fw = (fw + 1UL == D) ? 0UL : fw + 1UL ) {
       ulong due = rate > 0.0 ? p0 + (ulong)((double)seq * 1e9 / rate) : 0UL;   /* paced: open loop */
       if( due ) {
         ulong tn;
@@ -1163,8 +1168,8 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
          of a frag the tile still reads is reused; refreshed only when the
          cached credit runs out */
       if( !lap ) while( seq >= cr ) cr = __atomic_load_n( &in_fseq, __ATOMIC_ACQUIRE ) + lim;
-      ulong k = seq % pool_n, sz = 96UL + msg_sz[k];
-      ulong fr = writes ? seq % D : k;
+      ulong sz = 96UL + msg_sz[k];
+      ulong fr = writes ? fw : k;
       if( writes ) put_frame( dcache + fr * frame, k );
       /* tsorig = the scheduled send time when paced, so producer stalls
          count as latency; the input seq when lapping (the check needs it) */
@@ -1176,7 +1181,7 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   std::thread cons( [&]() {
     pin_to( 2 );
     ulong seq = 0, fseq = 0;   /* fseq: last value published to out_fseq (every 64 frags, or when idle) */
-    ulong exp_s = 0;           /* check: next input seq that should be published */
+    ulong exp_s = 0, exp_k = 0; /* check: next input seq that should be published, and seq % pool_n */
     long  last = -1;
     ulong tl = 0;              /* when the previous frag was seen */
     for( ;; ) {
@@ -1184,16 +1189,17 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
       if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) == seq ) {
         if( !(seq & 15UL) ) { ulong tn = now_ns(); if( tl ) gap_max = std::max( gap_max, tn - tl ); tl = tn; }
         if( check ) {
-          ulong tag = m->sig, chunk = m->chunk, sz = m->sz, s_in;
+          ulong tag = m->sig, chunk = m->chunk, sz = m->sz, s_in, k;
           if( lap ) {
             s_in = m->tsorig;
             if( (long)s_in <= last ) mism++;
+            k = s_in % pool_n;
           } else {
-            while( exp_s < frag_cnt && expect_err[exp_s % pool_n] ) exp_s++;
-            s_in = exp_s++;
+            while( exp_s < frag_cnt && expect_err[exp_k] ) { exp_s++; exp_k = (exp_k + 1UL == pool_n) ? 0UL : exp_k + 1UL; }
+            s_in = exp_s++; k = exp_k;
+            exp_k = (exp_k + 1UL == pool_n) ? 0UL : exp_k + 1UL;
           }
           last = (long)s_in;
-          ulong k = s_in % pool_n;
           uchar const * q = out_chunk0 + (chunk << FD_CHUNK_LG_SZ);
           bool ok = s_in < frag_cnt && !expect_err[k] && tag == expect_tag[k] && sz == 96UL + msg_sz[k];
           if( ok && !(checked & byte_mask) )
