@@ -215,8 +215,9 @@ def dsm_roofline(st, kernel_ms, n, kernel="k_dsm", note=None):
     traffic = [pmc_traffic(k, n) for k in kernel.split("+")] if "(" not in kernel else [None]
     r = {"bound": "valu-imad64", "kernel": kernel, "achieved": achieved, "peak": PEAK_TMAC, "unit": "TMAC/s",
          "frac": achieved / PEAK_TMAC, "traffic": None if None in traffic else sum(traffic),
-         "traffic_note": "HBM bytes per launch from the committed PMC pass (profiles/r02_pmc_latest.json: "
-                         "2*FETCH_SIZE+WRITE_SIZE KB, gfx950 correction), scaled to this batch",
+         "traffic_note": "HBM bytes per launch from the committed PMC pass (profiles/%s: "
+                         "2*FETCH_SIZE+WRITE_SIZE KB, gfx950 correction), scaled to this batch"
+                         % os.path.basename(pmc_summary_path() or "none"),
          "mac_per_sig": mac / max(live, 1.0)}
     if note:
         r["note"] = note
@@ -235,15 +236,22 @@ def dsm_in_pipeline(st, ms_per_step, stage_ms, n):
                     "duration"}
 
 
+def pmc_summary_path():
+    """The newest round's committed PMC summary (profiles/rNN_pmc_latest.json)."""
+    for r in ("r03", "r02", "r01"):
+        path = os.path.join(ROOT, "profiles", r + "_pmc_latest.json")
+        if os.path.exists(path):
+            return path
+    return None
+
+
 def pmc_traffic(kernel, n):
     """HBM bytes per launch of `kernel` at batch n, from the PMC summary
     committed under profiles/ (tools/prof_pmc.sh + tools/pmc_summary.py on
     the same build), scaled linearly from the profiled batch size."""
-    path = os.path.join(ROOT, "profiles", "r02_pmc_latest.json")
-    if not os.path.exists(path):
-        path = os.path.join(ROOT, "profiles", "r01_pmc_latest.json")
+    path = pmc_summary_path()
     try:
-        d = json.load(open(path))
+        d = json.load(open(path or ""))
         b = d[kernel]["derived"]["hbm_bytes_per_launch"]
         return b * n / d.get("_sigs_per_launch", 262144)
     except (OSError, KeyError, ValueError):
