@@ -1741,8 +1741,6 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
 #else
   (void)w;
 #endif
-#ifdef FD_POOL_DEBUG
-#endif
 }
 
 #ifdef FD_POOL_DEBUG
