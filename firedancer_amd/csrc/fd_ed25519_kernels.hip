@@ -1451,9 +1451,13 @@ pool_store_ts( PTR s, u32 stride, p1p1 const & t ) {
 }
 
 /* a pure DBL step is chosen while its lane count is at least this percentage
-   of a mixed step's (the measured cost ratio of the two steps) */
+   of a mixed step's.  100: only a full DBL step (64 lanes) beats a mixed one.
+   The steps' cost ratio (~0.72) was the round-2 setting (78); a model of the
+   pool's op streams and an interleaved A/B both favour 100: ADD slots wait
+   less, so fewer signatures sit in the pool with nothing but an ADD to do
+   (DSM stage -1 to -2 %, profiles/r03_pool_tune_ab.txt) */
 #ifndef FD_POOL_DBL_PCT
-#define FD_POOL_DBL_PCT 78u
+#define FD_POOL_DBL_PCT 100u
 #endif
 /* free slots that trigger a refill (one counter atomic + init loads) */
 #ifndef FD_POOL_REFILL
@@ -1582,8 +1586,7 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
          or a MIXED step (k_dsm's uniform 8-mul step) that takes every ADD
          slot first and fills the rest with DBL slots.  An ADD op costs the
          same in either, so ADDs always go through mixed steps; a DBL step
-         wins while it is nearly as full as a mixed one (cost ratio ~0.78,
-         measured). */
+         runs only when it fills the wave (FD_POOL_DBL_PCT 100). */
       mixed = 100u * kD < FD_POOL_DBL_PCT * kM;
       nsel = mixed ? kM : kD;
       /* owner view: the rank of my slots in the selection order [ADD slots
