@@ -8,7 +8,7 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 import numpy as np  # noqa: E402
 from firedancer_amd import ed25519, workload  # noqa: E402
 
