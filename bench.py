@@ -364,13 +364,37 @@ def run_txn(args, rank, world, dist):
 
 # ---------------------------------------------------------------- configs[4]
 
-def stream_rows(local, pub, sig, off, sz, blob, args):
+# decompression work per signature (k_decomp's bodies: two points, each
+# pow22523 = 250 squares + 11 muls, plus ~9 more muls and 4 squares), in the
+# same MAC units as the double-scalar multiply
+MAC_DECOMP = 2 * (254 * MAC_SQ + 20 * MAC_MUL)
+
+
+def _lat_parts(r):
+    """The tile's per-frag latency decomposition (fd_verify_amd_tile_set_trace), us."""
+    us = lambda k: r[k] / 1e3  # noqa: E731
+    return {"cut_wait": [us("cut_p50_ns"), us("cut_p99_ns")], "queue_wait": [us("queue_p50_ns"), us("queue_p99_ns")],
+            "service": [us("service_p50_ns"), us("service_p99_ns")],
+            "publish_wait": [us("publish_p50_ns"), us("publish_p99_ns")],
+            "input_wait": [us("input_p50_ns"), us("input_p99_ns")],
+            "service_p50_latency_chunks": us("service_lat_chunk_p50_ns"),
+            "service_p50_throughput_chunks": us("service_thr_chunk_p50_ns"),
+            "chunks": {"latency": int(r["gpu_chunks_lat"]), "throughput": int(r["gpu_chunks_thr"])},
+            "mode_switches": int(r["mode_switches"]),
+            "note": "[p50, p99] us per published frag: staged -> handed over (cut), -> a wave claimed the chunk "
+                    "(queue), -> results stored (service, GPU clock mapped onto the host's), -> published "
+                    "(in-order wait + poll); input = producer publish -> staged"}
+
+
+def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1, dist=None):
     """config 5: tango mcache/dcache feed -> verify tile -> consumer, per
     batch cap, copy and zero-copy staging.  The pool carries 10 % corrupted
-    frags (one message bit each: full verify cost, verdict -3); the
-    consumer checks every published frag against the batch engine's
-    verdicts and the SHA-512 tags (verdict, tag and order of every frag;
-    the bytes in the tile's output dcache of every 16th)."""
+    frags (one message bit each: full verify cost, verdict -3); saturated
+    runs check every published frag against the batch engine's verdicts and
+    the SHA-512 tags (verdict, tag and order of every frag; the bytes in the
+    tile's output dcache of every 16th); paced runs (50 % / 80 % of the
+    row's saturated rate, and a fixed 1 M frags/s) measure latency and its
+    decomposition."""
     from firedancer_amd import ed25519, tango
     m = min(pub.shape[0], 1 << 16)
     p_pub, p_sig, p_sz = pub[:m], sig[:m], sz[:m]
@@ -386,40 +410,174 @@ def stream_rows(local, pub, sig, off, sz, blob, args):
     p_tag = np.array([int.from_bytes(hashlib.sha512(bytes(p_sig[i][:32]) + bytes(p_pub[i]) +
                                                     bytes(p_blob[p_off[i]:p_off[i] + p_sz[i]])).digest()[:8],
                                      "little") for i in range(m)], np.uint64)
+    pool = (p_pub, p_sig, p_off, p_sz, p_blob)
+
+    def paced(bmax, zc, rate):
+        nf = int(min(args.stream_frags, max(20000, rate * 1.0)))
+        r = tango.bench_stream(local, bmax, 0, *pool, nf, rate=rate, zero_copy=zc)
+        return {"offered_frags_per_s": rate, "frags_per_s": r["frags_per_s"], "p50_us": r["p50_ns"] / 1e3,
+                "p99_us": r["p99_ns"] / 1e3, "p99_over_p50": r["p99_ns"] / max(r["p50_ns"], 1.0),
+                "mean_chunk": r["mean_batch"], "sv_filt": int(r["sv_filt"]),
+                "decomposition": _lat_parts(r),
+                "stalls_us": {"producer_late_max": r["producer_late_max_ns"] / 1e3,
+                              "tile_pass_max": r["tile_pass_max_ns"] / 1e3,
+                              "consumer_gap_max": r["consumer_gap_max_ns"] / 1e3}}
+
     rows = []
-    for bmax in (256, 1024, 4096, 16384):
+    bmaxes = (256, 1024, 4096, 16384) if world == 1 else (16384,)
+    for bmax in bmaxes:
         row = {"batch_max": bmax}
-        for zc in (False, True):
+        for zc in (False, True) if world == 1 else (True,):
             key = "zero_copy" if zc else "copy"
-            kw = dict(zero_copy=zc, expect_err=p_err, expect_tag=p_tag, sample_bytes=True)
-            sat = tango.bench_stream(local, bmax, 0, p_pub, p_sig, p_off, p_sz, p_blob, args.stream_frags, **kw)
-            rr = {"saturated_frags_per_s": sat["frags_per_s"], "saturated_mean_batch": sat["mean_batch"],
+            sat = tango.bench_stream(local, bmax, 0, *pool, args.stream_frags, zero_copy=zc, expect_err=p_err,
+                                     expect_tag=p_tag, sample_bytes=True)
+            rr = {"saturated_frags_per_s": sat["frags_per_s"], "saturated_mean_chunk": sat["mean_batch"],
                   "published": int(sat["published"]), "sv_filt": int(sat["sv_filt"]), "ovrn": int(sat["ovrn"]),
                   "check_mismatches": int(sat["mismatches"]), "checked": int(sat["checked"])}
+            if mac_per_sig:
+                a = sat["frags_per_s"] * (mac_per_sig + MAC_DECOMP) / 1e12
+                rr["roofline"] = {"achieved": a, "peak": PEAK_TMAC, "unit": "TMAC/s", "frac": a / PEAK_TMAC,
+                                  "mac_per_frag": mac_per_sig + MAC_DECOMP,
+                                  "note": "saturated frags/s x (DSM MACs per signature of the resident batch + "
+                                          "decompression's %d) vs the integer-multiply peak" % MAC_DECOMP}
             for load in (0.5, 0.8):
-                rate = load * sat["frags_per_s"]
-                nf = int(min(args.stream_frags, max(20000, rate * 1.0)))
-                r = tango.bench_stream(local, bmax, 0, p_pub, p_sig, p_off, p_sz, p_blob, nf, rate=rate, **kw)
-                rr["at_%d%%" % int(load * 100)] = {"offered_frags_per_s": rate, "frags_per_s": r["frags_per_s"],
-                                                    "p50_us": r["p50_ns"] / 1e3, "p99_us": r["p99_ns"] / 1e3,
-                                                    "mean_batch": r["mean_batch"], "sv_filt": int(r["sv_filt"]),
-                                                    "check_mismatches": int(r["mismatches"]),
-                                                    "stalls_us": {"producer_late_max": r["producer_late_max_ns"] / 1e3,
-                                                                  "tile_pass_max": r["tile_pass_max_ns"] / 1e3,
-                                                                  "consumer_gap_max": r["consumer_gap_max_ns"] / 1e3}}
+                rr["at_%d%%" % int(load * 100)] = paced(bmax, zc, load * sat["frags_per_s"])
+            lo, hi = rr["at_50%"], rr["at_80%"]
+            rr["p50_nondecreasing_with_load"] = hi["p50_us"] >= lo["p50_us"]
+            rr["p99_within_2_5x_p50"] = max(lo["p99_over_p50"], hi["p99_over_p50"]) <= 2.5
             row[key] = rr
         rows.append(row)
-    return {"path": "producer (metadata only; frames pre-placed in the data region as a NIC would) -> in "
-                    "mcache/dcache -> verify tile (one persistent GPU kernel fed through mapped ring/descriptor "
-                    "memory, load-adaptive chunks; copy: frag copied into the tile's output dcache and released; "
-                    "zero_copy: GPU copies from the mapped input region, input released when the frag is "
-                    "published) -> out mcache + tile-owned out dcache -> consumer (checks "
-                    "verdict, tag and order of every frag, bytes of every 16th); latency = scheduled send to tile publish",
-            "pool": "%d signatures of %d B, %d with one message bit flipped" % (m, int(p_sz[0]), bad.size),
-            "frags_per_run": args.stream_frags,
-            "all_checks_pass": all(r[k]["check_mismatches"] == 0 and r[k]["at_50%"]["check_mismatches"] == 0 and
-                                   r[k]["at_80%"]["check_mismatches"] == 0 for r in rows for k in ("copy", "zero_copy")),
-            "rows": rows}
+    fixed = {}
+    if world == 1:
+        for zc in (False, True):
+            fixed["zero_copy" if zc else "copy"] = paced(4096, zc, 1e6)
+    allr = [r[k] for r in rows for k in ("copy", "zero_copy") if k in r]
+    out = {"path": "producer (metadata only; frames pre-placed in the data region as a NIC would) -> in "
+                   "mcache/dcache -> verify tile (one persistent GPU kernel fed through mapped ring/descriptor "
+                   "memory; latency chunks of 8 frags below the rate switch, 64-frag chunks above; copy: frag copied "
+                   "into the tile's output dcache and released; zero_copy: GPU copies from the mapped input region, "
+                   "input released when the frag is published; a second host thread publishes) -> out mcache + "
+                   "tile-owned out dcache -> consumer (saturated runs check verdict, tag and order of every frag, "
+                   "bytes of every 16th); latency = scheduled send to tile publish",
+           "pool": "%d signatures of %d B, %d with one message bit flipped" % (m, int(p_sz[0]), bad.size),
+           "frags_per_run": args.stream_frags,
+           "all_checks_pass": all(r["check_mismatches"] == 0 for r in allr),
+           "every_row_p99_within_2_5x_p50": all(r["p99_within_2_5x_p50"] for r in allr),
+           "every_row_p50_nondecreasing_with_load": all(r["p50_nondecreasing_with_load"] for r in allr),
+           "rows": rows}
+    if fixed:
+        out["fixed_1M_frags_per_s_batch_max_4096"] = fixed
+    return out
+
+
+def _txn_first_tag(p):
+    """SHA-512 tag of a wire transaction's first signature: R = signature 0,
+    A = account address 0, M = the message (fd_txn.h layout; the synthetic
+    transactions have < 128 accounts, so every compact-u16 is one byte)."""
+    m = 1 + 64 * p[0]
+    a = m + (1 if p[m] & 0x80 else 0) + 4
+    return int.from_bytes(hashlib.sha512(bytes(p[1:33]) + bytes(p[a:a + 32]) + bytes(p[m:])).digest()[:8], "little")
+
+
+def txn_stream_row(local, args):
+    """configs[3]'s frames through the tile (TXN framing, its batch path):
+    GPU-signed multi-signer transactions, 10 % with a corrupted signature
+    byte, saturated (every published transaction checked: verdict, first
+    signature's tag, bytes of every 16th, order) and at half load."""
+    from firedancer_amd import ed25519, tango, workload
+    payload, toff, tsz, _ = workload.txn_batch(1 << 17, 777)
+    payload = payload.copy()
+    rng = np.random.default_rng(56)
+    bad = rng.choice(toff.size, toff.size // 10, replace=False)
+    for t in bad:
+        payload[int(toff[t]) + 1 + int(rng.integers(0, 64))] ^= 1 << int(rng.integers(0, 8))
+    eng = ed25519.Engine(device=local, batch_max=1 << 16, blob_max=payload.size + 64)
+    terr = eng.verify_txns(payload, toff, tsz)
+    eng.close()
+    tag = np.array([_txn_first_tag(payload[int(o):int(o) + int(z)]) for o, z in zip(toff, tsz)], np.uint64)
+    zpub, zsig = np.zeros((toff.size, 32), np.uint8), np.zeros((toff.size, 64), np.uint8)
+    pool = (zpub, zsig, toff, tsz, payload)
+    nf = args.stream_frags // 4
+    sat = tango.bench_stream(local, 4096, 0, *pool, nf, zero_copy=True, txn=True, expect_err=terr, expect_tag=tag,
+                             sample_bytes=True)
+    half = tango.bench_stream(local, 4096, 0, *pool, int(min(nf, max(20000, 0.5 * sat["frags_per_s"]))),
+                              rate=0.5 * sat["frags_per_s"], zero_copy=True, txn=True)
+    sigs_per_txn = float(ed25519.txn_slots(payload, toff, tsz)[1]) / toff.size
+    return {"path": "TXN framing (wire transactions, multi-signer; the tile's batch path: parse, verify, reduce per "
+                    "batch, 4 batches in flight), batch_max 4096, zero copy",
+            "pool": "%d transactions, %.2f signatures each, %d with a flipped signature bit" % (toff.size, sigs_per_txn,
+                                                                                              bad.size),
+            "saturated_txns_per_s": sat["frags_per_s"], "saturated_verifies_per_s": sat["frags_per_s"] * sigs_per_txn,
+            "check_mismatches": int(sat["mismatches"]), "checked": int(sat["checked"]),
+            "published": int(sat["published"]), "sv_filt": int(sat["sv_filt"]),
+            "at_50%": {"offered_txns_per_s": 0.5 * sat["frags_per_s"], "p50_us": half["p50_ns"] / 1e3,
+                       "p99_us": half["p99_ns"] / 1e3}}
+
+
+def stream_node(local, pub, sig, off, sz, blob, args, rank, world, dist):
+    """N GPUs, the reference's scaling unit (N verify tiles, one per
+    input link: fd_frank_init:67-80, fd_frank_main.c:118-143): every rank
+    runs its own tile on its own GPU at batch_max 16384, zero copy, all at
+    once -- saturated, then at half its own saturated rate -- with its
+    host threads on its GPU's NUMA node (ranks that share a node split its
+    CPUs).  Rank 0 reports the node sum."""
+    import torch
+    from firedancer_amd import hip, tango
+    from firedancer_amd.shard import cpu_slice, max_over_ranks, peer_slot
+    from firedancer_amd import ed25519
+    ndev = max(1, hip.device_count())
+    keys = [None] * world
+    dist.all_gather_object(keys, {"numa": ed25519.device_numa_node(local), "dev": local % ndev})
+    k, n = peer_slot([x["numa"] for x in keys], rank)
+    saved = os.sched_getaffinity(0)
+    cpus = cpu_slice(saved, k, n) if n > 1 else sorted(saved)
+    if len(cpus) >= 5:
+        os.sched_setaffinity(0, cpus)
+    _, share = peer_slot([x["dev"] for x in keys], rank)
+    waves = 0
+    if share > 1:   # rehearsal: ranks mapped onto one GPU split its wave slots
+        cus = ctypes_cus(local)
+        waves = 8 * cus // share
+    m = min(pub.shape[0], 1 << 16)
+    p_off = (off[:m] - off[0]).astype(np.uint32)
+    pool = (pub[:m], sig[:m], p_off, sz[:m], blob[off[0]:off[0] + int(p_off[-1]) + int(sz[m - 1])].copy())
+    nf = 4 * args.stream_frags
+    res = []
+    try:
+        dist.barrier()
+        t0 = time.perf_counter()
+        sat = tango.bench_stream(local, 16384, 0, *pool, nf, zero_copy=True, waves=waves)
+        span_sat = max_over_ranks(time.perf_counter() - t0)
+        dist.barrier()
+        rate = 0.5 * sat["frags_per_s"]
+        half = tango.bench_stream(local, 16384, 0, *pool, int(min(nf, max(20000, rate))), rate=rate, zero_copy=True,
+                                  waves=waves)
+        res = [sat["frags_per_s"], half["frags_per_s"], half["p50_ns"] / 1e3, half["p99_ns"] / 1e3, float(len(cpus)),
+               float(waves)]
+    finally:
+        os.sched_setaffinity(0, saved)
+    t = torch.zeros(world * len(res), dtype=torch.float64)
+    t[rank * len(res):(rank + 1) * len(res)] = torch.tensor(res, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    per = t.view(world, len(res)).tolist()
+    return {"ranks": world, "batch_max": 16384, "staging": "zero_copy",
+            "saturated_frags_per_s_node": sum(r[0] for r in per),
+            "saturated_run_span_s_max": span_sat,
+            "at_50%_frags_per_s_node": sum(r[1] for r in per),
+            "per_rank": [{"saturated_frags_per_s": r[0], "at_50%": {"frags_per_s": r[1], "p50_us": r[2], "p99_us": r[3]},
+                          "cpus": int(r[4]), "waves": int(r[5]), "numa_node": keys[i]["numa"], "device": keys[i]["dev"]}
+                         for i, r in enumerate(per)],
+            "note": "every rank's tile runs at once (barrier before each run); node value = sum of the ranks' rates"}
+
+
+def ctypes_cus(device):
+    import ctypes
+    from firedancer_amd import hip
+    v = ctypes.c_int(0)
+    H = hip.hip()
+    if H.hipDeviceGetAttribute(ctypes.byref(v), 63, int(device)) != 0 or v.value <= 0:   # MultiprocessorCount
+        return 256
+    return v.value
 
 
 # ---------------------------------------------------------------- multi-engine
@@ -617,6 +775,10 @@ def main():
                             "of each chunk's planes and message window, no host copy -> kernels; rank bound to its "
                             "GPU's NUMA node; value = all ranks' signatures / max-over-ranks time"}
 
+    node_tile = None
+    if world > 1 and not args.no_stream:
+        node_tile = stream_node(local, pub, sig, off, sz, blob, args, rank, world, dist)
+
     if rank != 0:
         return
     total = n * args.steps * world
@@ -718,7 +880,10 @@ def main():
             out["host_soa_registered"] = {"verifies_per_s": host_fed["verifies_per_s"] / world,
                                           "note": "rank 0's share of host_fed_node (every rank ran it at once)"}
     if world == 1 and not args.no_stream:
-        out["stream_tile"] = stream_rows(local, pub, sig, off, sz, blob, args)
+        out["stream_tile"] = stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=out["roofline"]["mac_per_sig"])
+        out["stream_tile"]["txn_framing"] = txn_stream_row(local, args)
+    if node_tile:
+        out["stream_tile_node"] = node_tile
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(pub, sig, off, sz, blob, args.cpu_sample, args.cpu_threads, err,
                                            args.cpu_seconds)

@@ -4,6 +4,9 @@
 
 Outputs:
     firedancer_amd/libfd_ed25519_amd.so   the product: HIP kernels + C-ABI
+    firedancer_amd/libfd_ed25519_amd_diag.so  (python -m firedancer_amd.build --diag) the same plus the
+                                          FD_AMD_DIAG measurement aids (k_tile_synth, the pool's and the
+                                          tile kernel's clocks) -- tools only, never the product
     oracle/liboracle.so                   CPU restatement (checker only)
     oracle/_ref/libfdref.so               the reference's own sources, compiled
                                           (only when /root/reference exists)
@@ -12,11 +15,13 @@ import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "firedancer_amd")
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libfd_ed25519_amd.so")
+LIB_DIAG = os.path.join(PKG, "libfd_ed25519_amd_diag.so")
 ARCH = os.environ.get("FD_AMD_ARCH", "gfx950")
 
 SOURCES = ["fd_ed25519_kernels.hip", "fd_txn_kernels.hip", "fd_ed25519_sign.hip", "fd_ed25519_engine.cpp", "fd_ed25519_multi.cpp", "fd_ed25519_host.cpp",
@@ -40,6 +45,8 @@ def _stale(out, deps):
 
 
 def build_engine(force=False, verbose=False, out=None, defines=()):
+    """Compile every source to an object in parallel (one hipcc per file),
+    then link the shared library."""
     consts = os.path.join(CSRC, "fd_ed25519_consts.h")
     gen = os.path.join(ROOT, "tools", "gen_consts.py")
     if force or _stale(consts, [gen]):
@@ -48,15 +55,33 @@ def build_engine(force=False, verbose=False, out=None, defines=()):
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [consts]
     if not force and not defines and not _stale(lib, deps):
         return lib
-    cmd = [_hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-o", lib + ".tmp"] + ["-D" + d for d in defines]
-    cmd += [os.path.join(CSRC, s) for s in SOURCES]
-    cmd += ["-lpthread"]
+    objdir = os.path.join(PKG, "_obj", os.path.basename(lib).replace(".so", ""))
+    os.makedirs(objdir, exist_ok=True)
+    base = [_hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+    base += ["-D" + d for d in defines]
+    objs = [os.path.join(objdir, s + ".o") for s in SOURCES]
+
+    def cc(k):
+        cmd = base + ["-c", os.path.join(CSRC, SOURCES[k]), "-o", objs[k]]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd, cwd=CSRC)
+
+    with ThreadPoolExecutor(max_workers=min(len(SOURCES), max(1, min(8, os.cpu_count() or 1)))) as ex:
+        list(ex.map(cc, range(len(SOURCES))))
+    cmd = [_hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib + ".tmp"] + objs + ["-lpthread"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd, cwd=CSRC)
     os.replace(lib + ".tmp", lib)
     return lib
+
+
+def build_diag(force=False, verbose=False):
+    """The diagnostics library (FD_AMD_DIAG): tools load it through FD_AMD_LIB."""
+    if not force and not _stale(LIB_DIAG, [os.path.join(CSRC, s) for s in SOURCES + HEADERS]):
+        return LIB_DIAG
+    return build_engine(force=True, verbose=verbose, out=LIB_DIAG, defines=("FD_AMD_DIAG",))
 
 
 def build_oracle(verbose=False):
@@ -90,7 +115,9 @@ def build(force=False, verbose=False):
 
 if __name__ == "__main__":
     # python -m firedancer_amd.build [--force] [--variant OUT.so DEF1,DEF2]  (A/B experiment builds)
-    if "--variant" in sys.argv:
+    if "--diag" in sys.argv:
+        print(build_diag(force="--force" in sys.argv, verbose=True))
+    elif "--variant" in sys.argv:
         k = sys.argv.index("--variant")
         out, defs = sys.argv[k + 1], [d for d in sys.argv[k + 2].split(",") if d]
         print(build_engine(force=True, verbose=True, out=os.path.abspath(out), defines=defs))

@@ -87,11 +87,15 @@ typedef struct { uint64_t first; uint32_t count; uint32_t pad; } fd_amd_tile_des
    per instruction (whole lines) -- interleaved 8-B stores into mapped host
    memory held the L2 so long that every wave of the GPU slowed ~5x
    (tools/tile_synth.py, profiles/r03_tile_persist_ab.txt). */
-/* host-written control words, each on its own 64-B line */
+/* control words in mapped host memory, each on its own 64-B line: the
+   first three are written by the host, the last by the GPU's scout */
 typedef struct {
   uint64_t head;  uint64_t pad0[7];   /* chunk descriptors [.., head) are published to the GPU */
   uint64_t beat;  uint64_t pad1[7];   /* host heartbeat: the kernel's watchdog */
   uint32_t stop;  uint32_t kerr;  uint64_t pad2[7];   /* stop: exit once drained; kerr: set by the kernel on a watchdog exit */
+  uint64_t gclock;                    /* scout: its s_memrealtime (100 MHz), every ~10 us; nonzero = the kernel started */
+  uint64_t gdone;                     /* scout: chunks the waves finished (mirror of dctl->done) */
+  uint64_t pad3[6];
 } fd_amd_tile_hctl_t;
 /* device control block (zeroed by the host before each launch) */
 #define FD_AMD_TILE_MIRRORS (8)
@@ -99,8 +103,9 @@ typedef struct { uint64_t w; uint64_t pad[7]; } fd_amd_tile_mirror_t;
 typedef struct {
   uint64_t             ticket;  uint64_t pad0[7];   /* next chunk ticket (one atomic add per chunk) */
   fd_amd_tile_mirror_t mw[FD_AMD_TILE_MIRRORS];     /* per XCD: descriptor head | heartbeat << 48 | err << 62 | stop << 63 */
+  uint64_t             done;    uint64_t pad1[7];   /* chunks finished (one atomic add per chunk; the scout mirrors it) */
   uint64_t             stat[4];                     /* chunks in latency mode, in throughput mode; frags in each */
-  uint64_t             prof[8];                     /* debug (args.prof): summed ticks gather, front, DSM, results, wait, fence */
+  uint64_t             prof[8];                     /* diagnostics build (FD_AMD_DIAG, args.prof): summed ticks gather, front, DSM, results, wait, fence */
 } fd_amd_tile_dctl_t;
 typedef struct {
   fd_amd_tile_hctl_t *       hctl;     /* device address of the mapped control words */
@@ -108,20 +113,24 @@ typedef struct {
   fd_amd_tile_desc_t const * desc;     /* device address of the mapped chunk descriptors (same size as the ring) */
   uint64_t *                 res_tag;  /* device address of the mapped results: tags */
   uint64_t *                 res_word; /*   and verdict words */
+  uint64_t *                 res_time; /*   and (NULL = none) per frag: claim | done << 32, low 32 bits of the
+                                            s_memrealtime ticks when its wave took the chunk and stored its results */
   uint64_t                   mask;     /* ring size - 1 (power of 2) */
   uint8_t const *            src;      /* frag source region (mapped): input dcache (zero-copy) or the output frames */
   uint8_t *                  out;      /* output frames (mapped) to fill, or NULL (copy mode: the host filled them) */
   fd_amd_tile_dctl_t *       dctl;
   uint8_t *                  scratch;  /* per-wave scratch, fd_amd_tile_scratch_stride() bytes apart */
   uint64_t                   watchdog; /* s_memrealtime ticks (100 MHz) without a host heartbeat before the kernel gives up */
-  uint32_t                   prof;     /* debug: sum per-phase time stamps into dctl->prof */
+  uint32_t                   prof;     /* diagnostics build only: sum per-phase time stamps into dctl->prof */
 } fd_amd_tile_args_t;
 size_t fd_amd_tile_scratch_stride( void );
 /* waves: grid size (wave 0 is the scout that mirrors the host words) */
 int fd_amd_launch_tile_persist( fd_amd_tile_args_t const * a, uint32_t waves, hipStream_t stream );
 
-/* measurement aid: the chunk pipeline alone, every argument in device memory */
+#ifdef FD_AMD_DIAG
+/* diagnostics build: the chunk pipeline alone, every argument in device memory */
 int fd_amd_launch_tile_synth( fd_amd_tile_args_t const * a, uint32_t waves, uint32_t iters, int eight, hipStream_t stream );
+#endif
 
 /* Dense slide digits of the last call on workspace d_ws (debug): u16
    [n][256] (low byte h digit, high byte s digit) rebuilt from the event

@@ -1327,7 +1327,7 @@ enum { OP_D = 0, OP_AA = 1, OP_AB = 2, OP_EMPTY = 3, OP_NONE = 4 };
    [Z = 1 | Y-X | Y+X | 2dT] x 12 limbs (10 used), so ADD-A and ADD-B load
    their operand with the same code from different bases */
 __device__ i32 g_bi12[8][48];
-#ifdef FD_POOL_DEBUG
+#ifdef FD_AMD_DIAG
 __device__ u32 g_pool_dbg[4];   /* steps, live lanes, ADD steps, refill-only steps (summed over waves) */
 __device__ u64 g_pool_dbg_t[8192][4];   /* per wave: wall_clock64 at start, at exhaustion of the counter, at exit; steps after exhaustion | lanes << 32 */
 #endif
@@ -1491,7 +1491,7 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
   u64 const valid1 = (P >= 128u) ? ~0UL : ((1UL << (P - 64u)) - 1UL);   /* slots 64.. that exist */
 
   u64 mD0 = 0, mD1 = 0, mA0 = 0, mA1 = 0;
-#ifdef FD_POOL_DEBUG
+#ifdef FD_AMD_DIAG
   u64 dbg_t0 = wall_clock64(), dbg_te = 0; bool dbg_after = false; u64 dbg_sa = 0, dbg_la = 0;
 #endif
   u32 * ctr = (u32 *)(ws + L.ctr);   /* next unclaimed signature, shared by all waves */
@@ -1504,7 +1504,7 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
   u64 iter_max = ((u64)n + 2u*P) * 448u;
   if( iter_cap < iter_max ) iter_max = iter_cap;
   bool guard = true;
-#ifdef FD_POOL_DEBUG
+#ifdef FD_AMD_DIAG
   u32 dbg_steps = 0, dbg_lanes = 0, dbg_add = 0, dbg_idle = 0;
 #endif
   for( u64 iter = 0; iter < iter_max; iter++ ) {
@@ -1515,7 +1515,7 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
     /* refill in batches (one global round trip per 16 finished signatures),
        or whenever no class fills a wave */
     if( more && nfree && (nfree >= FD_POOL_REFILL || (nD < 64u && nA < 64u)) ) {
-#ifdef FD_POOL_DEBUG
+#ifdef FD_AMD_DIAG
       dbg_idle++;
 #endif
       /* claim nfree signatures (one vector atomic; faster waves claim more,
@@ -1525,7 +1525,7 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
       base = (u32)__builtin_amdgcn_readfirstlane( (int)base );
       if( base + nfree >= n || base + nfree < base ) {
         more = false;
-#ifdef FD_POOL_DEBUG
+#ifdef FD_AMD_DIAG
         dbg_te = wall_clock64(); dbg_after = true;
 #endif
       }
@@ -1604,7 +1604,7 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
     }
     bool in0 = __builtin_amdgcn_inverse_ballot_w64( S0 ), in1 = __builtin_amdgcn_inverse_ballot_w64( S1 );
     mA0 &= ~S0; mA1 &= ~S1; mD0 &= ~S0; mD1 &= ~S1;
-#ifdef FD_POOL_DEBUG
+#ifdef FD_AMD_DIAG
     dbg_steps++; dbg_lanes += nsel; dbg_add += mixed;
     if( dbg_after ) { dbg_sa++; dbg_la += nsel; }
 #endif
@@ -1738,7 +1738,7 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
     mD1 |= S1 & d1; mA1 |= S1 & x1 & ~d1;
   }
   if( guard && l == 0u ) atomicOr( (u32 *)(ws + L.ctr) + 1, 1u );
-#ifdef FD_POOL_DEBUG
+#ifdef FD_AMD_DIAG
   if( l == 0u ) { atomicAdd( &g_pool_dbg[0], dbg_steps ); atomicAdd( &g_pool_dbg[1], dbg_lanes ); atomicAdd( &g_pool_dbg[2], dbg_add ); atomicAdd( &g_pool_dbg[3], dbg_idle ); }
   if( l == 0u && w < 8192u ) { g_pool_dbg_t[w][0] = dbg_t0; g_pool_dbg_t[w][1] = dbg_te; g_pool_dbg_t[w][2] = wall_clock64(); g_pool_dbg_t[w][3] = dbg_sa | (dbg_la << 32); }
 #else
@@ -1746,7 +1746,7 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
 #endif
 }
 
-#ifdef FD_POOL_DEBUG
+#ifdef FD_AMD_DIAG
 extern "C" int
 fd_amd_pool_debug( unsigned * out, int reset ) {
   if( hipMemcpyFromSymbol( out, HIP_SYMBOL( g_pool_dbg ), sizeof(unsigned)*4 ) != hipSuccess ) return -1;
@@ -1909,15 +1909,25 @@ __host__ __device__ constexpr tile_scratch_t tile_scratch_layout( void ) {
 
 size_t fd_amd_tile_scratch_stride( void ) { return tile_scratch_layout().total; }
 
-/* The scout (wave 0, lane 0): host words -> the XCDs' mirror words. */
+/* The scout (wave 0, lane 0): host words -> the XCDs' mirror words, and
+   back to the host every ~10 us its clock (the host maps the waves' time
+   stamps onto its own clock with it; its first store tells the host the
+   kernel started) and the count of finished chunks (the host's progress
+   watchdog). */
 __device__ __noinline__ void
 tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog ) {
   u64 word = ld_dev64( &D->mw[0].w ), lastb = ~0UL, beat = 0UL;
-  u64 tb = __builtin_amdgcn_s_memrealtime(), tpub = tb;
+  u64 tb = __builtin_amdgcn_s_memrealtime(), tpub = tb, tclk = tb;
+  st_sys64( &H->gclock, tb );
   for( ;; ) {
     u64 h = ld_sys64( &H->head ), b = ld_sys64( &H->beat );
     u32 st = ld_sys32( &H->stop );
     u64 now = __builtin_amdgcn_s_memrealtime();
+    if( now - tclk >= 1000UL ) {
+      tclk = now;
+      st_sys64( &H->gdone, ld_dev64( &D->done ) );
+      st_sys64( &H->gclock, now );
+    }
     if( b != lastb ) { lastb = b; tb = now; }
     bool dead = now - tb > watchdog;
     if( dead ) st_sys32( &H->kerr, 1u );
@@ -1934,14 +1944,20 @@ tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog ) {
   }
 }
 
-/* Verify ring entries [c0, c0 + k) (k <= 64) on this wave. */
+/* Verify ring entries [c0, c0 + k) (k <= 64) on this wave, claimed at
+   s_memrealtime tc. */
 __device__ __forceinline__ void
 tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __restrict__ scr, ws_layout_t L,
-            tile_scratch_t const & S, i32 (* __restrict__ bi)[48], u64 (* __restrict__ evl)[33], u64 * pt ) {
-  /* pt (debug, A.prof): s_memrealtime ticks spent in gather, prep + decomp,
-     DSM, results; wave-uniform values */
+            tile_scratch_t const & S, i32 (* __restrict__ bi)[48], u64 (* __restrict__ evl)[33], u64 * pt, u64 tc ) {
+#ifdef FD_AMD_DIAG
+  /* pt (diagnostics build, A.prof): s_memrealtime ticks spent in gather,
+     prep + decomp, DSM, results; wave-uniform values */
   u64 ts = A.prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
 # define TILE_STAMP( k_ ) do { if( A.prof ) { u64 t_ = __builtin_amdgcn_s_memrealtime(); if( !threadIdx.x ) pt[k_] += t_ - ts; ts = t_; } } while(0)
+#else
+  (void)pt;
+# define TILE_STAMP( k_ ) do { } while(0)
+#endif
   /* opaque per chunk: otherwise the compiler hoists every per-lane address
      of the bodies out of the persistent loop and spills them */
   {
@@ -2008,6 +2024,7 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __rest
         system-scope release, then the words the host polls */
   u64 const idx = c0 + l, j = idx & A.mask;
   if( l < k ) st_sys64( A.res_tag + j, ((u64 const *)(ws + L.tag))[l] );
+  if( A.res_time && l < k ) st_sys64( A.res_time + j, (u64)(u32)tc | ((u64)(u32)__builtin_amdgcn_s_memrealtime() << 32) );
   __builtin_amdgcn_fence( __ATOMIC_RELEASE, "" );
   asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
   u64 const wd = ((idx + 1UL) << 8) | (u64)(u8)err[l];
@@ -2035,11 +2052,16 @@ k_tile_persist( fd_amd_tile_args_t A ) {
   u64 const * mw = &D->mw[xcc].w;
   u8 * scr = A.scratch + (size_t)blockIdx.x * S.total;
   /* per-wave tallies in LDS, not registers (the DSM bodies want every VGPR):
-     [0..7] debug (A.prof) gather, front, DSM, results, wait, fence, -, -;
-     [8..11] latency chunks, throughput chunks, their frags */
+     [0..7] diagnostics build (A.prof) gather, front, DSM, results, wait,
+     fence, -, -; [8..11] latency chunks, throughput chunks, their frags */
   __shared__ u64 s_tally[12];
   if( l < 12u ) s_tally[l] = 0UL;
   u64 * const pt = s_tally;
+#ifdef FD_AMD_DIAG
+  bool const prof = A.prof != 0u;
+#else
+  constexpr bool prof = false;
+#endif
   for( ;; ) {
     u64 t = 0;
     if( l == 0u ) t = atomicAdd( (unsigned long long *)&D->ticket, 1ULL );
@@ -2059,8 +2081,9 @@ k_tile_persist( fd_amd_tile_args_t A ) {
       u32 const nap = d < 2UL ? 1u : d < 64UL ? (u32)d : 64u;
       for( u32 z = 0; z < nap; z++ ) __builtin_amdgcn_s_sleep( 4 );
     }
-    if( A.prof && !l ) pt[4] += __builtin_amdgcn_s_memrealtime() - t0;
+    if( prof && !l ) pt[4] += __builtin_amdgcn_s_memrealtime() - t0;
     if( !go ) break;
+    u64 const tc = __builtin_amdgcn_s_memrealtime();   /* claimed */
     /* descriptor t (host memory): { first ring index, count | latency mode << 31 } */
     u64 c = 0, cm = 0;
     if( l == 0u ) {
@@ -2072,20 +2095,24 @@ k_tile_persist( fd_amd_tile_args_t A ) {
     bool const e8 = ((u32)cm >> 31) != 0u;
     /* the frames were written by the host (copy mode) or the producer
        (zero-copy) into host memory: drop this CU's stale lines first */
-    u64 const tf = A.prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
+    u64 const tf = prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
     __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "" );
     asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
-    if( A.prof && !l ) pt[5] += __builtin_amdgcn_s_memrealtime() - tf;
-    if( take && take <= 64u ) tile_chunk( A, c, take, e8, scr, L, S, bi, evl, pt );
-    if( !l ) { s_tally[e8 ? 8 : 9] += 1UL; s_tally[e8 ? 10 : 11] += take; }
+    if( prof && !l ) pt[5] += __builtin_amdgcn_s_memrealtime() - tf;
+    if( take && take <= 64u ) tile_chunk( A, c, take, e8, scr, L, S, bi, evl, pt, tc );
+    if( !l ) {
+      s_tally[e8 ? 8 : 9] += 1UL; s_tally[e8 ? 10 : 11] += take;
+      atomicAdd( (unsigned long long *)&D->done, 1ULL );   /* progress, mirrored to the host by the scout */
+    }
   }
   if( l == 0u ) {
     _Pragma("unroll") for( int q=0; q<4; q++ ) atomicAdd( (unsigned long long *)&D->stat[q], (unsigned long long)s_tally[8 + q] );
-    if( A.prof ) { _Pragma("unroll") for( int q=0; q<8; q++ ) atomicAdd( (unsigned long long *)&D->prof[q], (unsigned long long)pt[q] ); }
+    if( prof ) { _Pragma("unroll") for( int q=0; q<8; q++ ) atomicAdd( (unsigned long long *)&D->prof[q], (unsigned long long)pt[q] ); }
   }
 }
 
-/* Measurement aid: k_tile_persist's chunk pipeline without the host
+#ifdef FD_AMD_DIAG
+/* Diagnostics build only.  Measurement aid: k_tile_persist's chunk pipeline without the host
    hand-off (no tickets, no polling, nothing in mapped memory): wave w runs
    `iters` chunks of k ring entries, [(w iters + it) k, +k), with every
    argument in device memory (fd_amd_tile_synth, tools/tile_synth.py). */
@@ -2116,7 +2143,7 @@ k_tile_synth( fd_amd_tile_args_t A, u32 iters, u32 eight ) {
   }
   u8 * scr = A.scratch + (size_t)blockIdx.x * S.total;
   for( u32 it = 0; it < iters; it++ )
-    tile_chunk( A, ((u64)blockIdx.x * iters + it) * k, k, eight != 0u, scr, L, S, bi, evl, pt );
+    tile_chunk( A, ((u64)blockIdx.x * iters + it) * k, k, eight != 0u, scr, L, S, bi, evl, pt, 0UL );
   if( A.hctl && threadIdx.x == 0u ) atomicAdd( (unsigned long long *)&A.dctl->stat[0], 1ULL );
 }
 
@@ -2126,6 +2153,7 @@ fd_amd_launch_tile_synth( fd_amd_tile_args_t const * a, uint32_t waves, uint32_t
   hipLaunchKernelGGL( k_tile_synth, dim3(waves), dim3(64), 0, stream, *a, iters, (u32)(eight != 0) );
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+#endif /* FD_AMD_DIAG */
 
 int
 fd_amd_launch_tile_persist( fd_amd_tile_args_t const * a, uint32_t waves, hipStream_t stream ) {
@@ -2225,7 +2253,7 @@ pool_waves( u32 n ) {
     cus = v;
   }
   u32 wmax = 8u * (u32)cus;
-#ifdef FD_POOL_DEBUG
+#ifdef FD_AMD_DIAG
   if( char const * e = getenv( "FD_POOL_WAVES" ) ) { u32 v = (u32)atoi( e ); if( v ) wmax = v; }
 #endif
   u32 want = (n + 63u) / 64u;

@@ -86,6 +86,18 @@ def lib():
     L.fd_ed25519_amd_debug_set_pool_iter_cap.restype = None
     L.fd_verify_amd_tile_new.argtypes = [i, ul, ul, ul, ul]
     L.fd_verify_amd_tile_new.restype = vp
+    L.fd_verify_amd_tile_cfg_default.argtypes = [vp]
+    L.fd_verify_amd_tile_cfg_default.restype = None
+    L.fd_verify_amd_tile_new_cfg.argtypes = [vp]
+    L.fd_verify_amd_tile_new_cfg.restype = vp
+    L.fd_verify_amd_tile_set_trace.argtypes = [vp, vp, ul]
+    L.fd_verify_amd_tile_set_trace.restype = None
+    L.fd_verify_amd_tile_set_verdict_log.argtypes = [vp, vp, ul]
+    L.fd_verify_amd_tile_set_verdict_log.restype = None
+    L.fd_verify_amd_tile_cut.argtypes = [vp, ul, ul, ul, i, ul, i]
+    L.fd_verify_amd_tile_cut.restype = ul
+    L.fd_verify_amd_tile_mode.argtypes = [i, i, ctypes.c_double, ctypes.c_double, ctypes.c_double]
+    L.fd_verify_amd_tile_mode.restype = i
     L.fd_verify_amd_tile_out_chunk0.argtypes = [vp]
     L.fd_verify_amd_tile_out_chunk0.restype = vp
     L.fd_verify_amd_tile_out_data_sz.argtypes = [vp]
@@ -121,7 +133,7 @@ def lib():
     L.fd_verify_amd_tickcount.argtypes = []
     L.fd_verify_amd_tickcount.restype = ui
     L.fd_verify_amd_bench_stream.argtypes = [i, ul, ul, ctypes.c_double, i, ul, ul, vp, vp, vp, vp, vp, vp, vp, ul,
-                                             vp]
+                                             ul, vp]
     L.fd_verify_amd_bench_stream.restype = i
     _lib = L
     return L

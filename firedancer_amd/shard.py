@@ -83,3 +83,21 @@ def bind_to_device_node(device, sysfs="/sys"):
         os.sched_setaffinity(0, want)
         out["cpus"] = len(want)
     return out
+
+
+def peer_slot(keys, rank):
+    """Among the ranks whose key equals keys[rank] (e.g. the same NUMA node,
+    or the same GPU): (this rank's index among them, how many there are)."""
+    mine = keys[rank]
+    same = [r for r, k in enumerate(keys) if k == mine]
+    return same.index(rank), len(same)
+
+
+def cpu_slice(cpus, k, n):
+    """The k-th of n contiguous, disjoint slices of the sorted CPU list (the
+    spinning threads of ranks that share a NUMA node must not share CPUs)."""
+    cpus = sorted(cpus)
+    if n < 1 or not (0 <= k < n):
+        raise ValueError("bad slice %r of %r" % (k, n))
+    per = len(cpus) // n
+    return cpus[k * per:(k + 1) * per]

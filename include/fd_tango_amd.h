@@ -104,46 +104,105 @@ typedef struct {
   ulong gpu_chunk_thr_cnt;   /* ... 1 lane per signature (throughput mode) */
   ulong gpu_frag_lat_cnt;    /* frags in those chunks */
   ulong gpu_frag_thr_cnt;
+  ulong sv_filt_code_cnt[3]; /* SV_FILT by verdict: FD_ED25519_ERR_SIG, _PUBKEY, _MSG (PUB_SIG_MSG framing) */
+  ulong halt_drop_cnt;       /* frags taken in but neither published nor filtered: the run halted (*stop) while
+                                its output stayed backpressured past the halt grace */
+  ulong mode_switch_cnt;     /* persistent path: switches between latency and throughput chunks */
 } fd_verify_amd_diag_t;
 
 typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
 
-/* A tile bound to HIP device `device`.  tcache_depth: HA dedup window
-   (tags remembered, 0 disables).
+/* Tile configuration (fd_verify_amd_tile_new_cfg).  Fill it with
+   fd_verify_amd_tile_cfg_default, then change what differs.
 
    GPU side (PUB_SIG_MSG framing): ONE persistent kernel per run
-   (k_tile_persist) holds its share of the GPU's wave slots (8 x CUs over
-   the tiles that exist on the device: create a GPU's tiles before running
-   any; FD_AMD_TILE_WAVES sets the count) and verifies what the
-   tile's host thread hands over through mapped host memory -- ring entries
-   (frag chunk, output frame, size) and chunk descriptors -- on one stream,
-   so it needs one hardware queue (HIP's default GPU_MAX_HW_QUEUES = 4 is
-   enough) and the GPU never drains between hand-offs.  Hand-off rule
-   (adaptive): while fewer than 32 x CUs frags are in flight, everything
-   staged goes as soon as the input is momentarily drained, in chunks of up
-   to 8 frags verified 8 lanes per signature (latency); under load only
-   whole 64-frag chunks go, verified 1 lane per signature (throughput), a
-   partial one once its oldest frag waited 50 us.  batch_max: the most frags
-   staged before a hand-off is forced.  batch_wait_ns != 0 replaces
-   "drained" by "the oldest staged frag waited batch_wait_ns" while frags
-   are in flight.  At most 64 x batch_max (>= 2^13; 2^18 from batch_max
-   4096) frags are in flight.
+   (k_tile_persist) holds `waves` wave slots of the GPU while the run lasts
+   (0: 8 x CUs divided by the PUB_SIG_MSG tiles that exist on the device --
+   create a GPU's tiles before running any; tiles in different processes
+   set their share here) and verifies what the tile's host side hands over
+   through mapped host memory -- ring entries (frag chunk, output frame,
+   size) and chunk descriptors -- on one stream, so it needs one hardware
+   queue and the GPU never drains between hand-offs.  Its share must be
+   free when the run starts: a run whose kernel does not start within 2 s
+   (another kernel holds the slots) or stops making progress returns
+   FD_ED25519_AMD_ERR_DEVICE instead of waiting.
+
+   Chunks.  A chunk takes one wave whatever its size.  Latency chunks hold
+   up to 8 frags verified 8 lanes per signature (~0.45 ms on a SIMD of its
+   own); throughput chunks up to 64 frags, 1 lane per signature (~1.2 ms
+   alone, ~2.9 ms with every wave slot busy), 3-4x the frags per wave-ms.
+   chunk_mode AUTO picks by the staging rate (mean over ~0.4 ms): throughput
+   chunks above thr_rate_hi frags/s, latency chunks again below thr_rate_lo
+   (0: 55 % / 40 % of the latency chunks' capacity, min(waves, 4 x CUs) x
+   8 frags / 0.45 ms).  Whole chunks go at once; a partial latency chunk
+   goes once its oldest frag waited lat_fill_ns, or at once while fewer
+   than lat_free_chunks chunks are in flight; a partial throughput chunk
+   once its oldest waited chunk_wait_ns.  Everything staged goes at
+   batch_max staged frags, when the window or the output frames run out,
+   at the end of the input, and (batch_wait_ns != 0) once the oldest waited
+   batch_wait_ns.  At most `window` frags are in flight (handed over, not
+   yet published; 0: 64 x batch_max, >= 2^13, 2^18 from batch_max 4096).
    TXN framing uses the batch path: up to 4 batches in flight, each on its
    own stream (parse, verify, reduce per batch).
+
+   Host side.  The caller's thread polls, dedups and stages; publishing
+   runs on a second host thread when publish_cpu >= 0 (pinned there) or,
+   with FD_VERIFY_AMD_PUBLISH_AUTO, when the caller's CPU set holds another
+   CPU (the thread gets that set minus the caller's current CPU);
+   FD_VERIFY_AMD_PUBLISH_INLINE keeps both on the caller's thread.  After
+   *stop the run publishes what completes, for at most halt_grace_ns while
+   its output is backpressured, then returns (halt_drop_cnt).
 
    Output data region.  Like the reference verify tile, which publishes
    frags out of a dcache it owns (fd_frank_verify_synth_load.c:324,409-411),
    the tile owns its output dcache: out_frame_cnt frames of
-   FD_VERIFY_AMD_FRAME_SZ bytes (0: out_depth_hint + 5*batch_max, the
-   fd_dcache_req_data_sz rule with burst = the frags the tile holds staged
-   or in flight; out_depth_hint = 4096).  Every published frag's chunk is
-   relative to fd_verify_amd_tile_out_chunk0 and its bytes are the bytes
-   that were verified.  A frame is reused only once the consumer's out_fseq
-   has passed the frag it last carried (backpressure otherwise), so the
-   output never changes under a consumer that honours flow control.
-   NULL on failure. */
+   FD_VERIFY_AMD_FRAME_SZ bytes (0: 4096 + batch_max + the frags it can
+   hold in flight -- the PUB_SIG_MSG window, or 4 x batch_max for TXN
+   framing; pinned host memory, ~370 MB at the 2^18 window).  Every
+   published frag's chunk is relative to fd_verify_amd_tile_out_chunk0 and
+   its bytes are the bytes that were verified.  A frame is reused only once
+   the consumer's out_fseq has passed the frag it last carried
+   (backpressure otherwise), so the output never changes under a consumer
+   that honours flow control. */
 #define FD_VERIFY_AMD_FRAME_SZ (1408UL)   /* 22 chunks >= 96 + FD_ED25519_AMD_MSG_MAX */
 
+#define FD_VERIFY_AMD_CHUNK_AUTO       (0)
+#define FD_VERIFY_AMD_CHUNK_LATENCY    (1)   /* every chunk a latency chunk */
+#define FD_VERIFY_AMD_CHUNK_THROUGHPUT (2)   /* every chunk a throughput chunk */
+#define FD_VERIFY_AMD_PUBLISH_AUTO   (-2)
+#define FD_VERIFY_AMD_PUBLISH_INLINE (-1)
+
+typedef struct {
+  int   device;           /* HIP device */
+  int   framing;          /* FD_VERIFY_AMD_FRAMING_* (below) */
+  ulong batch_max;        /* 1 .. 2^20 */
+  ulong batch_wait_ns;
+  ulong tcache_depth;     /* HA dedup window (tags remembered, 0 disables) */
+  ulong out_frame_cnt;    /* 0: default */
+  ulong waves;            /* 0: the device's share */
+  int   chunk_mode;       /* FD_VERIFY_AMD_CHUNK_* */
+  int   publish_cpu;      /* FD_VERIFY_AMD_PUBLISH_AUTO / _INLINE, or a CPU */
+  ulong window;           /* 0: default */
+  ulong lat_fill_ns;
+  ulong lat_free_chunks;
+  ulong chunk_wait_ns;
+  ulong thr_rate_hi;      /* frags/s, 0: default */
+  ulong thr_rate_lo;
+  ulong halt_grace_ns;
+} fd_verify_amd_tile_cfg_t;
+
+/* Defaults: device 0, PUB_SIG_MSG, batch_max 4096, batch_wait_ns 0,
+   tcache_depth 2^16, out_frame_cnt 0, waves 0, AUTO chunks, AUTO
+   publisher, window 0, lat_fill_ns 20 us, lat_free_chunks CUs / 2,
+   chunk_wait_ns 50 us, thr rates 0, halt_grace_ns 50 ms. */
+void
+fd_verify_amd_tile_cfg_default( fd_verify_amd_tile_cfg_t * cfg );
+
+/* NULL on failure (bad configuration, no device, out of memory). */
+fd_verify_amd_tile_t *
+fd_verify_amd_tile_new_cfg( fd_verify_amd_tile_cfg_t const * cfg );
+
+/* The defaults with these five fields. */
 fd_verify_amd_tile_t *
 fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong tcache_depth, ulong out_frame_cnt );
 
@@ -190,7 +249,13 @@ int
 fd_verify_amd_tile_register_dcache( fd_verify_amd_tile_t * tile, void * base, ulong sz );
 
 /* Run the tile until `frag_cnt` input sequence numbers were consumed (0:
-   until *stop != 0) and every accepted frag is published.  Input:
+   until *stop != 0) and every accepted frag is published.  A raised *stop
+   (stop may be NULL when frag_cnt != 0) also ends a frag_cnt run; the run
+   then publishes what it took in, and returns at the latest halt_grace_ns
+   after the stop was seen even if the output is backpressured (the rest is
+   counted in halt_drop_cnt), the way the reference tile keeps its HALT
+   check running while backpressured (fd_frank_verify_synth_load.c:
+   223-274).  Input:
    in_mcache (depth in_depth, power of 2), in_chunk0 = local address of
    chunk 0 of the input data region (fd_chunk_to_laddr), first sequence
    number in_seq0.  in_fseq (NULL = none) receives the tile's flow-control
@@ -223,23 +288,46 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t *  tile,
 /* The tile's timestamp clock (tsorig/tspub units): nanoseconds on the
    CLOCK_MONOTONIC scale, low 32 bits (fd_frag_meta_ts_comp-style
    compression), read from the invariant TSC calibrated once against
-   CLOCK_MONOTONIC (the reference stamps frags with fd_tickcount;
-   FD_AMD_TILE_CLOCK=mono reads clock_gettime instead). */
+   CLOCK_MONOTONIC (the reference stamps frags with fd_tickcount). */
 uint
 fd_verify_amd_tickcount( void );
 
-/* The tile's hand-off rule (pure; what fd_verify_amd_tile_run applies to
-   its staged frags [handed, staged) with pubd the next frag to publish):
-   returns how far to hand over now; *lat_mode (may be NULL) = 1 for 8-frag
-   latency chunks (fewer than light_frags frags in flight), 0 for 64-frag
-   throughput chunks.  Latency mode hands over everything once idle_in (the
-   input is momentarily drained; with wait_ns != 0 only while nothing is in
-   flight); throughput mode whole 64-frag chunks, a remainder once
-   waited_ns >= chunk_wait_ns; both everything at batch_max staged, on full,
-   done_in, or waited_ns >= wait_ns != 0. */
+/* Per-frag latency decomposition of the next runs (persistent path):
+   parts[4 i .. 4 i + 3] for the i-th published frag (the same frags, in
+   the same order, as the run's lat samples), in ns: cut wait (staged ->
+   handed over), queue wait (handed over -> a wave claimed its chunk),
+   service (claimed -> results stored; bit 31 set for a latency chunk),
+   publish wait (results stored -> published: the in-order wait behind
+   older frags plus the host's poll).  GPU times are mapped onto the host
+   clock through the scout's clock word.  parts NULL stops tracing. */
+void
+fd_verify_amd_tile_set_trace( fd_verify_amd_tile_t * tile, uint * parts, ulong parts_max );
+
+/* Verdict log of the next runs (PUB_SIG_MSG framing): log[seq - in_seq0]
+   = the verdict (FD_ED25519_SUCCESS / ERR_*) of every input frag the GPU
+   verified whose run-relative sequence is below log_max; frags dropped
+   before verification (HA duplicates, bad frags, overruns) leave their
+   entry untouched.  log NULL stops logging. */
+void
+fd_verify_amd_tile_set_verdict_log( fd_verify_amd_tile_t * tile, schar * log, ulong log_max );
+
+/* The persistent path's hand-off rule (pure; what fd_verify_amd_tile_run
+   applies to its staged frags [handed, staged)): returns how far to hand
+   over now.  thr: throughput chunks (64 frags) else latency chunks (8).
+   Whole chunks go at once; a partial latency chunk once waited_ns (its
+   oldest frag's wait) >= lat_fill_ns or while chunks_in_flight <
+   lat_free_chunks; a partial throughput chunk once waited_ns >=
+   chunk_wait_ns; everything at batch_max staged, on flush (window or
+   frames ran out, end of input) or waited_ns >= batch_wait_ns != 0. */
 ulong
-fd_verify_amd_tile_cut( ulong staged, ulong handed, ulong pubd, ulong light_frags, ulong batch_max, ulong waited_ns,
-                        ulong wait_ns, ulong chunk_wait_ns, int idle_in, int full, int done_in, int * lat_mode );
+fd_verify_amd_tile_cut( fd_verify_amd_tile_cfg_t const * cfg, ulong staged, ulong handed, ulong chunks_in_flight,
+                        int thr, ulong waited_ns, int flush );
+
+/* The persistent path's chunk-mode rule (pure): 1 = throughput chunks.
+   AUTO: from latency chunks to throughput chunks when rate > rate_hi,
+   back when rate < rate_lo; the other modes are fixed. */
+int
+fd_verify_amd_tile_mode( int chunk_mode, int thr, double rate, double rate_hi, double rate_lo );
 
 /* Streaming benchmark and end-to-end check (config 5): a producer thread
    publishes frags public_key | signature | message cyclically from the
@@ -281,11 +369,27 @@ fd_verify_amd_tile_cut( ulong staged, ulong handed, ulong pubd, ulong light_frag
    largest lateness behind its schedule (ns; its stalls count as latency),
    out[15] = the tile thread's longest pass of its run loop (ns; a stall of
    the host thread shows here), out[16] = the consumer's longest gap between
-   two frags it saw.  out holds 17 doubles.  Returns 0 or an error code. */
+   two frags it saw.  Latency decomposition (fd_verify_amd_tile_set_trace,
+   every published frag, ns; not in check mode): out[17..26] = p50, p99 of
+   the cut wait, queue wait, service, publish wait and input wait (latency
+   minus the other four: producer publish -> staged), out[27] / out[28] =
+   p50 service of latency / throughput chunks, out[29] = chunk-mode
+   switches, out[30] = frags traced, out[31] = 0.  out holds 32 doubles.
+   Threads: producer, tile, the tile's publisher and consumer each pinned
+   to a CPU of their own when the process may use 5 or more (else unpinned,
+   publisher inline).  waves: the tile's cfg.waves (0: the device's share;
+   ranks that share a GPU in separate processes each pass theirs).  Returns
+   0 or an error code. */
 #define FD_VERIFY_AMD_BENCH_ZERO_COPY (1)
 #define FD_VERIFY_AMD_BENCH_WRITE     (2)
 #define FD_VERIFY_AMD_BENCH_LAP       (4)
 #define FD_VERIFY_AMD_BENCH_SAMPLE_BYTES (8)
+#define FD_VERIFY_AMD_BENCH_CHUNK_LAT (16)   /* chunk_mode LATENCY */
+#define FD_VERIFY_AMD_BENCH_CHUNK_THR (32)   /* chunk_mode THROUGHPUT */
+#define FD_VERIFY_AMD_BENCH_PUB_INLINE (64)  /* publish on the tile's thread */
+#define FD_VERIFY_AMD_BENCH_TXN        (128) /* TXN framing: pool entry k is the wire transaction
+                                                blob[msg_off[k], +msg_sz[k]) (pub, sig unused); expect_err /
+                                                expect_tag per transaction (verdict, first signature's tag) */
 
 int
 fd_verify_amd_bench_stream( int           device,
@@ -303,6 +407,7 @@ fd_verify_amd_bench_stream( int           device,
                             schar const * expect_err,
                             ulong const * expect_tag,
                             ulong         frag_cnt,
+                            ulong         waves,
                             double *      out );
 
 #ifdef __cplusplus

@@ -385,3 +385,198 @@ def test_tile_runs_until_stop_and_continues(zero_copy):
     assert d1["sv_filt_cnt"] + d2["sv_filt_cnt"] == sv and tile.in_fseq == len(order)
     assert [int(mc_out[o]["seq"]) for o in range(len(exp))] == list(range(len(exp)))
     assert [int(mc_out[o]["sig"]) for o in range(len(exp))] == [t for _, t in exp]
+
+
+@pytest.mark.parametrize("chunk_mode", [1, 2])      # tango.CHUNK_LATENCY, tango.CHUNK_THROUGHPUT
+@pytest.mark.parametrize("zero_copy", [False, True])
+def test_tile_golden_codes_per_chunk_mode(golden, chunk_mode, zero_copy):
+    """Every golden vector (the reference's codes, the 156 limb-compare false
+    rejects included) through k_tile_persist with every chunk forced to one
+    mode: 8-lane latency chunks (k_dsm8's body) or 64-frag throughput chunks
+    (k_dsm's body).  The tile's verdict log must equal the reference's code
+    for every frag; the published set and the per-code SV_FILT counts follow."""
+    from firedancer_amd import tango
+    n = len(golden)
+    idx = [i for i in range(n) if golden.msg_sz[i] <= 1232]
+    assert len(idx) == n
+    msgs = [golden.msg(i) for i in range(n)]
+    order = np.arange(n)
+    mc_in, dc, _, _, _ = _feed(golden.pub, golden.sig, msgs, order, 4096)
+    mc_out = tango.mcache_new(4096)
+    tile = tango.VerifyTile(0, batch_max=4096, tcache_depth=0, chunk_mode=chunk_mode)
+    if zero_copy:
+        tile.register_dcache(dc)
+    log = np.full(n, 99, np.int8)
+    tile.set_verdict_log(log)
+    try:
+        diag, _ = tile.run(mc_in, dc, 0, mc_out, 0, n)
+    finally:
+        tile.close()
+    exp = golden.expect
+    bad = np.nonzero(log != exp)[0]
+    assert bad.size == 0, [(int(i), int(log[i]), int(exp[i])) for i in bad[:10]]
+    assert diag["out_cnt"] == int((exp == 0).sum())
+    assert [diag["sv_filt_sig_cnt"], diag["sv_filt_pubkey_cnt"], diag["sv_filt_msg_cnt"]] == \
+        [int((exp == c).sum()) for c in (-1, -2, -3)]
+    key = "gpu_frag_lat_cnt" if chunk_mode == 1 else "gpu_frag_thr_cnt"
+    assert diag[key] == n
+    assert all(int(mc_out[o]["seq"]) == o for o in range(diag["out_cnt"]))
+
+
+def _signed_feed(seed, count, depth):
+    from firedancer_amd import ed25519
+    prv, blob, off, sz, fk, fp = _oracle.stream_inputs(seed, count, 0, 300, False)
+    pub, sig = ed25519.sign_batch(prv, blob, off, sz)
+    msgs = [bytes(blob[off[i]:off[i] + sz[i]]) for i in range(len(sz))]
+    return pub, sig, msgs, _feed(pub, sig, msgs, np.arange(count), depth)
+
+
+def test_tile_halts_while_backpressured():
+    """The consumer stops advancing out_fseq: the tile fills its output
+    credit (out_depth frags) and is backpressured.  A raised *stop returns
+    the run within 100 ms (the halt grace is 50 ms), the way the reference
+    tile keeps its HALT check running while backpressured; the frags it
+    could not publish are counted in halt_drop_cnt."""
+    import ctypes
+    import threading
+    import time
+    from firedancer_amd import tango
+    n = 6000
+    pub, sig, msgs, (mc_in, dc, _, _, _) = _signed_feed(3131, n, 8192)
+    mc_out = tango.mcache_new(256)
+    out_fseq = ctypes.c_ulong(0)                 # a consumer that never moves
+    tile = tango.VerifyTile(0, batch_max=1024, tcache_depth=0)
+    stop = ctypes.c_int(0)
+    res = {}
+
+    def go():
+        try:
+            res["r"] = tile.run(mc_in, dc, 0, mc_out, 0, 0, stop=stop, out_fseq=out_fseq)
+        except Exception as e:   # noqa: BLE001
+            res["e"] = e
+        res["t"] = time.perf_counter()
+
+    th = threading.Thread(target=go)
+    th.start()
+    try:
+        t0 = time.time()
+        while int(mc_out[255]["seq"]) != 255 and time.time() - t0 < 30:
+            time.sleep(0.001)
+        time.sleep(0.05)                            # the tile now spins backpressured
+        assert th.is_alive()
+        t_stop = time.perf_counter()
+        stop.value = 1
+        th.join(timeout=10)
+        assert not th.is_alive()
+    finally:
+        stop.value = 1
+        th.join(timeout=10)
+        tile.close()
+    assert "e" not in res, res.get("e")
+    assert res["t"] - t_stop < 0.1
+    diag, _ = res["r"]
+    assert diag["out_cnt"] == 256 and diag["halt_drop_cnt"] > 0
+    assert diag["out_cnt"] + diag["sv_filt_cnt"] + diag["halt_drop_cnt"] == diag["in_cnt"]
+
+
+def test_engine_call_beside_a_tile_with_a_partial_share(golden, engine):
+    """A tile whose run holds a quarter of the GPU's wave slots (cfg.waves)
+    does not starve the device: an engine batch call on the same GPU
+    completes while the run lasts, with the reference's codes."""
+    import ctypes
+    import threading
+    import time
+    from firedancer_amd import tango
+    n = 500
+    pub, sig, msgs, (mc_in, dc, _, _, _) = _signed_feed(4141, n, 1024)
+    mc_out = tango.mcache_new(1024)
+    tile = tango.VerifyTile(0, batch_max=1024, tcache_depth=0, waves=512)
+    stop = ctypes.c_int(0)
+    res = {}
+    th = threading.Thread(target=lambda: res.setdefault("r", tile.run(mc_in, dc, 0, mc_out, 0, 0, stop=stop)))
+    th.start()
+    try:
+        t0 = time.time()
+        while int(mc_out[n - 1]["seq"]) != n - 1 and time.time() - t0 < 30:
+            time.sleep(0.001)
+        assert th.is_alive() and int(mc_out[n - 1]["seq"]) == n - 1      # the tile's kernel is live
+        out = {}
+        eth = threading.Thread(target=lambda: out.setdefault("err", engine.verify_soa(
+            golden.pub, golden.sig, golden.msg_off, golden.msg_sz, golden.blob)))
+        eth.start()
+        eth.join(timeout=60)
+        assert not eth.is_alive()
+        assert np.array_equal(out["err"], golden.expect)
+        assert th.is_alive()
+    finally:
+        stop.value = 1
+        th.join(timeout=30)
+        tile.close()
+    diag, _ = res["r"]
+    assert diag["out_cnt"] == n
+
+
+def test_tile_run_refuses_when_its_kernel_cannot_start():
+    """A second tile created after a first tile's run took every wave slot:
+    its kernel cannot start, so its run returns an error within ~2 s
+    instead of spinning; the first run is unaffected."""
+    import ctypes
+    import threading
+    import time
+    from firedancer_amd import ed25519, tango
+    n = 300
+    pub, sig, msgs, (mc_in, dc, _, _, _) = _signed_feed(5151, n, 1024)
+    mc_out = tango.mcache_new(1024)
+    a = tango.VerifyTile(0, batch_max=1024, tcache_depth=0)          # the device's whole share
+    stop = ctypes.c_int(0)
+    res = {}
+    th = threading.Thread(target=lambda: res.setdefault("r", a.run(mc_in, dc, 0, mc_out, 0, 0, stop=stop)))
+    th.start()
+    b = None
+    try:
+        t0 = time.time()
+        while int(mc_out[n - 1]["seq"]) != n - 1 and time.time() - t0 < 30:
+            time.sleep(0.001)
+        assert int(mc_out[n - 1]["seq"]) == n - 1
+        b = tango.VerifyTile(0, batch_max=1024, tcache_depth=0, waves=1024)
+        mc_out2 = tango.mcache_new(1024)
+        t1 = time.perf_counter()
+        with pytest.raises(ed25519.EngineError):
+            b.run(mc_in, dc, 0, mc_out2, 0, n)
+        assert time.perf_counter() - t1 < 4.0
+        assert th.is_alive()
+    finally:
+        stop.value = 1
+        th.join(timeout=30)
+        if b is not None:
+            b.close()                                # waits for its queued kernel, which exits at once
+        a.close()
+    diag, _ = res["r"]
+    assert diag["out_cnt"] == n
+
+
+def test_tile_trace_decomposes_latency():
+    """fd_verify_amd_tile_set_trace: per published frag the cut wait, queue
+    wait, service and publish wait; they sum to at most the frag's latency
+    (the rest is the input wait), service is a chunk's GPU time (tens of
+    us to a few ms), and latency chunks carry their flag."""
+    from firedancer_amd import tango
+    n = 3000
+    pub, sig, msgs, (mc_in, dc, _, _, ts) = _signed_feed(6161, n, 4096)
+    now = tango.tickcount()
+    for s in range(n):                              # tsorig = now: latency from here
+        mc_in[s]["tsorig"] = now
+    mc_out = tango.mcache_new(4096)
+    tile = tango.VerifyTile(0, batch_max=1024, tcache_depth=0, chunk_mode=tango.CHUNK_LATENCY)
+    parts = np.zeros((n, 4), np.uint32)
+    tile.set_trace(parts)
+    try:
+        diag, lat = tile.run(mc_in, dc, 0, mc_out, 0, n, lat_max=n)
+    finally:
+        tile.close()
+    assert diag["out_cnt"] == n and lat.size == n
+    svc = parts[:, 2] & 0x7FFFFFFF
+    assert ((parts[:, 2] >> 31) == 1).all()          # every chunk a latency chunk
+    assert (svc > 20_000).all() and (svc < 50_000_000).all()
+    tot = parts[:, 0].astype(np.int64) + parts[:, 1] + svc + parts[:, 3]
+    assert (tot <= lat.astype(np.int64) + 20_000).all()   # GPU clock mapping within 20 us
