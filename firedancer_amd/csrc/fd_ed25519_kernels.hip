@@ -1923,11 +1923,19 @@ tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog ) {
     u64 h = ld_sys64( &H->head ), b = ld_sys64( &H->beat );
     u32 st = ld_sys32( &H->stop );
     u64 now = __builtin_amdgcn_s_memrealtime();
+#ifndef FD_AMD_AB_SCOUT_NOCLK
     if( now - tclk >= 1000UL ) {
       tclk = now;
+#ifdef FD_AMD_AB_SCOUT_NODONE
+      st_sys64( &H->gdone, 0UL );
+#else
       st_sys64( &H->gdone, ld_dev64( &D->done ) );
+#endif
       st_sys64( &H->gclock, now );
     }
+#else
+    (void)tclk;
+#endif
     if( b != lastb ) { lastb = b; tb = now; }
     bool dead = now - tb > watchdog;
     if( dead ) st_sys32( &H->kerr, 1u );
@@ -2102,7 +2110,9 @@ k_tile_persist( fd_amd_tile_args_t A ) {
     if( take && take <= 64u ) tile_chunk( A, c, take, e8, scr, L, S, bi, evl, pt, tc );
     if( !l ) {
       s_tally[e8 ? 8 : 9] += 1UL; s_tally[e8 ? 10 : 11] += take;
+#ifndef FD_AMD_AB_NO_DONE_ATOMIC
       atomicAdd( (unsigned long long *)&D->done, 1ULL );   /* progress, mirrored to the host by the scout */
+#endif
     }
   }
   if( l == 0u ) {

@@ -376,6 +376,9 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
      the tile's own batch streams never queue behind it. */
   int prio_lo = 0, prio_hi = 0;
   if( hipDeviceGetStreamPriorityRange( &prio_lo, &prio_hi ) != hipSuccess ) prio_hi = 0;
+#ifdef FD_AMD_TILE_PRIO_NORMAL   /* A/B build */
+  prio_hi = prio_lo;
+#endif
   if( hipStreamCreateWithPriority( &t->pst, hipStreamNonBlocking, prio_hi ) != hipSuccess ||
       hipEventCreateWithFlags( &t->pdone, hipEventDisableTiming ) != hipSuccess ||
       hipHostMalloc( (void **)&t->hctl, sizeof(fd_amd_tile_hctl_t), hf ) != hipSuccess ||
@@ -753,7 +756,11 @@ struct prun_t {
   alignas(64) std::atomic<int>   quit;      /* stager -> publisher: stop now (error, or the halt grace ran out) */
 };
 
+#ifdef FD_AMD_AB_BEAT_STORE
+inline void beat( fd_amd_tile_hctl_t * H ) { __atomic_store_n( &H->beat, __atomic_load_n( &H->beat, __ATOMIC_RELAXED ) + 1UL, __ATOMIC_RELAXED ); }
+#else
 inline void beat( fd_amd_tile_hctl_t * H ) { __atomic_fetch_add( &H->beat, 1UL, __ATOMIC_RELAXED ); }
+#endif
 
 /* The GPU clock (s_memrealtime, 100 MHz) on the host's: sample the scout's
    clock word, keep the smallest (host - GPU) offset of each 20 ms window
@@ -885,8 +892,11 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
                   ulong const * out_fseq, ulong frag_cnt, int const * stop, fd_verify_amd_diag_t * diag, uint * lat,
                   ulong lat_max, uint8_t const * zc_dev, ulong zc_lim ) {
   int rc = tile_persist_alloc( t );
-  if( rc ) return rc;
-  if( tile_kernel_busy( t ) ) return FD_ED25519_AMD_ERR_DEVICE;
+  if( rc ) { fprintf( stderr, "fd_verify_amd_tile_run: allocating the persistent consumer failed (%d)\n", rc ); return rc; }
+  if( tile_kernel_busy( t ) ) {
+    fprintf( stderr, "fd_verify_amd_tile_run: the kernel of an earlier run of this tile has not finished\n" );
+    return FD_ED25519_AMD_ERR_DEVICE;
+  }
   ulong const F = t->frame_cnt, mask = t->R - 1UL, W = t->window, base = t->ring_seq;
   fd_amd_tile_hctl_t * H = t->hctl;
 
@@ -905,6 +915,9 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   for( int x=0; x<FD_AMD_TILE_MIRRORS; x++ ) t->d0.mw[x].w = dbase;
   if( hipMemcpyAsync( t->dctl, &t->d0, sizeof t->d0, hipMemcpyHostToDevice, t->pst ) != hipSuccess )
     return FD_ED25519_AMD_ERR_DEVICE;
+#ifdef FD_AMD_TILE_SYNC_SEED   /* A/B build */
+  if( hipStreamSynchronize( t->pst ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+#endif
   fd_amd_tile_args_t A;
   memset( &A, 0, sizeof A );
   A.hctl = (fd_amd_tile_hctl_t *)t->hctl_dev;
@@ -920,6 +933,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   A.scratch = t->scratch;
   A.watchdog = 500000000UL;   /* 5 s of s_memrealtime (100 MHz) without a heartbeat */
   if( fd_amd_launch_tile_persist( &A, t->waves, t->pst ) || hipEventRecord( t->pdone, t->pst ) != hipSuccess ) {
+    fprintf( stderr, "fd_verify_amd_tile_run: launching the tile kernel failed\n" );
     (void)hipStreamSynchronize( t->pst );
     return FD_ED25519_AMD_ERR_DEVICE;
   }
@@ -941,8 +955,16 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   {
     cpu_set_t cs; CPU_ZERO( &cs );
     bool two = false;
+#ifdef FD_AMD_AB_PUB_INLINE
+    if( 0 ) {}
+#else
     if( t->cfg.publish_cpu >= 0 ) { CPU_SET( t->cfg.publish_cpu, &cs ); two = true; }
+#endif
+#ifdef FD_AMD_AB_PUB_INLINE
+    else if( 0 &&
+#else
     else if( t->cfg.publish_cpu == FD_VERIFY_AMD_PUBLISH_AUTO &&
+#endif
              !pthread_getaffinity_np( pthread_self(), sizeof cs, &cs ) && CPU_COUNT( &cs ) >= 2 ) {
       int me = sched_getcpu();
       if( me >= 0 && me < CPU_SETSIZE ) CPU_CLR( me, &cs );
@@ -969,7 +991,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   ulong ovrn = 0, bad = 0, ha = 0, ha_sz = 0, backp = 0, nbatch = 0, nsig = 0, switches = 0;
   ulong cdone = dbase;                   /* first descriptor not known to be finished */
   ulong iter = 0UL, pass_t = now_ns(), pass_max = 0UL, t_halt = 0UL;
-  ulong t_chk = pass_t, g_seen = 0UL, t_prog = pass_t;
+  ulong t_chk = pass_t, g_seen = 0UL, t_prog = pass_t, gc_first = 0UL, gc_last = 0UL, gc_host = 0UL;
   ulong r_t0 = pass_t, r_n0 = staged;
   double rate = 0.0;
   int thr = fd_verify_amd_tile_mode( t->cfg.chunk_mode, 0, 0.0, t->rate_hi, t->rate_lo );
@@ -982,6 +1004,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
        pass: each store after a GPU read of the line is a cache-line
        ownership round trip */
     if( !(++iter & 63UL) ) beat( H );
+    if( !gc_first ) gc_first = __atomic_load_n( &H->gclock, __ATOMIC_ACQUIRE );
     ulong const tn = now_ns();
     pass_max = std::max( pass_max, tn - pass_t ); pass_t = tn;
 
@@ -1105,20 +1128,33 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       }
     }
 
-    /* 5. every ~1 ms: the kernel is running, started, and making progress */
+    /* 5. every ~1 ms: the kernel started, is alive and makes progress.
+          Read from the scout's words only: its clock advances every
+          ~10 us while the kernel lives (HIP is asked about the kernel only
+          once that clock has stood still for 100 ms), and gdone counts the
+          chunks finished. */
     if( t3 - t_chk >= 1000000UL ) {
       t_chk = t3;
-      hipError_t q = hipEventQuery( t->pdone );
-      ulong const g = __atomic_load_n( &H->gdone, __ATOMIC_ACQUIRE );
+      ulong const g  = __atomic_load_n( &H->gdone,  __ATOMIC_ACQUIRE );
+      ulong const gc = __atomic_load_n( &H->gclock, __ATOMIC_ACQUIRE );
+      if( gc != gc_last ) { gc_last = gc; gc_host = t3; }
       if( g != g_seen || t->desc_seq - dbase == g ) { g_seen = g; t_prog = t3; }
       char const * why = NULL;
-      if( q != hipErrorNotReady ) why = "the tile kernel exited early";
-      else if( !__atomic_load_n( &H->gclock, __ATOMIC_ACQUIRE ) && t3 - t_launch > 2000000000UL )
-        why = "the tile kernel did not start within 2 s (its wave slots are held by another kernel?)";
-      else if( t3 - t_prog > 2000000000UL ) why = "the tile kernel made no progress for 2 s";
+      hipError_t q = hipSuccess;
+      if( !gc ) {
+        if( t3 - t_launch > 2000000000UL ) why = "the tile kernel did not start within 2 s (its wave slots are held by another kernel?)";
+      } else if( t3 - gc_host > 100000000UL ) {
+#ifdef FD_AMD_AB_NO_QUERY
+        q = hipErrorNotReady;
+#else
+        q = hipEventQuery( t->pdone );
+#endif
+        why = q != hipErrorNotReady ? "the tile kernel exited early" : "the tile kernel's scout stopped (its clock stood still for 100 ms)";
+      } else if( t3 - t_prog > 2000000000UL ) why = "the tile kernel made no progress for 2 s";
       if( why ) {
-        fprintf( stderr, "fd_verify_amd_tile_run: %s (%s, watchdog %u)\n", why, hipGetErrorString( q ),
-                 __atomic_load_n( &H->kerr, __ATOMIC_ACQUIRE ) );
+        fprintf( stderr, "fd_verify_amd_tile_run: %s (%s, watchdog %u; chunks done %lu of %lu, staged %lu handed %lu "
+                 "published %lu)\n", why, hipGetErrorString( q ), __atomic_load_n( &H->kerr, __ATOMIC_ACQUIRE ),
+                 g, t->desc_seq - dbase, staged - base, handed - base, pubd - base );
         rc = FD_ED25519_AMD_ERR_DEVICE;
         break;
       }
@@ -1142,11 +1178,20 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     }
     if( q == hipErrorNotReady ) { t->pending = true; rc = FD_ED25519_AMD_ERR_DEVICE; }
     else if( q != hipSuccess ) rc = FD_ED25519_AMD_ERR_DEVICE;
+    if( q != hipSuccess )
+      fprintf( stderr, "fd_verify_amd_tile_run: the tile kernel %s after the stop (%s; scout clock ran %.3f ms, last change "
+               "%.3f ms before the stop, chunks done %lu of %lu, kerr %u)\n", q == hipErrorNotReady ? "did not exit" : "failed",
+               hipGetErrorString( q ), gc_first ? 1e-5 * (double)(__atomic_load_n( &H->gclock, __ATOMIC_ACQUIRE ) - gc_first) : -1.0,
+               gc_host ? 1e-6 * (double)(t0 - gc_host) : -1.0, (ulong)__atomic_load_n( &H->gdone, __ATOMIC_ACQUIRE ),
+               t->desc_seq - dbase, __atomic_load_n( &H->kerr, __ATOMIC_ACQUIRE ) );
   }
   ulong st[4] = { 0, 0, 0, 0 };
   if( !t->pending && ( hipMemcpyAsync( st, t->dctl->stat, sizeof st, hipMemcpyDeviceToHost, t->pst ) != hipSuccess ||
                        hipStreamSynchronize( t->pst ) != hipSuccess ) ) rc = FD_ED25519_AMD_ERR_DEVICE;
-  if( __atomic_load_n( &H->kerr, __ATOMIC_ACQUIRE ) ) rc = FD_ED25519_AMD_ERR_DEVICE;
+  if( __atomic_load_n( &H->kerr, __ATOMIC_ACQUIRE ) ) {
+    fprintf( stderr, "fd_verify_amd_tile_run: the tile kernel's watchdog fired (no host heartbeat for 5 s)\n" );
+    rc = FD_ED25519_AMD_ERR_DEVICE;
+  }
   diag->gpu_chunk_lat_cnt += st[0]; diag->gpu_chunk_thr_cnt += st[1];
   diag->gpu_frag_lat_cnt  += st[2]; diag->gpu_frag_thr_cnt  += st[3];
   diag->ovrn_cnt += ovrn + r.d.ovrn_cnt; diag->bad_frag_cnt += bad;

@@ -1,7 +1,7 @@
 """k_dsmp A/B aid: a resident 2^20 batch through the per-lane (k_dsm) and the
 pooled (k_ai + k_dsmp + k_fin) double-scalar multiply, DSM-stage time from
 HIP events, verdicts compared, and the pool's fill statistics when the
-library was built with FD_POOL_DEBUG (fd_amd_pool_debug)."""
+library was built with FD_AMD_DIAG (fd_amd_pool_debug)."""
 import ctypes
 import json
 import os

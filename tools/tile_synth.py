@@ -1,11 +1,16 @@
 """Measurement aid: k_tile_persist's chunk pipeline alone (fd_amd_tile_synth:
 frags already in device memory, no host hand-off).  Per configuration the
-launch time, the time per chunk per wave and the verdict check.
-    python tools/tile_synth.py"""
+launch time, the time per chunk per wave and the verdict check.  Runs on the
+diagnostics library (FD_AMD_DIAG build; the product library does not carry
+k_tile_synth):
+    python -m firedancer_amd.build --diag && python tools/tile_synth.py"""
 import ctypes
 import json
 import os
 import sys
+
+os.environ.setdefault("FD_AMD_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                 "firedancer_amd", "libfd_ed25519_amd_diag.so"))
 
 import numpy as np
 
