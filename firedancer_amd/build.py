@@ -69,12 +69,46 @@ def build_engine(force=False, verbose=False, out=None, defines=()):
 
     with ThreadPoolExecutor(max_workers=min(len(SOURCES), max(1, min(8, os.cpu_count() or 1)))) as ex:
         list(ex.map(cc, range(len(SOURCES))))
+    v = kernel_vgprs(objs[0], "_Z14k_tile_persist18fd_amd_tile_args_t")
+    if v is not None and v > TILE_VGPR_LIMIT:
+        raise RuntimeError("k_tile_persist compiled to %d VGPRs (limit %d): at 256 its scout wave stops; "
+                           "see profiles/r04_tile_scout_vgpr_ab.txt" % (v, TILE_VGPR_LIMIT))
     cmd = [_hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib + ".tmp"] + objs + ["-lpthread"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd, cwd=CSRC)
     os.replace(lib + ".tmp", lib)
     return lib
+
+
+def kernel_vgprs(obj, kernel):
+    """VGPR count of `kernel` in a compiled .hip object (its gfx950 code
+    object's metadata), or None when the LLVM tools are missing."""
+    import re
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not os.path.exists(os.path.join(llvm, "llvm-readelf")):
+        return None
+    subprocess.check_call([os.path.join(llvm, "llvm-objdump"), "--offloading", obj], stdout=subprocess.DEVNULL,
+                          stderr=subprocess.DEVNULL)
+    co = obj + ".0.hipv4-amdgcn-amd-amdhsa--" + ARCH
+    host = obj + ".0.host-x86_64-unknown-linux-gnu-"
+    try:
+        notes = subprocess.check_output([os.path.join(llvm, "llvm-readelf"), "--notes", co], text=True)
+    finally:
+        for f in (co, host):
+            if os.path.exists(f):
+                os.remove(f)
+    i = notes.find(".name:           " + kernel)
+    if i < 0:
+        return None
+    j = notes.find("\n  - .", i)   # the kernel's metadata entry: from its "- ." line to the next one
+    m = re.search(r"\.vgpr_count:\s*(\d+)", notes[notes.rfind("- .", 0, i):j if j > 0 else len(notes)])
+    return int(m.group(1)) if m else None
+
+
+# k_tile_persist at 256 VGPRs: its scout wave stopped ~0.7 ms into every run
+# (round-4 A/B, profiles/r04_tile_scout_vgpr_ab.txt) -- refuse such a build
+TILE_VGPR_LIMIT = 255
 
 
 def build_diag(force=False, verbose=False):

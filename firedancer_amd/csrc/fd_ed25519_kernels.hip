@@ -1923,19 +1923,11 @@ tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog ) {
     u64 h = ld_sys64( &H->head ), b = ld_sys64( &H->beat );
     u32 st = ld_sys32( &H->stop );
     u64 now = __builtin_amdgcn_s_memrealtime();
-#ifndef FD_AMD_AB_SCOUT_NOCLK
     if( now - tclk >= 1000UL ) {
       tclk = now;
-#ifdef FD_AMD_AB_SCOUT_NODONE
-      st_sys64( &H->gdone, 0UL );
-#else
       st_sys64( &H->gdone, ld_dev64( &D->done ) );
-#endif
       st_sys64( &H->gclock, now );
     }
-#else
-    (void)tclk;
-#endif
     if( b != lastb ) { lastb = b; tb = now; }
     bool dead = now - tb > watchdog;
     if( dead ) st_sys32( &H->kerr, 1u );
@@ -1957,15 +1949,10 @@ tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog ) {
 __device__ __forceinline__ void
 tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __restrict__ scr, ws_layout_t L,
             tile_scratch_t const & S, i32 (* __restrict__ bi)[48], u64 (* __restrict__ evl)[33], u64 * pt, u64 tc ) {
-#ifdef FD_AMD_DIAG
-  /* pt (diagnostics build, A.prof): s_memrealtime ticks spent in gather,
-     prep + decomp, DSM, results; wave-uniform values */
+  /* pt (A.prof, set by the diagnostics build's host only): s_memrealtime
+     ticks spent in gather, prep + decomp, DSM, results; wave-uniform */
   u64 ts = A.prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
 # define TILE_STAMP( k_ ) do { if( A.prof ) { u64 t_ = __builtin_amdgcn_s_memrealtime(); if( !threadIdx.x ) pt[k_] += t_ - ts; ts = t_; } } while(0)
-#else
-  (void)pt;
-# define TILE_STAMP( k_ ) do { } while(0)
-#endif
   /* opaque per chunk: otherwise the compiler hoists every per-lane address
      of the bodies out of the persistent loop and spills them */
   {
@@ -2065,11 +2052,12 @@ k_tile_persist( fd_amd_tile_args_t A ) {
   __shared__ u64 s_tally[12];
   if( l < 12u ) s_tally[l] = 0UL;
   u64 * const pt = s_tally;
-#ifdef FD_AMD_DIAG
+  /* A run-time flag (the host sets it only in the diagnostics build), not a
+     compile-time constant: with the profiling branches folded away the
+     compiler gives this kernel all 256 VGPRs, and at 256 its scout wave
+     stopped ~0.7 ms into every run (round-4 A/B, profiles/
+     r04_tile_scout_vgpr_ab.txt); build.py refuses a build at 256. */
   bool const prof = A.prof != 0u;
-#else
-  constexpr bool prof = false;
-#endif
   for( ;; ) {
     u64 t = 0;
     if( l == 0u ) t = atomicAdd( (unsigned long long *)&D->ticket, 1ULL );
@@ -2110,9 +2098,7 @@ k_tile_persist( fd_amd_tile_args_t A ) {
     if( take && take <= 64u ) tile_chunk( A, c, take, e8, scr, L, S, bi, evl, pt, tc );
     if( !l ) {
       s_tally[e8 ? 8 : 9] += 1UL; s_tally[e8 ? 10 : 11] += take;
-#ifndef FD_AMD_AB_NO_DONE_ATOMIC
       atomicAdd( (unsigned long long *)&D->done, 1ULL );   /* progress, mirrored to the host by the scout */
-#endif
     }
   }
   if( l == 0u ) {

@@ -376,9 +376,6 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
      the tile's own batch streams never queue behind it. */
   int prio_lo = 0, prio_hi = 0;
   if( hipDeviceGetStreamPriorityRange( &prio_lo, &prio_hi ) != hipSuccess ) prio_hi = 0;
-#ifdef FD_AMD_TILE_PRIO_NORMAL   /* A/B build */
-  prio_hi = prio_lo;
-#endif
   if( hipStreamCreateWithPriority( &t->pst, hipStreamNonBlocking, prio_hi ) != hipSuccess ||
       hipEventCreateWithFlags( &t->pdone, hipEventDisableTiming ) != hipSuccess ||
       hipHostMalloc( (void **)&t->hctl, sizeof(fd_amd_tile_hctl_t), hf ) != hipSuccess ||
@@ -756,11 +753,7 @@ struct prun_t {
   alignas(64) std::atomic<int>   quit;      /* stager -> publisher: stop now (error, or the halt grace ran out) */
 };
 
-#ifdef FD_AMD_AB_BEAT_STORE
-inline void beat( fd_amd_tile_hctl_t * H ) { __atomic_store_n( &H->beat, __atomic_load_n( &H->beat, __ATOMIC_RELAXED ) + 1UL, __ATOMIC_RELAXED ); }
-#else
 inline void beat( fd_amd_tile_hctl_t * H ) { __atomic_fetch_add( &H->beat, 1UL, __ATOMIC_RELAXED ); }
-#endif
 
 /* The GPU clock (s_memrealtime, 100 MHz) on the host's: sample the scout's
    clock word, keep the smallest (host - GPU) offset of each 20 ms window
@@ -915,9 +908,6 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   for( int x=0; x<FD_AMD_TILE_MIRRORS; x++ ) t->d0.mw[x].w = dbase;
   if( hipMemcpyAsync( t->dctl, &t->d0, sizeof t->d0, hipMemcpyHostToDevice, t->pst ) != hipSuccess )
     return FD_ED25519_AMD_ERR_DEVICE;
-#ifdef FD_AMD_TILE_SYNC_SEED   /* A/B build */
-  if( hipStreamSynchronize( t->pst ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
-#endif
   fd_amd_tile_args_t A;
   memset( &A, 0, sizeof A );
   A.hctl = (fd_amd_tile_hctl_t *)t->hctl_dev;
@@ -932,6 +922,9 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   A.dctl = t->dctl;
   A.scratch = t->scratch;
   A.watchdog = 500000000UL;   /* 5 s of s_memrealtime (100 MHz) without a heartbeat */
+#ifdef FD_AMD_DIAG
+  { char const * e = getenv( "FD_AMD_TILE_PROF" ); A.prof = e && *e && *e != '0'; }   /* diagnostics build only */
+#endif
   if( fd_amd_launch_tile_persist( &A, t->waves, t->pst ) || hipEventRecord( t->pdone, t->pst ) != hipSuccess ) {
     fprintf( stderr, "fd_verify_amd_tile_run: launching the tile kernel failed\n" );
     (void)hipStreamSynchronize( t->pst );
@@ -955,16 +948,8 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   {
     cpu_set_t cs; CPU_ZERO( &cs );
     bool two = false;
-#ifdef FD_AMD_AB_PUB_INLINE
-    if( 0 ) {}
-#else
     if( t->cfg.publish_cpu >= 0 ) { CPU_SET( t->cfg.publish_cpu, &cs ); two = true; }
-#endif
-#ifdef FD_AMD_AB_PUB_INLINE
-    else if( 0 &&
-#else
     else if( t->cfg.publish_cpu == FD_VERIFY_AMD_PUBLISH_AUTO &&
-#endif
              !pthread_getaffinity_np( pthread_self(), sizeof cs, &cs ) && CPU_COUNT( &cs ) >= 2 ) {
       int me = sched_getcpu();
       if( me >= 0 && me < CPU_SETSIZE ) CPU_CLR( me, &cs );
@@ -1143,14 +1128,10 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       hipError_t q = hipSuccess;
       if( !gc ) {
         if( t3 - t_launch > 2000000000UL ) why = "the tile kernel did not start within 2 s (its wave slots are held by another kernel?)";
-      } else if( t3 - gc_host > 100000000UL ) {
-#ifdef FD_AMD_AB_NO_QUERY
-        q = hipErrorNotReady;
-#else
+      } else if( gc && t3 - gc_host > 100000000UL ) {
         q = hipEventQuery( t->pdone );
-#endif
         why = q != hipErrorNotReady ? "the tile kernel exited early" : "the tile kernel's scout stopped (its clock stood still for 100 ms)";
-      } else if( t3 - t_prog > 2000000000UL ) why = "the tile kernel made no progress for 2 s";
+      } else if( gc && t3 - t_prog > 2000000000UL ) why = "the tile kernel made no progress for 2 s";
       if( why ) {
         fprintf( stderr, "fd_verify_amd_tile_run: %s (%s, watchdog %u; chunks done %lu of %lu, staged %lu handed %lu "
                  "published %lu)\n", why, hipGetErrorString( q ), __atomic_load_n( &H->kerr, __ATOMIC_ACQUIRE ),

@@ -101,3 +101,20 @@ def test_two_rank_gloo_shards_match_single_process():
     g = _golden.load_vectors()
     assert elapsed == 2.0                      # max over ranks
     assert np.array_equal(np.array(allerr, np.int8), g.expect)
+
+
+def test_peer_slot_and_cpu_slice():
+    """Ranks that share a NUMA node (or a GPU) find their index among their
+    peers, and split the node's CPUs into disjoint slices (the per-rank tile
+    rows of bench.py pin each rank's spinning threads to its own slice)."""
+    from firedancer_amd.shard import cpu_slice, peer_slot
+    keys = [0, 0, 1, 1, 0, 1, 0, 1]                 # NUMA node per rank
+    assert [peer_slot(keys, r) for r in range(8)] == [(0, 4), (1, 4), (0, 4), (1, 4), (2, 4), (2, 4), (3, 4),
+                                                        (3, 4)]
+    cpus = list(range(64, 96)) + list(range(0, 32))
+    slices = [cpu_slice([c for c in cpus if c < 32], k, 4) for k in range(4)]
+    assert slices == [list(range(8 * k, 8 * k + 8)) for k in range(4)]
+    assert cpu_slice(range(10), 0, 1) == list(range(10))
+    assert cpu_slice(range(10), 2, 3) == [6, 7, 8]
+    with pytest.raises(ValueError):
+        cpu_slice(range(10), 3, 3)
