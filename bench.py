@@ -431,9 +431,16 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
             key = "zero_copy" if zc else "copy"
             sat = tango.bench_stream(local, bmax, 0, *pool, args.stream_frags, zero_copy=zc, expect_err=p_err,
                                      expect_tag=p_tag, sample_bytes=True)
-            rr = {"saturated_frags_per_s": sat["frags_per_s"], "saturated_mean_chunk": sat["mean_batch"],
+            rr = {"saturated_frags_per_s": sat["frags_per_s"], "saturated_mean_hand_off": sat["mean_batch"],
                   "published": int(sat["published"]), "sv_filt": int(sat["sv_filt"]), "ovrn": int(sat["ovrn"]),
-                  "check_mismatches": int(sat["mismatches"]), "checked": int(sat["checked"])}
+                  "check_mismatches": int(sat["mismatches"]), "checked": int(sat["checked"]),
+                  "saturated_loop": {k: int(sat[k]) for k in ("passes", "hand_offs", "stop_window", "stop_frames",
+                                                                "stop_batch_max", "stop_pass_bound", "gpu_chunks_lat",
+                                                                "gpu_chunks_thr", "gpu_frags_lat", "gpu_frags_thr",
+                                                                "mode_switches")},
+                  "saturated_stalls_us": {"producer_late_max": sat["producer_late_max_ns"] / 1e3,
+                                          "tile_pass_max": sat["tile_pass_max_ns"] / 1e3,
+                                          "consumer_gap_max": sat["consumer_gap_max_ns"] / 1e3}}
             if mac_per_sig:
                 a = sat["frags_per_s"] * (mac_per_sig + MAC_DECOMP) / 1e12
                 rr["roofline"] = {"achieved": a, "peak": PEAK_TMAC, "unit": "TMAC/s", "frac": a / PEAK_TMAC,
@@ -474,8 +481,8 @@ def _txn_first_tag(p):
     """SHA-512 tag of a wire transaction's first signature: R = signature 0,
     A = account address 0, M = the message (fd_txn.h layout; the synthetic
     transactions have < 128 accounts, so every compact-u16 is one byte)."""
-    m = 1 + 64 * p[0]
-    a = m + (1 if p[m] & 0x80 else 0) + 4
+    m = 1 + 64 * int(p[0])
+    a = m + (1 if int(p[m]) & 0x80 else 0) + 4
     return int.from_bytes(hashlib.sha512(bytes(p[1:33]) + bytes(p[a:a + 32]) + bytes(p[m:])).digest()[:8], "little")
 
 

@@ -206,6 +206,11 @@ struct fd_verify_amd_tile {
   ulong                pass_max_ns;   /* longest pass of the last run's loop (stall diagnosis) */
   uint *               trace;  ulong trace_max;
   schar *              vlog;   ulong vlog_max;
+  /* the last persistent run's loop: passes, hand-offs, and the passes whose
+     staging stopped at the window, the output frames, batch_max staged,
+     or the STAGE_PASS bound (bench diagnostics) */
+  ulong                n_pass, n_hand, n_stop_window, n_stop_frames, n_stop_bmax, n_stop_pass;
+  volatile int         started;    /* the current run's kernel wrote its first clock word */
 };
 
 extern "C" void
@@ -975,6 +980,8 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   ulong in_cnt = diag->in_cnt, cons = out_seq0, fseq_pub = ~0UL;
   ulong ovrn = 0, bad = 0, ha = 0, ha_sz = 0, backp = 0, nbatch = 0, nsig = 0, switches = 0;
   ulong cdone = dbase;                   /* first descriptor not known to be finished */
+  ulong n_pass = 0, n_hand = 0, n_stop_window = 0, n_stop_frames = 0, n_stop_bmax = 0, n_stop_pass = 0;
+  t->started = 0;
   ulong iter = 0UL, pass_t = now_ns(), pass_max = 0UL, t_halt = 0UL;
   ulong t_chk = pass_t, g_seen = 0UL, t_prog = pass_t, gc_first = 0UL, gc_last = 0UL, gc_host = 0UL;
   ulong r_t0 = pass_t, r_n0 = staged;
@@ -989,7 +996,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
        pass: each store after a GPU read of the line is a cache-line
        ownership round trip */
     if( !(++iter & 63UL) ) beat( H );
-    if( !gc_first ) gc_first = __atomic_load_n( &H->gclock, __ATOMIC_ACQUIRE );
+    if( !gc_first && (gc_first = __atomic_load_n( &H->gclock, __ATOMIC_ACQUIRE )) ) t->started = 1;
     ulong const tn = now_ns();
     pass_max = std::max( pass_max, tn - pass_t ); pass_t = tn;
 
@@ -1014,10 +1021,11 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     /* 2. stage (at most STAGE_PASS frags, so hand-offs keep flowing) */
     bool full = false;
     ulong const stage_end = staged + STAGE_PASS;
+    n_pass++;
     uint const ts32 = (uint)tn;
     while( !done_in && staged - handed < t->batch_max && staged != stage_end ) {
       if( frag_cnt && in_seq - in_seq0 >= frag_cnt ) break;
-      if( staged - pubd >= W ) { full = true; break; }
+      if( staged - pubd >= W ) { full = true; n_stop_window++; break; }
       fd_frag_meta_t const * m = in_mcache + (in_seq & (in_depth-1UL));
       __builtin_prefetch( in_mcache + ((in_seq + 16UL) & (in_depth-1UL)) );
       ulong seq_found = __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE );
@@ -1034,7 +1042,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       /* reserve the next output frame: not in flight, and no longer read
          by a consumer that honours flow control */
       ulong fr = t->frame_next, f = t->frame_next_idx;
-      if( fr - retired >= F ) { full = true; break; }
+      if( fr - retired >= F ) { full = true; n_stop_frames++; break; }
       if( out_fseq && t->frame_pub[f] != FRAME_FREE && (long)(t->frame_pub[f] - cons) >= 0 ) {
         cons = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE );
         if( (long)(t->frame_pub[f] - cons) >= 0 ) { backp++; full = true; break; }
@@ -1071,6 +1079,8 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       t->ppend[staged & mask] = pending_t{ in_seq - 1UL, fr, (ushort)sz, (ushort)ctl, (uint)tsorig, (uint)f, ts32, 0u, 0u };
       staged++;
     }
+    n_stop_bmax += staged - handed >= t->batch_max;
+    n_stop_pass += staged == stage_end;
     __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
     if( in_fseq && !zc_dev && in_seq != fseq_pub ) { __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE ); fseq_pub = in_seq; }
     done_in = done_in || (frag_cnt && in_seq - in_seq0 >= frag_cnt);
@@ -1079,7 +1089,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     ulong const t3 = now_ns();
     if( t3 - r_t0 >= 200000UL ) {
       double inst = (double)(staged - r_n0) * 1e9 / (double)(t3 - r_t0);
-      rate = 0.5 * (rate + inst);
+      rate = rate > 0.0 ? 0.75 * rate + 0.25 * inst : inst;   /* ~0.8 ms memory: a burst does not flip the mode */
       r_t0 = t3; r_n0 = staged;
       int nthr = fd_verify_amd_tile_mode( t->cfg.chunk_mode, thr, rate, t->rate_hi, t->rate_lo );
       switches += nthr != thr;
@@ -1106,7 +1116,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
         }
         for( ulong c = handed; c < upto; c++ ) t->ppend[c & mask].t_hand = th | (thr ? 0u : 1u);   /* bit 0: latency chunk */
         t->desc_seq = ds;
-        nbatch++; nsig += upto - handed;
+        nbatch++; nsig += upto - handed; n_hand++;
         handed = upto;
         r.handed.store( handed, std::memory_order_release );
         __atomic_store_n( &H->head, ds, __ATOMIC_RELEASE );
@@ -1186,6 +1196,8 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   if( halted || rc ) diag->halt_drop_cnt += staged - r.pubd;
   t->ring_seq = staged;
   t->pass_max_ns = pass_max;
+  t->n_pass = n_pass; t->n_hand = n_hand; t->n_stop_window = n_stop_window; t->n_stop_frames = n_stop_frames;
+  t->n_stop_bmax = n_stop_bmax; t->n_stop_pass = n_stop_pass;
   __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
   if( in_fseq ) __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE );
   t->out_seq_end = r.out_seq;
@@ -1316,11 +1328,20 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   fd_verify_amd_diag_t diag; memset( &diag, 0, sizeof diag );
   int tile_rc = 0;
   ulong mism = 0, checked = 0, late_max = 0, gap_max = 0;
-  ulong t0 = now_ns();
+  ulong t0 = now_ns(), t_prod0 = 0UL;   /* the rate is timed from the producer's start */
 
   std::thread prod( [&]() {
     pin_to( 1 );
+    /* start once the tile's kernel runs (+2 ms): the launch of a run's
+       persistent kernel is not part of the stream's latency (a deployed
+       tile runs until halted); the TXN batch path has no kernel to wait for */
+    if( !txn ) {
+      ulong const w0 = now_ns();
+      while( !tile->started && !__atomic_load_n( &tile_rc, __ATOMIC_ACQUIRE ) && now_ns() - w0 < 5000000000UL ) { /* spin */ }
+      ulong const w1 = now_ns(); while( now_ns() - w1 < 2000000UL ) { /* spin */ }
+    }
     ulong p0 = now_ns(), cr = 0;   /* cr: first seq not covered by the cached credit */
+    __atomic_store_n( &t_prod0, p0, __ATOMIC_RELEASE );
     uint  tnow = 0;                /* saturated: one timestamp per 32 frags (the producer must outrun the tile) */
     ulong lim = writes ? std::min( depth, D ) : depth;
     ulong k = 0, fw = 0;           /* seq % pool_n, seq % D, kept incrementally (no division per frag) */
@@ -1399,11 +1420,12 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   prod.join(); cons.join();
   if( pin ) (void)pthread_setaffinity_np( pthread_self(), sizeof saved, &saved );
   ulong const pass_max = tile->pass_max_ns;
+  ulong const stg[6] = { tile->n_pass, tile->n_hand, tile->n_stop_window, tile->n_stop_frames, tile->n_stop_bmax, tile->n_stop_pass };
   fd_verify_amd_tile_delete( tile );
   free( dcache );
   if( rc ) return rc;
   ulong n = std::min( (ulong)diag.out_cnt, frag_cnt );
-  for( int k=0; k<32; k++ ) out[k] = 0.0;
+  for( int k=0; k<38; k++ ) out[k] = 0.0;
   /* decomposition (before lat is sorted: the samples are per published frag) */
   if( !parts.empty() && n ) {
     std::vector<uint> v[7];
@@ -1427,9 +1449,11 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
     out[30] = (double)n;
   }
   out[29] = (double)diag.mode_switch_cnt;
+  for( int k=0; k<6; k++ ) out[32 + k] = (double)stg[k];
   std::sort( lat.begin(), lat.begin() + (long)n );
   auto pct = [&]( double q ) -> double { return n && !lap ? (double)lat[ std::min( n-1UL, (ulong)(q * (double)n) ) ] : 0.0; };
-  out[0] = (double)diag.in_cnt / ((double)(t1 - t0) * 1e-9);
+  { ulong const ts = __atomic_load_n( &t_prod0, __ATOMIC_ACQUIRE );
+    out[0] = (double)diag.in_cnt / ((double)(t1 - (ts ? ts : t0)) * 1e-9); }
   out[1] = pct( 0.50 ); out[2] = pct( 0.99 ); out[3] = pct( 0.999 );
   out[4] = diag.batch_cnt ? (double)diag.batch_sig_cnt / (double)diag.batch_cnt : 0.0;
   out[5] = (double)diag.out_cnt; out[6] = (double)diag.sv_filt_cnt; out[7] = (double)diag.ovrn_cnt;

@@ -374,7 +374,11 @@ fd_verify_amd_tile_mode( int chunk_mode, int thr, double rate, double rate_hi, d
    the cut wait, queue wait, service, publish wait and input wait (latency
    minus the other four: producer publish -> staged), out[27] / out[28] =
    p50 service of latency / throughput chunks, out[29] = chunk-mode
-   switches, out[30] = frags traced, out[31] = 0.  out holds 32 doubles.
+   switches, out[30] = frags traced, out[31] = 0; out[32..37] = the run
+   loop's passes, hand-offs, and passes whose staging stopped at the
+   window, the output frames, batch_max staged frags and the per-pass
+   bound.  out holds 38 doubles.  Paced runs start once the tile's kernel
+   runs (+2 ms): a run's kernel launch is not part of the stream.
    Threads: producer, tile, the tile's publisher and consumer each pinned
    to a CPU of their own when the process may use 5 or more (else unpinned,
    publisher inline).  waves: the tile's cfg.waves (0: the device's share;
