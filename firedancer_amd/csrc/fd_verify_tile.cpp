@@ -1325,6 +1325,10 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   ulong in_fseq = 0UL;                                   /* the tile's credit to the producer */
   std::atomic<ulong> out_fseq( 0UL );                    /* consumer progress (the tile's output credit) */
   std::vector<uint> lat( frag_cnt );
+  /* steady state: published frags scheduled 20 ms or more after the
+     producer's start (paced runs; the consumer marks them from tsorig) */
+  std::vector<uchar> steady( check ? 0UL : frag_cnt, (uchar)0 );
+  ulong const warm_ns = 20000000UL;
   fd_verify_amd_diag_t diag; memset( &diag, 0, sizeof diag );
   int tile_rc = 0;
   ulong mism = 0, checked = 0, late_max = 0, gap_max = 0;
@@ -1376,6 +1380,10 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
       fd_frag_meta_t const * m = &out_mc[ seq & (out_depth-1UL) ];
       if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) == seq ) {
         if( !(seq & 15UL) ) { ulong tn = now_ns(); if( tl ) gap_max = std::max( gap_max, tn - tl ); tl = tn; }
+        if( !check && seq < frag_cnt && rate > 0.0 ) {
+          ulong const p0 = __atomic_load_n( &t_prod0, __ATOMIC_ACQUIRE );
+          steady[seq] = (uchar)((int)((uint)m->tsorig - (uint)(p0 + warm_ns)) >= 0);
+        }
         if( check ) {
           ulong tag = m->sig, chunk = m->chunk, sz = m->sz, s_in, k;
           if( lap ) {
@@ -1425,12 +1433,22 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   free( dcache );
   if( rc ) return rc;
   ulong n = std::min( (ulong)diag.out_cnt, frag_cnt );
-  for( int k=0; k<38; k++ ) out[k] = 0.0;
+  for( int k=0; k<40; k++ ) out[k] = 0.0;
   /* decomposition (before lat is sorted: the samples are per published frag) */
-  if( !parts.empty() && n ) {
+  /* paced runs: percentiles over the steady state (n_st samples); the
+     all-frags p50 / p99 go to out[38], out[39] */
+  std::vector<uint> lat_all;
+  ulong n_st = n;
+  if( !steady.empty() && rate > 0.0 ) {
+    lat_all.assign( lat.begin(), lat.begin() + (long)n );
+    n_st = 0;
+    for( ulong i=0; i<n; i++ ) if( steady[i] ) { lat[n_st] = lat[i]; if( !parts.empty() ) memmove( &parts[4*n_st], &parts[4*i], 16 ); n_st++; }
+    if( !n_st ) { n_st = n; lat.assign( lat_all.begin(), lat_all.end() ); lat.resize( frag_cnt ); }
+  }
+  if( !parts.empty() && n_st ) {
     std::vector<uint> v[7];
-    for( auto & x : v ) x.reserve( n );
-    for( ulong i=0; i<n; i++ ) {
+    for( auto & x : v ) x.reserve( n_st );
+    for( ulong i=0; i<n_st; i++ ) {
       uint const * p = parts.data() + 4UL * i;
       uint const svc = p[2] & 0x7fffffffu;
       ulong sum = (ulong)p[0] + p[1] + svc + p[3];
@@ -1446,12 +1464,17 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
     };
     for( int k=0; k<5; k++ ) { out[17 + 2*k] = q( v[k], 0.50 ); out[18 + 2*k] = q( v[k], 0.99 ); }
     out[27] = q( v[5], 0.50 ); out[28] = q( v[6], 0.50 );
-    out[30] = (double)n;
+    out[30] = (double)n_st;
   }
   out[29] = (double)diag.mode_switch_cnt;
   for( int k=0; k<6; k++ ) out[32 + k] = (double)stg[k];
-  std::sort( lat.begin(), lat.begin() + (long)n );
-  auto pct = [&]( double q ) -> double { return n && !lap ? (double)lat[ std::min( n-1UL, (ulong)(q * (double)n) ) ] : 0.0; };
+  std::sort( lat.begin(), lat.begin() + (long)n_st );
+  auto pct = [&]( double q ) -> double { return n_st && !lap ? (double)lat[ std::min( n_st-1UL, (ulong)(q * (double)n_st) ) ] : 0.0; };
+  if( !lat_all.empty() ) {
+    std::sort( lat_all.begin(), lat_all.end() );
+    out[38] = (double)lat_all[ std::min( n-1UL, (ulong)(0.50 * (double)n) ) ];
+    out[39] = (double)lat_all[ std::min( n-1UL, (ulong)(0.99 * (double)n) ) ];
+  }
   { ulong const ts = __atomic_load_n( &t_prod0, __ATOMIC_ACQUIRE );
     out[0] = (double)diag.in_cnt / ((double)(t1 - (ts ? ts : t0)) * 1e-9); }
   out[1] = pct( 0.50 ); out[2] = pct( 0.99 ); out[3] = pct( 0.999 );

@@ -377,8 +377,11 @@ fd_verify_amd_tile_mode( int chunk_mode, int thr, double rate, double rate_hi, d
    switches, out[30] = frags traced, out[31] = 0; out[32..37] = the run
    loop's passes, hand-offs, and passes whose staging stopped at the
    window, the output frames, batch_max staged frags and the per-pass
-   bound.  out holds 38 doubles.  Paced runs start once the tile's kernel
-   runs (+2 ms): a run's kernel launch is not part of the stream.
+   bound.  Paced runs start once the tile's kernel runs (+2 ms): a run's
+   kernel launch is not part of the stream; their latency percentiles
+   (out[1..3], out[17..28]) cover the steady state, the frags scheduled
+   20 ms or more after the start, and out[38] / out[39] = p50 / p99 of every
+   frag.  out holds 40 doubles.
    Threads: producer, tile, the tile's publisher and consumer each pinned
    to a CPU of their own when the process may use 5 or more (else unpinned,
    publisher inline).  waves: the tile's cfg.waves (0: the device's share;

@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from firedancer_amd import ed25519, hip, tango, workload  # noqa: E402
 
 what = sys.argv[1] if len(sys.argv) > 1 else "both"
-pub, sig, off, sz, blob = workload.sig_batch(1 << 14, 200, 9)
+pub, sig, off, sz, blob = workload.sig_batch(1 << 16, 200, 9)
 if what in ("tile", "both"):
     r = tango.bench_stream(0, 16384, 0, pub, sig, off, sz, blob, 1 << 20, zero_copy=True)
     print("tile", {k: round(v) for k, v in r.items()}, flush=True)
