@@ -462,9 +462,28 @@ struct evq {
  * takes one more step (PH_FIN): its p1p1->p2 result is R', compared with
  * the limb memcmp of fd_ed25519_user.c:417-425, then it idles (PH_DONE).
  */
+/* Streaming tile (k_tile_persist): the wave's issue priority follows the
+   age of its chunk, claimed at s_memrealtime tc (100 MHz): 0 below 0.4 ms,
+   then one level per 0.4 ms.  Two waves share a SIMD, and at equal priority
+   the arbiter prefers the older WAVE -- in a persistent kernel always the
+   same one, so one wave of each pair ran its chunks ~1.1 ms and the other
+   ~5 ms, and the tile publishes in order behind the slow ones.  By chunk age
+   the older CHUNK goes first.  Scalar only (SGPRs, s_setprio). */
+__device__ __forceinline__ void
+tile_age_prio( u64 tc, u32 & lvl ) {
+  u64 const el = __builtin_amdgcn_s_memrealtime() - tc;
+  u32 const want = el < 40000UL ? 0u : el < 80000UL ? 1u : el < 120000UL ? 2u : 3u;
+  if( want == lvl ) return;
+  lvl = want;
+  if( want == 1u )      __builtin_amdgcn_s_setprio( 1 );
+  else if( want == 2u ) __builtin_amdgcn_s_setprio( 2 );
+  else if( want == 3u ) __builtin_amdgcn_s_setprio( 3 );
+  else                  __builtin_amdgcn_s_setprio( 0 );
+}
+
 __device__ __forceinline__ void
 dsm_lane_body( u32 i, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats,
-               i32 (* __restrict__ bi)[48], u64 (* __restrict__ evl)[33] ) {
+               i32 (* __restrict__ bi)[48], u64 (* __restrict__ evl)[33], u64 tc = 0UL ) {
   /* bi: the base-point table in the Ai slab's row layout (bi12_fill), so
      ADD-A and ADD-B operands load alike */
   bool act = (i < n) && (err[i] == 1);
@@ -531,8 +550,10 @@ dsm_lane_body( u32 i, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_lay
 # define Q_SET( R_, K_, V_ ) ( q[R_].v[K_] = (V_) )
   p1p1 t;   /* identity as a completed point: p1p1->p3 gives (0,1,1,0) */
   t.X = fe_zero(); t.Y = fe_one(); t.Z = fe_one(); t.T = fe_one();
+  u32 lvl = 0u;
 
   for( ;; ) {
+    if( tc ) tile_age_prio( tc, lvl );
     /* p1p1 -> p3 (its X,Y,Z are the reference's p1p1 -> p2) */
     p3 u = ge_p1p1_to_p3_fold( t );
 
@@ -1159,7 +1180,7 @@ quad8_body_ownc5( fe & C, fe5 const & pm, fe const & qrow, bool isD, bool neg, u
    Also the streaming tile's latency chunks (k_tile_persist). */
 __device__ __forceinline__ void
 dsm8_body( u32 gt, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats,
-           i32 (* __restrict__ bi12)[48], u64 (* __restrict__ evl)[33] ) {
+           i32 (* __restrict__ bi12)[48], u64 (* __restrict__ evl)[33], u64 tc = 0UL ) {
   u32 i = gt >> 3;
   int qd = (int)(threadIdx.x & 3u);
   int hh = (int)((threadIdx.x >> 2) & 1u);            /* which half of every field mul this lane computes */
@@ -1197,8 +1218,10 @@ dsm8_body( u32 gt, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout
   bool qneg = false;
   fe qrow = fe_zero();
   fe C = (qd == 2) ? fe_zero() : fe_one();   /* identity: own coordinate (Z, T, X, Y)[q] = (1, 1, 0, 1) */
+  u32 lvl = 0u;
 
   for( ;; ) {
+    if( tc ) tile_age_prio( tc, lvl );
     fe5 pm5 = quad8_p3_ownc5( C, H );          /* q0 u.Z, q1 u.Y, q2 u.X, q3 u.T (split limbs) */
 
     bool fin = (ph == PH_FIN);
@@ -1916,6 +1939,7 @@ size_t fd_amd_tile_scratch_stride( void ) { return tile_scratch_layout().total; 
    watchdog). */
 __device__ __noinline__ void
 tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog ) {
+  __builtin_amdgcn_s_setprio( 3 );   /* beside the workers' aged chunks on its SIMD */
   u64 word = ld_dev64( &D->mw[0].w ), lastb = ~0UL, beat = 0UL;
   u64 tb = __builtin_amdgcn_s_memrealtime(), tpub = tb, tclk = tb;
   st_sys64( &H->gclock, tb );
@@ -1950,7 +1974,8 @@ __device__ __forceinline__ void
 tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __restrict__ scr, ws_layout_t L,
             tile_scratch_t const & S, i32 (* __restrict__ bi)[48], u64 (* __restrict__ evl)[33], u64 * pt, u64 tc ) {
   /* pt (A.prof, set by the diagnostics build's host only): s_memrealtime
-     ticks spent in gather, prep + decomp, DSM, results; wave-uniform */
+     ticks spent in gather [0], prep [6], decomp [1], DSM [2], results [3];
+     wave-uniform */
   u64 ts = A.prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
 # define TILE_STAMP( k_ ) do { if( A.prof ) { u64 t_ = __builtin_amdgcn_s_memrealtime(); if( !threadIdx.x ) pt[k_] += t_ - ts; ts = t_; } } while(0)
   /* opaque per chunk: otherwise the compiler hoists every per-lane address
@@ -2007,12 +2032,14 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __rest
   /* 3. the verify pipeline on the chunk (k_prep, k_decomp, k_dsm8 / k_dsm bodies) */
   prep_body( l, k, pub, sig, off, sz, mir, err, ws, L, (i8 const *)0 );
   __syncthreads();
+  TILE_STAMP( 6 );
   decomp_body( l, k, pub, sig, err, ws, L, true );                 /* points 0..63: signatures 0..31 */
   if( k > 32u ) decomp_body( l + 64u, k, pub, sig, err, ws, L, true );
   __syncthreads();
   TILE_STAMP( 1 );
-  if( eight ) dsm8_body( l, k, err, ws, L, 0, bi, evl );
-  else        dsm_lane_body( l, k, err, ws, L, 0, bi, evl );
+  if( eight ) dsm8_body( l, k, err, ws, L, 0, bi, evl, tc );
+  else        dsm_lane_body( l, k, err, ws, L, 0, bi, evl, tc );
+  __builtin_amdgcn_s_setprio( 0 );
   __syncthreads();
   TILE_STAMP( 2 );
   /* 4. results: tags (and, zero-copy, the output frames above) first, one
@@ -2120,7 +2147,9 @@ k_tile_synth( fd_amd_tile_args_t A, u32 iters, u32 eight ) {
   __shared__ u64 evl[64][33];
   bi12_fill( bi );
   __syncthreads();
-  u64 pt[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
+  __shared__ u64 pt[8];
+  if( threadIdx.x < 8u ) pt[threadIdx.x] = 0UL;
+  __syncthreads();
   u32 const k = eight ? 8u : 64u;
   if( A.hctl && blockIdx.x == gridDim.x - 1u ) {
     /* A/B: a scout-like wave polling the host control words until the
@@ -2140,6 +2169,9 @@ k_tile_synth( fd_amd_tile_args_t A, u32 iters, u32 eight ) {
   u8 * scr = A.scratch + (size_t)blockIdx.x * S.total;
   for( u32 it = 0; it < iters; it++ )
     tile_chunk( A, ((u64)blockIdx.x * iters + it) * k, k, eight != 0u, scr, L, S, bi, evl, pt, 0UL );
+  if( A.prof && threadIdx.x == 0u ) {
+    _Pragma("unroll") for( int q=0; q<8; q++ ) atomicAdd( (unsigned long long *)&A.dctl->prof[q], (unsigned long long)pt[q] );
+  }
   if( A.hctl && threadIdx.x == 0u ) atomicAdd( (unsigned long long *)&A.dctl->stat[0], 1ULL );
 }
 

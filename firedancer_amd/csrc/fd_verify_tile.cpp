@@ -348,6 +348,27 @@ fd_verify_amd_tile_delete( fd_verify_amd_tile_t * t ) {
   delete t;
 }
 
+/* Copy mode's staging copy: whole 16-B words (a frag's chunks are 64-B
+   granular, so the rounded-up tail stays inside its own chunks) with
+   non-temporal stores -- the frame is read next by the GPU over PCIe, not by
+   this CPU, so it skips the read-for-ownership of every destination line and
+   stays out of the cache.  Weakly ordered: the stager fences (sfence) before
+   it publishes the head that hands the frames over. */
+static inline void
+stage_copy_nt( uchar * dst, uchar const * src, ulong sz ) {
+  ulong const n = (sz + 15UL) >> 4;
+  __m128i const * s = (__m128i const *)src;
+  __m128i * d = (__m128i *)dst;
+  ulong k = 0;
+  for( ; k + 4UL <= n; k += 4UL ) {
+    __m128i const a = _mm_loadu_si128( s + k ), b = _mm_loadu_si128( s + k + 1 );
+    __m128i const c = _mm_loadu_si128( s + k + 2 ), e = _mm_loadu_si128( s + k + 3 );
+    _mm_stream_si128( d + k, a ); _mm_stream_si128( d + k + 1, b );
+    _mm_stream_si128( d + k + 2, c ); _mm_stream_si128( d + k + 3, e );
+  }
+  for( ; k < n; k++ ) _mm_stream_si128( d + k, _mm_loadu_si128( s + k ) );
+}
+
 /* The persistent window rule: frags handed over and not yet published */
 static ulong
 tile_window( fd_verify_amd_tile_cfg_t const * c ) {
@@ -643,7 +664,7 @@ tile_run_batched( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
         /* copy mode: the frame is the tile's copy; a frag lapped while it
            was copied is dropped (speculative read, then seq re-check) */
         uint8_t * dst = t->out_base + f * FD_VERIFY_AMD_FRAME_SZ;
-        memcpy( dst, p, sz );
+        stage_copy_nt( dst, p, sz );
         __atomic_thread_fence( __ATOMIC_ACQUIRE );
         if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != in_seq ) { diag->ovrn_cnt++; in_seq++; continue; }
         p = dst;
@@ -1059,7 +1080,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
         /* copy mode: the frame is the tile's copy; a frag lapped while it
            was copied is dropped (speculative read, then seq re-check) */
         uint8_t * dst = t->out_base + f * FD_VERIFY_AMD_FRAME_SZ;
-        memcpy( dst, p, sz );
+        stage_copy_nt( dst, p, sz );
         __atomic_thread_fence( __ATOMIC_ACQUIRE );
         if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != in_seq ) { ovrn++; in_seq++; continue; }
         p = dst;
@@ -1119,6 +1140,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
         nbatch++; nsig += upto - handed; n_hand++;
         handed = upto;
         r.handed.store( handed, std::memory_order_release );
+        if( !zc_dev ) _mm_sfence();   /* the staged copies (non-temporal stores) before the head */
         __atomic_store_n( &H->head, ds, __ATOMIC_RELEASE );
       }
     }
@@ -1259,7 +1281,16 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   bool lap       = writes && (flags & FD_VERIFY_AMD_BENCH_LAP);
   bool check     = expect_err && expect_tag;
   ulong byte_mask = (flags & FD_VERIFY_AMD_BENCH_SAMPLE_BYTES) ? 15UL : 0UL;   /* compare bytes of every 16th frag */
-  ulong depth = 1UL; while( depth < 8UL*batch_max + 1024UL ) depth <<= 1;   /* > batches in flight + staging */
+  /* input depth > the frags the tile holds (zero copy releases a frag to the
+     producer only once published: a depth under the tile's window would
+     bound the stream instead of the tile); the rewriting modes keep 8
+     batches (their dcache is sized past the depth) */
+  ulong depth_min = 8UL*batch_max + 1024UL;
+  if( !writes ) {
+    fd_verify_amd_tile_cfg_t wc; fd_verify_amd_tile_cfg_default( &wc ); wc.batch_max = batch_max;
+    depth_min = std::max( depth_min, tile_window( &wc ) + 4096UL );
+  }
+  ulong depth = 1UL; while( depth < depth_min ) depth <<= 1;
   ulong out_depth = 1UL; while( out_depth < 2UL*batch_max + 1024UL ) out_depth <<= 1;
   ulong const frame = FD_VERIFY_AMD_FRAME_SZ, frame_c = FRAME_CHUNKS;
   /* Data region: either every pool frame once (what a NIC would have
@@ -1541,11 +1572,20 @@ fd_amd_tile_synth( int device, uint32_t waves, uint32_t iters, int eight, uint32
   if( h_ctl ) memset( h_ctl, 0, sizeof(fd_amd_tile_hctl_t) );
   A.ent = d_ent; A.res_tag = d_res; A.res_word = d_res + R; A.mask = R - 1UL; A.src = d_fr; A.out = NULL; A.dctl = d_ctl; A.scratch = d_scr;
   A.hctl = (fd_amd_tile_hctl_t *)h_ctl_dev; A.watchdog = 1000000000UL;
+  A.prof = (where & 32u) ? 1u : 0u;     /* per-phase clocks of every chunk, summed (stderr) */
   if( hipEventRecord( e0, st ) != hipSuccess || fd_amd_launch_tile_synth( &A, waves + (h_ctl ? 1u : 0u), iters, eight, st ) ||
       hipEventRecord( e1, st ) != hipSuccess || hipStreamSynchronize( st ) != hipSuccess ||
       hipEventElapsedTime( &ms, e0, e1 ) != hipSuccess ||
       hipMemcpy( res.data(), hm[1] ? hm[1] : (void *)d_res, 2UL * R * sizeof(uint64_t), hipMemcpyDefault ) != hipSuccess ) goto done;
   *out_ms = (double)ms;
+  if( A.prof ) {
+    fd_amd_tile_dctl_t dc;
+    if( hipMemcpy( &dc, d_ctl, sizeof dc, hipMemcpyDeviceToHost ) != hipSuccess ) goto done;
+    /* s_memrealtime runs at 100 MHz: per chunk per wave, in us */
+    double const c = (double)waves * iters * 100.;
+    fprintf( stderr, "tile_synth prof (us per chunk): gather %.1f prep %.1f decomp %.1f dsm %.1f results %.1f\n",
+             (double)dc.prof[0] / c, (double)dc.prof[6] / c, (double)dc.prof[1] / c, (double)dc.prof[2] / c, (double)dc.prof[3] / c );
+  }
   for( ulong j=0; j<n; j++ ) verdict[j] = (res[R + j] >> 8) == j + 1UL ? (int8_t)(uint8_t)(res[R + j] & 0xffUL) : (int8_t)99;
   rc = FD_ED25519_AMD_OK;
 done:
