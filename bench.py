@@ -456,7 +456,9 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
             for load in (0.5, 0.8):
                 rr["at_%d%%" % int(load * 100)] = paced(bmax, zc, load * sat["frags_per_s"])
             lo, hi = rr["at_50%"], rr["at_80%"]
-            rr["p50_nondecreasing_with_load"] = hi["p50_us"] >= lo["p50_us"]
+            # within 1 %: the p50 of one row at a fixed load moves by ~0.5 % run to run
+            # (profiles/r04_bench_tile_*.json), and both loads run throughput chunks
+            rr["p50_nondecreasing_with_load"] = hi["p50_us"] >= 0.99 * lo["p50_us"]
             rr["p99_within_2_5x_p50"] = max(lo["p99_over_p50"], hi["p99_over_p50"]) <= 2.5
             row[key] = rr
         rows.append(row)
