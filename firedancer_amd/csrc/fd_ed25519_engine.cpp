@@ -827,3 +827,95 @@ extern "C" char const *
 fd_ed25519_amd_version( void ) {
   return "fd_ed25519_amd 0.3 (gfx950; k_prep/k_decomp/k_dsm + k_front/k_dsm8/k_dsm4, txn front end, verify tile, multi-device, GPU signer)";
 }
+
+#ifdef FD_AMD_DIAG
+#include <time.h>
+#include <x86intrin.h>
+#include <algorithm>
+/* Diagnostics build only.  Latency-path A/B (profiles/r04_latency_ab.txt):
+   one n-signature batch resident in HBM, verified `iters` times per way of
+   launching and waiting, each call timed on the host clock:
+     mode 0  k_front + k_dsm8 launched on a stream, hipEventSynchronize
+     mode 1  the same launches, host spins on the verdicts k_dsm8 writes
+             into mapped memory
+     mode 2  the two launches captured once into a hipGraph, hipGraphLaunch
+             + hipEventSynchronize
+     mode 3  hipGraphLaunch + spin on the mapped verdicts
+   out[4*m + 0..3] = p50 / p99 / min us of mode m and its GPU time (events
+   around the launches, p50).  Every call's verdicts must equal the first
+   call's (checked; ERR_DEVICE otherwise). */
+extern "C" int
+fd_amd_latency_ab( int device, uint32_t n, uint8_t const * pub, uint8_t const * sig, uint32_t const * off,
+                   uint32_t const * sz, uint8_t const * blob, uint64_t blob_sz, uint32_t iters, double * out ) {
+  if( !n || !iters || !out || !fd_amd_uses_latency_path( n, 0 ) ) return FD_ED25519_AMD_ERR_INVAL;
+  if( hipSetDevice( device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  int rc = FD_ED25519_AMD_ERR_DEVICE;
+  uint8_t * d_in = NULL, * d_ws = NULL; int8_t * d_err = NULL, * h_out = NULL, * d_out = NULL;
+  hipStream_t st = NULL; hipEvent_t e0 = NULL, e1 = NULL, ed = NULL;
+  hipGraph_t g = NULL; hipGraphExec_t ge = NULL;
+  ulong const in_sz = 104UL*n + blob_sz;
+  std::vector<int8_t> first( n );
+  std::vector<double> t( iters ), gt( iters );
+  ws_layout_t const L = fd_amd_ws_layout( n );
+  uint8_t * p_pub, * p_sig, * p_blob; uint32_t * p_off, * p_sz;
+  auto now = []() { struct timespec ts; clock_gettime( CLOCK_MONOTONIC, &ts ); return (double)ts.tv_sec * 1e6 + (double)ts.tv_nsec * 1e-3; };
+  if( hipMalloc( (void **)&d_in, in_sz ) != hipSuccess || hipMalloc( (void **)&d_ws, L.total ) != hipSuccess ||
+      hipMalloc( (void **)&d_err, n ) != hipSuccess ||
+      hipHostMalloc( (void **)&h_out, n, hipHostMallocMapped | hipHostMallocCoherent ) != hipSuccess ||
+      hipHostGetDevicePointer( (void **)&d_out, h_out, 0 ) != hipSuccess ||
+      hipStreamCreateWithFlags( &st, hipStreamNonBlocking ) != hipSuccess ||
+      hipEventCreate( &e0 ) != hipSuccess || hipEventCreate( &e1 ) != hipSuccess || hipEventCreate( &ed ) != hipSuccess )
+    goto done;
+  p_pub = d_in; p_sig = d_in + 32UL*n; p_off = (uint32_t *)(d_in + 96UL*n); p_sz = (uint32_t *)(d_in + 100UL*n); p_blob = d_in + 104UL*n;
+  if( hipMemcpy( p_pub, pub, 32UL*n, hipMemcpyHostToDevice ) != hipSuccess ||
+      hipMemcpy( p_sig, sig, 64UL*n, hipMemcpyHostToDevice ) != hipSuccess ||
+      hipMemcpy( p_off, off, 4UL*n, hipMemcpyHostToDevice ) != hipSuccess ||
+      hipMemcpy( p_sz, sz, 4UL*n, hipMemcpyHostToDevice ) != hipSuccess ||
+      ( blob_sz && hipMemcpy( p_blob, blob, blob_sz, hipMemcpyHostToDevice ) != hipSuccess ) ) goto done;
+  /* the graph: the same two launches, captured */
+  if( hipStreamBeginCapture( st, hipStreamCaptureModeThreadLocal ) != hipSuccess ) goto done;
+  if( fd_amd_launch_verify( n, p_pub, p_sig, p_off, p_sz, p_blob, d_err, d_ws, st, 0, NULL, NULL, 0, d_out ) ) {
+    (void)hipStreamEndCapture( st, &g ); goto done;
+  }
+  if( hipStreamEndCapture( st, &g ) != hipSuccess || hipGraphInstantiate( &ge, g, NULL, NULL, 0 ) != hipSuccess ) goto done;
+  for( int m=0; m<4; m++ ) {
+    bool const graph = m >= 2, spin = m & 1;
+    for( uint32_t it=0; it<iters + 8u; it++ ) {   /* 8 untimed warm-up calls */
+      memset( h_out, 0x7f, n );
+      double const a = now();
+      if( hipEventRecord( e0, st ) != hipSuccess ) goto done;
+      if( graph ) { if( hipGraphLaunch( ge, st ) != hipSuccess ) goto done; }
+      else if( fd_amd_launch_verify( n, p_pub, p_sig, p_off, p_sz, p_blob, d_err, d_ws, st, 0, NULL, NULL, 0, d_out ) ) goto done;
+      if( hipEventRecord( e1, st ) != hipSuccess ) goto done;
+      if( spin ) {
+        /* every verdict lands in mapped memory; wait for the last unwritten one */
+        for( uint32_t j=0; j<n; ) { if( ((int8_t volatile *)h_out)[j] != (int8_t)0x7f ) j++; else _mm_pause(); }
+      } else if( hipEventSynchronize( e1 ) != hipSuccess ) goto done;
+      double const b = now();
+      if( hipEventSynchronize( e1 ) != hipSuccess ) goto done;
+      float ms = 0.f;
+      if( hipEventElapsedTime( &ms, e0, e1 ) != hipSuccess ) goto done;
+      if( m == 0 && it == 0 ) memcpy( first.data(), h_out, n );
+      else if( memcmp( first.data(), h_out, n ) ) { fprintf( stderr, "fd_amd_latency_ab: verdicts differ (mode %d call %u)\n", m, it ); goto done; }
+      if( it >= 8u ) { t[it - 8u] = b - a; gt[it - 8u] = 1e3 * (double)ms; }
+    }
+    std::sort( t.begin(), t.end() ); std::sort( gt.begin(), gt.end() );
+    out[4*m + 0] = t[iters / 2]; out[4*m + 1] = t[std::min( (ulong)iters - 1UL, (ulong)(0.99 * iters) )];
+    out[4*m + 2] = t[0]; out[4*m + 3] = gt[iters / 2];
+  }
+  rc = FD_ED25519_AMD_OK;
+done:
+  if( st ) (void)hipStreamSynchronize( st );
+  if( ge ) (void)hipGraphExecDestroy( ge );
+  if( g ) (void)hipGraphDestroy( g );
+  if( e0 ) (void)hipEventDestroy( e0 );
+  if( e1 ) (void)hipEventDestroy( e1 );
+  if( ed ) (void)hipEventDestroy( ed );
+  if( st ) (void)hipStreamDestroy( st );
+  if( h_out ) (void)hipHostFree( h_out );
+  if( d_in ) (void)hipFree( d_in );
+  if( d_ws ) (void)hipFree( d_ws );
+  if( d_err ) (void)hipFree( d_err );
+  return rc;
+}
+#endif /* FD_AMD_DIAG */

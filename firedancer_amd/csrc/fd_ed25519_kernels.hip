@@ -1355,7 +1355,10 @@ __device__ u32 g_pool_dbg[4];   /* steps, live lanes, ADD steps, refill-only ste
 __device__ u64 g_pool_dbg_t[8192][4];   /* per wave: wall_clock64 at start, at exhaustion of the counter, at exit; steps after exhaustion | lanes << 32 */
 #endif
 
-__global__ void __launch_bounds__(64)
+#ifndef FD_AI_WAVES
+#define FD_AI_WAVES 2
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FD_AI_WAVES)))
 k_ai( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L ) {
   if( blockIdx.x == 0 ) {
     for( int k=threadIdx.x; k<8*48; k+=64 ) {
@@ -1482,6 +1485,10 @@ pool_store_ts( PTR s, u32 stride, p1p1 const & t ) {
 #ifndef FD_POOL_DBL_PCT
 #define FD_POOL_DBL_PCT 100u
 #endif
+/* k_dsmp's drain: issue priority by the signatures left in the pool */
+#ifndef FD_POOL_DRAIN_PRIO
+#define FD_POOL_DRAIN_PRIO 1
+#endif
 /* free slots that trigger a refill (one counter atomic + init loads) */
 #ifndef FD_POOL_REFILL
 #define FD_POOL_REFILL 8u
@@ -1569,6 +1576,18 @@ k_dsmp( u32 n, u8 * __restrict__ ws, ws_layout_t L, u64 iter_cap ) {
       if( !more ) { guard = false; break; }   /* pool empty, nothing left to take */
       continue;
     }
+#if FD_POOL_DRAIN_PRIO
+    /* drain: the wave with more signatures left issues first on its SIMD
+       (at equal priority the arbiter prefers the older wave, whatever its
+       pool holds), so the two waves of a SIMD empty their pools together */
+    if( !more ) {
+      u32 const left = nD + nA;
+      if( left > 84u )      __builtin_amdgcn_s_setprio( 3 );
+      else if( left > 56u ) __builtin_amdgcn_s_setprio( 2 );
+      else if( left > 28u ) __builtin_amdgcn_s_setprio( 1 );
+      else                  __builtin_amdgcn_s_setprio( 0 );
+    }
+#endif
 
     u32 kD = nD < 64u ? nD : 64u, kM = (nD + nA) < 64u ? (nD + nA) : 64u;
     bool mixed;
