@@ -182,7 +182,8 @@ typedef struct {
   ulong waves;            /* 0: the device's share */
   int   chunk_mode;       /* FD_VERIFY_AMD_CHUNK_* */
   int   publish_cpu;      /* FD_VERIFY_AMD_PUBLISH_AUTO / _INLINE, or a CPU */
-  ulong window;           /* 0: default */
+  ulong window;           /* frags in flight; 0: 2^18 from batch_max 4096, 2^17 from 1024,
+                             else max( 64 x batch_max, 2^13 ) */
   ulong lat_fill_ns;
   ulong lat_free_chunks;
   ulong chunk_wait_ns;
