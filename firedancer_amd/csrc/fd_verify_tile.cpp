@@ -227,6 +227,7 @@ fd_verify_amd_tile_cfg_default( fd_verify_amd_tile_cfg_t * c ) {
   c->lat_free_chunks = 0UL;         /* resolved to CUs / 2 at creation */
   c->chunk_wait_ns = 50000UL;
   c->halt_grace_ns = 50000000UL;
+  c->copy_cpu = FD_VERIFY_AMD_COPY_INLINE;
 }
 
 extern "C" int
@@ -369,6 +370,38 @@ stage_copy_nt( uchar * dst, uchar const * src, ulong sz ) {
   for( ; k < n; k++ ) _mm_stream_si128( d + k, _mm_loadu_si128( s + k ) );
 }
 
+/* Copy mode's deferred staging: a pass first reserves a frame per frag and
+   lists the copies, then copies them -- half on the copy helper thread when
+   the tile has one and the pass is large enough -- and only then re-checks
+   each frag's mcache line and stages it (a frag lapped during its copy
+   leaves its frame unused). */
+struct copy_job_t {
+  uchar *                dst;
+  uchar const *          src;
+  fd_frag_meta_t const * m;
+  ulong                  seq, fr, sz, tag;   /* tag: the HA dedup tag, read from the source */
+  uint                   f, tsorig;
+  ushort                 ctl;
+};
+
+#define COPY_SPLIT_MIN (32UL)   /* passes of fewer frags are copied on the stager alone */
+
+struct copier_t {
+  alignas(64) std::atomic<ulong> gen;    /* stager -> helper: a new job range */
+  alignas(64) std::atomic<ulong> done;   /* helper -> stager: the range of gen `done` is copied */
+  alignas(64) copy_job_t const * jobs;
+  ulong                          lo, hi;
+  std::atomic<int>               quit;
+};
+
+static void
+copy_jobs( copy_job_t const * j, ulong lo, ulong hi ) {
+  for( ulong k=lo; k<hi; k++ ) {
+    if( k + 2UL < hi ) for( ulong o = 0; o < j[k+2].sz; o += 64UL ) __builtin_prefetch( j[k+2].src + o );
+    stage_copy_nt( j[k].dst, j[k].src, j[k].sz );
+  }
+}
+
 /* The persistent window rule: frags handed over and not yet published */
 static ulong
 tile_window( fd_verify_amd_tile_cfg_t const * c ) {
@@ -393,10 +426,16 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
   uint32_t waves = tile_share( t );
   if( waves < 2u || waves > 65536u ) return FD_ED25519_AMD_ERR_INVAL;
   t->window = W; t->R = R; t->waves = waves;
-  /* latency chunks' capacity: one 8-frag chunk per SIMD at ~0.45 ms */
-  double const cap = (double)std::min( (ulong)waves - 1UL, 4UL * (ulong)t->cus ) * 8.0 / 450e-6;
-  t->rate_hi = t->cfg.thr_rate_hi ? (double)t->cfg.thr_rate_hi : 0.55 * cap;
-  t->rate_lo = t->cfg.thr_rate_lo ? (double)t->cfg.thr_rate_lo : 0.40 * cap;
+  /* latency chunks' capacity: one 8-frag chunk per SIMD at ~0.45 ms, and
+     the window over their ~0.55 ms in flight.  Throughput chunks keep a frag
+     in flight 1.3-2.2 ms, so a small window caps them at W / 2 ms: when that
+     is below the latency chunks' capacity the tile stays in latency chunks
+     (batch_max 256: 8 M vs 18 M frags/s) */
+  double const cap  = std::min( (double)std::min( (ulong)waves - 1UL, 4UL * (ulong)t->cus ) * 8.0 / 450e-6,
+                                (double)W / 550e-6 );
+  bool const   thr_ok = (double)W / 2e-3 > cap;
+  t->rate_hi = t->cfg.thr_rate_hi ? (double)t->cfg.thr_rate_hi : thr_ok ? 0.55 * cap : HUGE_VAL;
+  t->rate_lo = t->cfg.thr_rate_lo ? (double)t->cfg.thr_rate_lo : thr_ok ? 0.40 * cap : HUGE_VAL;
   if( t->rate_lo > t->rate_hi ) t->rate_lo = t->rate_hi;
   unsigned const hf = hipHostMallocMapped | hipHostMallocCoherent;
   /* The run's kernel occupies its hardware queue for the whole run, and HIP
@@ -457,6 +496,7 @@ fd_verify_amd_tile_new_cfg( fd_verify_amd_tile_cfg_t const * cfg ) {
   if( c.framing == FD_VERIFY_AMD_FRAMING_TXN && c.batch_max < TXN_SIG_MAX_AT_MTU ) return NULL;
   if( c.chunk_mode < FD_VERIFY_AMD_CHUNK_AUTO || c.chunk_mode > FD_VERIFY_AMD_CHUNK_THROUGHPUT ) return NULL;
   if( c.publish_cpu < FD_VERIFY_AMD_PUBLISH_AUTO || c.publish_cpu >= CPU_SETSIZE ) return NULL;
+  if( c.copy_cpu < FD_VERIFY_AMD_COPY_INLINE || c.copy_cpu >= CPU_SETSIZE ) return NULL;
   if( c.waves == 1UL || c.waves > 65536UL ) return NULL;
   int cus = 0;
   if( hipDeviceGetAttribute( &cus, hipDeviceAttributeMultiprocessorCount, c.device ) != hipSuccess || cus <= 0 ) return NULL;
@@ -1002,6 +1042,36 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   }
   bool const inline_pub = !pub.joinable();
 
+  /* copy mode's helper: a thread of its own when cfg.copy_cpu names a CPU */
+  copier_t cpy;
+  cpy.gen.store( 0UL ); cpy.done.store( 0UL ); cpy.quit.store( 0 ); cpy.jobs = NULL; cpy.lo = cpy.hi = 0UL;
+  std::thread cth;
+  if( !zc_dev && t->cfg.copy_cpu >= 0 ) {
+    int const cpu = t->cfg.copy_cpu;
+    try {
+      cth = std::thread( [&cpy, cpu]() {
+        cpu_set_t one; CPU_ZERO( &one ); CPU_SET( cpu, &one );
+        (void)pthread_setaffinity_np( pthread_self(), sizeof one, &one );
+        ulong seen = 0UL;
+        for( ;; ) {
+          ulong const g = cpy.gen.load( std::memory_order_acquire );
+          if( g != seen ) {
+            seen = g;
+            copy_jobs( cpy.jobs, cpy.lo, cpy.hi );
+            _mm_sfence();   /* the copies before the stager sees them done */
+            cpy.done.store( g, std::memory_order_release );
+            continue;
+          }
+          if( cpy.quit.load( std::memory_order_acquire ) ) break;
+          _mm_pause();
+        }
+      } );
+    } catch( ... ) {}
+  }
+  copier_t * const cp = cth.joinable() ? &cpy : NULL;
+  ulong cgen = 0UL;
+  std::vector<copy_job_t> jobs( zc_dev ? 0UL : STAGE_PASS );
+
   ulong in_seq = in_seq0, staged = base, handed = base;
   ulong in_cnt = diag->in_cnt, cons = out_seq0, fseq_pub = ~0UL;
   ulong ovrn = 0, bad = 0, ha = 0, ha_sz = 0, backp = 0, nbatch = 0, nsig = 0, switches = 0;
@@ -1044,14 +1114,18 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     if( done_in && pubd == staged ) break;
     if( t_halt && tn - t_halt > t->cfg.halt_grace_ns ) { halted = true; break; }
 
-    /* 2. stage (at most STAGE_PASS frags, so hand-offs keep flowing) */
+    /* 2. stage (at most STAGE_PASS frags, so hand-offs keep flowing).  Copy
+          mode lists the pass's copies first (a frame reserved per frag),
+          copies them -- half on the copy helper when there is one -- and
+          then re-checks and stages each frag in input order */
     bool full = false;
     ulong const stage_end = staged + STAGE_PASS;
     n_pass++;
     uint const ts32 = (uint)tn;
-    while( !done_in && staged - handed < t->batch_max && staged != stage_end ) {
+    ulong nj = 0UL;
+    while( !done_in && staged + nj - handed < t->batch_max && staged + nj != stage_end ) {
       if( frag_cnt && in_seq - in_seq0 >= frag_cnt ) break;
-      if( staged - pubd >= W ) { full = true; n_stop_window++; break; }
+      if( staged + nj - pubd >= W ) { full = true; n_stop_window++; break; }
       fd_frag_meta_t const * m = in_mcache + (in_seq & (in_depth-1UL));
       __builtin_prefetch( in_mcache + ((in_seq + 16UL) & (in_depth-1UL)) );
       ulong seq_found = __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE );
@@ -1082,13 +1156,17 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
         for( ulong o = 0; o < n8; o += 64UL ) __builtin_prefetch( p8 + o );
       }
       if( !zc_dev ) {
-        /* copy mode: the frame is the tile's copy; a frag lapped while it
-           was copied is dropped (speculative read, then seq re-check) */
-        uint8_t * dst = t->out_base + f * FD_VERIFY_AMD_FRAME_SZ;
-        stage_copy_nt( dst, p, sz );
-        __atomic_thread_fence( __ATOMIC_ACQUIRE );
-        if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != in_seq ) { ovrn++; in_seq++; continue; }
-        p = dst;
+        /* copy mode: the frame is the tile's copy.  The HA tag is read from
+           the source now (the seq re-check after the copy covers it too) */
+        ulong tag = 0UL;
+        if( t->tc.depth ) memcpy( &tag, p + 32, 8 );
+        jobs[nj++] = copy_job_t{ t->out_base + f * FD_VERIFY_AMD_FRAME_SZ, p, m, in_seq, fr, sz, tag, (uint)f,
+                                 (uint)tsorig, (ushort)ctl };
+        t->frame_pub[f] = FRAME_FREE;
+        t->frame_next++;
+        if( ++t->frame_next_idx == F ) t->frame_next_idx = 0UL;
+        in_seq++;
+        continue;
       }
       in_seq++; in_cnt++;
       if( t->tc.depth ) {   /* HA dedup on the first 8 signature bytes (reads the frag: a cache miss in zero copy) */
@@ -1099,11 +1177,32 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       t->frame_next++;
       if( ++t->frame_next_idx == F ) t->frame_next_idx = 0UL;
       fd_amd_tile_ent_t * en = t->ring + (staged & mask);
-      en->src_chunk = zc_dev ? (uint32_t)chunk : (uint32_t)(f * FRAME_CHUNKS);
+      en->src_chunk = (uint32_t)chunk;
       en->out_chunk = (uint32_t)(f * FRAME_CHUNKS);
       en->sz        = (uint32_t)sz;
       t->ppend[staged & mask] = pending_t{ in_seq - 1UL, fr, (ushort)sz, (ushort)ctl, (uint)tsorig, (uint)f, ts32, 0u, 0u };
       staged++;
+    }
+    if( nj ) {
+      ulong const half = ( cp && nj >= COPY_SPLIT_MIN ) ? nj / 2UL : nj;
+      if( half < nj ) { cp->jobs = jobs.data(); cp->lo = half; cp->hi = nj; cp->gen.store( ++cgen, std::memory_order_release ); }
+      copy_jobs( jobs.data(), 0UL, half );
+      if( half < nj ) while( cp->done.load( std::memory_order_acquire ) != cgen ) _mm_pause();
+      __atomic_thread_fence( __ATOMIC_ACQUIRE );
+      for( ulong k=0; k<nj; k++ ) {
+        copy_job_t const & j = jobs[k];
+        /* a frag lapped while it was copied is dropped (speculative read,
+           then seq re-check); its frame stays unused */
+        if( __atomic_load_n( &j.m->seq, __ATOMIC_ACQUIRE ) != j.seq ) { ovrn++; continue; }
+        in_cnt++;
+        if( t->tc.depth && t->tc.insert( j.tag ) ) { ha++; ha_sz += j.sz; continue; }
+        fd_amd_tile_ent_t * en = t->ring + (staged & mask);
+        en->src_chunk = (uint32_t)(j.f * FRAME_CHUNKS);
+        en->out_chunk = (uint32_t)(j.f * FRAME_CHUNKS);
+        en->sz        = (uint32_t)j.sz;
+        t->ppend[staged & mask] = pending_t{ j.seq, j.fr, (ushort)j.sz, j.ctl, j.tsorig, j.f, ts32, 0u, 0u };
+        staged++;
+      }
     }
     n_stop_bmax += staged - handed >= t->batch_max;
     n_stop_pass += staged == stage_end;
@@ -1184,6 +1283,8 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   r.end.store( staged, std::memory_order_release );
   if( rc || halted ) r.quit.store( 1, std::memory_order_release );
   if( pub.joinable() ) pub.join();
+  cpy.quit.store( 1, std::memory_order_release );
+  if( cth.joinable() ) cth.join();
   __atomic_store_n( &H->stop, 1u, __ATOMIC_RELEASE );
   {
     /* a kernel that never started is not waited for (it exits at once
@@ -1328,12 +1429,13 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
      takes most of the machine's interrupts (tile passes of 1-5 ms and p99
      spikes were seen with the tile thread on CPU 0) */
   cpu_set_t allowed, saved; CPU_ZERO( &allowed ); CPU_ZERO( &saved );
-  int cpus[4] = { -1, -1, -1, -1 }, ncpu = 0;
+  int cpus[5] = { -1, -1, -1, -1, -1 }, ncpu = 0;
   bool pin = !sched_getaffinity( 0, sizeof allowed, &allowed ) && CPU_COUNT( &allowed ) >= 5;
   if( pin ) {
     saved = allowed;
-    for( int c=CPU_SETSIZE-1; c>0 && ncpu<4; c-- ) if( CPU_ISSET( c, &allowed ) ) cpus[ncpu++] = c;
-    pin = ncpu == 4;
+    int const want = CPU_COUNT( &allowed ) >= 6 ? 5 : 4;   /* the fifth: copy mode's helper */
+    for( int c=CPU_SETSIZE-1; c>0 && ncpu<want; c-- ) if( CPU_ISSET( c, &allowed ) ) cpus[ncpu++] = c;
+    pin = ncpu >= 4;
   }
   auto pin_to = [&]( int k ) {
     if( !pin ) return;
@@ -1349,6 +1451,8 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   cfg.chunk_mode = (flags & FD_VERIFY_AMD_BENCH_CHUNK_LAT) ? FD_VERIFY_AMD_CHUNK_LATENCY
                  : (flags & FD_VERIFY_AMD_BENCH_CHUNK_THR) ? FD_VERIFY_AMD_CHUNK_THROUGHPUT : FD_VERIFY_AMD_CHUNK_AUTO;
   cfg.publish_cpu = (flags & FD_VERIFY_AMD_BENCH_PUB_INLINE) || !pin ? FD_VERIFY_AMD_PUBLISH_INLINE : cpus[3];
+  cfg.copy_cpu    = zero_copy || (flags & FD_VERIFY_AMD_BENCH_COPY_INLINE) || !pin || cpus[4] < 0 ? FD_VERIFY_AMD_COPY_INLINE
+                                                                                               : cpus[4];
   fd_verify_amd_tile_t * tile = fd_verify_amd_tile_new_cfg( &cfg );
   if( !tile ) { free( dcache ); return FD_ED25519_AMD_ERR_DEVICE; }
   if( zero_copy && fd_verify_amd_tile_register_dcache( tile, dcache, region ) ) {

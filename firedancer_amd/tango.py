@@ -21,6 +21,7 @@ DIAG_FIELDS = ("in_cnt", "ha_filt_cnt", "ha_filt_sz", "sv_filt_cnt", "sv_filt_sz
                "sv_filt_msg_cnt", "halt_drop_cnt", "mode_switch_cnt")
 CHUNK_AUTO, CHUNK_LATENCY, CHUNK_THROUGHPUT = 0, 1, 2
 PUBLISH_AUTO, PUBLISH_INLINE = -2, -1
+COPY_INLINE = -1
 
 
 class TileCfg(ctypes.Structure):
@@ -30,7 +31,8 @@ class TileCfg(ctypes.Structure):
                 ("waves", ctypes.c_ulong), ("chunk_mode", ctypes.c_int), ("publish_cpu", ctypes.c_int),
                 ("window", ctypes.c_ulong), ("lat_fill_ns", ctypes.c_ulong), ("lat_free_chunks", ctypes.c_ulong),
                 ("chunk_wait_ns", ctypes.c_ulong), ("thr_rate_hi", ctypes.c_ulong), ("thr_rate_lo", ctypes.c_ulong),
-                ("halt_grace_ns", ctypes.c_ulong)]
+                ("halt_grace_ns", ctypes.c_ulong),
+                ("copy_cpu", ctypes.c_int)]
 
     @classmethod
     def default(cls, **kw):
@@ -86,7 +88,7 @@ class VerifyTile:
     def __init__(self, device=0, batch_max=4096, batch_wait_ns=0, tcache_depth=1 << 16, framing=0, out_frame_cnt=0,
                  **cfg):
         """cfg: further fd_verify_amd_tile_cfg_t fields (waves, chunk_mode, publish_cpu, window, lat_fill_ns,
-        lat_free_chunks, chunk_wait_ns, thr_rate_hi, thr_rate_lo, halt_grace_ns)."""
+        lat_free_chunks, chunk_wait_ns, thr_rate_hi, thr_rate_lo, halt_grace_ns, copy_cpu)."""
         L = ed25519.lib()
         self._h = None
         c = TileCfg.default(device=int(device), batch_max=int(batch_max), batch_wait_ns=int(batch_wait_ns),
@@ -161,12 +163,12 @@ class VerifyTile:
 
 
 BENCH_ZERO_COPY, BENCH_WRITE, BENCH_LAP, BENCH_SAMPLE_BYTES = 1, 2, 4, 8
-BENCH_CHUNK_LAT, BENCH_CHUNK_THR, BENCH_PUB_INLINE, BENCH_TXN = 16, 32, 64, 128
+BENCH_CHUNK_LAT, BENCH_CHUNK_THR, BENCH_PUB_INLINE, BENCH_TXN, BENCH_COPY_INLINE = 16, 32, 64, 128, 256
 
 
 def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, blob, frag_cnt, rate=0.0,
                  zero_copy=False, writes=False, lap=False, dcache_frames=0, expect_err=None, expect_tag=None,
-                 sample_bytes=False, chunk_mode=0, pub_inline=False, txn=False, waves=0):
+                 sample_bytes=False, chunk_mode=0, pub_inline=False, txn=False, waves=0, copy_inline=False):
     """fd_verify_amd_bench_stream: producer (rate frags/s, 0 = saturate) -> tile -> consumer; returns
     dict(frags_per_s, p50_ns, p99_ns, p999_ns, mean_batch, published, sv_filt, ovrn, mismatches, checked).
     With expect_err/expect_tag (per pool entry) the consumer checks every published frag."""
@@ -176,7 +178,7 @@ def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, bl
     et = np.ascontiguousarray(expect_tag, np.uint64) if expect_tag is not None else None
     flags = (BENCH_ZERO_COPY if zero_copy else 0) | (BENCH_WRITE if writes else 0) | (BENCH_LAP if lap else 0) | \
         (BENCH_SAMPLE_BYTES if sample_bytes else 0) | {0: 0, 1: BENCH_CHUNK_LAT, 2: BENCH_CHUNK_THR}[chunk_mode] | \
-        (BENCH_PUB_INLINE if pub_inline else 0) | (BENCH_TXN if txn else 0)
+        (BENCH_PUB_INLINE if pub_inline else 0) | (BENCH_TXN if txn else 0) | (BENCH_COPY_INLINE if copy_inline else 0)
     vp = ctypes.c_void_p
     rc = ed25519.lib().fd_verify_amd_bench_stream(int(device), int(batch_max), int(batch_wait_ns), float(rate), flags,
                                                   int(dcache_frames), p[2].shape[0],

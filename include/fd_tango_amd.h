@@ -130,18 +130,20 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    Chunks.  A chunk takes one wave whatever its size.  Latency chunks hold
    up to 8 frags verified 8 lanes per signature (~0.45 ms on a SIMD of its
    own); throughput chunks up to 64 frags, 1 lane per signature (~1.2 ms
-   alone, ~2.9 ms with every wave slot busy), 3-4x the frags per wave-ms.
-   chunk_mode AUTO picks by the staging rate (mean over ~0.4 ms): throughput
+   alone, ~2.2 ms with every wave slot busy), 3-4x the frags per wave-ms.
+   chunk_mode AUTO picks by the staging rate (EWMA over ~0.8 ms): throughput
    chunks above thr_rate_hi frags/s, latency chunks again below thr_rate_lo
-   (0: 55 % / 40 % of the latency chunks' capacity, min(waves, 4 x CUs) x
-   8 frags / 0.45 ms).  Whole chunks go at once; a partial latency chunk
+   (0: 55 % / 40 % of the latency chunks' capacity, min(min(waves, 4 x CUs)
+   x 8 frags / 0.45 ms, window / 0.55 ms); never throughput chunks when the
+   window caps them below that capacity, window / 2 ms).  Whole chunks go at once; a partial latency chunk
    goes once its oldest frag waited lat_fill_ns, or at once while fewer
    than lat_free_chunks chunks are in flight; a partial throughput chunk
    once its oldest waited chunk_wait_ns.  Everything staged goes at
    batch_max staged frags, when the window or the output frames run out,
    at the end of the input, and (batch_wait_ns != 0) once the oldest waited
    batch_wait_ns.  At most `window` frags are in flight (handed over, not
-   yet published; 0: 64 x batch_max, >= 2^13, 2^18 from batch_max 4096).
+   yet published; 0: 2^18 from batch_max 4096, 2^17 from 1024, else
+   64 x batch_max, >= 2^13).
    TXN framing uses the batch path: up to 4 batches in flight, each on its
    own stream (parse, verify, reduce per batch).
 
@@ -149,7 +151,10 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    runs on a second host thread when publish_cpu >= 0 (pinned there) or,
    with FD_VERIFY_AMD_PUBLISH_AUTO, when the caller's CPU set holds another
    CPU (the thread gets that set minus the caller's current CPU);
-   FD_VERIFY_AMD_PUBLISH_INLINE keeps both on the caller's thread.  After
+   FD_VERIFY_AMD_PUBLISH_INLINE keeps both on the caller's thread.  In copy
+   mode a third thread, pinned to copy_cpu (>= 0), copies half of each
+   staging pass's frags beside the caller's thread (passes of 32 frags or
+   more; FD_VERIFY_AMD_COPY_INLINE, the default: the caller copies all).  After
    *stop the run publishes what completes, for at most halt_grace_ns while
    its output is backpressured, then returns (halt_drop_cnt).
 
@@ -171,6 +176,7 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
 #define FD_VERIFY_AMD_CHUNK_THROUGHPUT (2)   /* every chunk a throughput chunk */
 #define FD_VERIFY_AMD_PUBLISH_AUTO   (-2)
 #define FD_VERIFY_AMD_PUBLISH_INLINE (-1)
+#define FD_VERIFY_AMD_COPY_INLINE    (-1)
 
 typedef struct {
   int   device;           /* HIP device */
@@ -190,12 +196,13 @@ typedef struct {
   ulong thr_rate_hi;      /* frags/s, 0: default */
   ulong thr_rate_lo;
   ulong halt_grace_ns;
+  int   copy_cpu;         /* FD_VERIFY_AMD_COPY_INLINE, or a CPU for the copy helper */
 } fd_verify_amd_tile_cfg_t;
 
 /* Defaults: device 0, PUB_SIG_MSG, batch_max 4096, batch_wait_ns 0,
    tcache_depth 2^16, out_frame_cnt 0, waves 0, AUTO chunks, AUTO
    publisher, window 0, lat_fill_ns 20 us, lat_free_chunks CUs / 2,
-   chunk_wait_ns 50 us, thr rates 0, halt_grace_ns 50 ms. */
+   chunk_wait_ns 50 us, thr rates 0, halt_grace_ns 50 ms, copy inline. */
 void
 fd_verify_amd_tile_cfg_default( fd_verify_amd_tile_cfg_t * cfg );
 
@@ -385,7 +392,8 @@ fd_verify_amd_tile_mode( int chunk_mode, int thr, double rate, double rate_hi, d
    frag.  out holds 40 doubles.
    Threads: producer, tile, the tile's publisher and consumer each pinned
    to a CPU of their own when the process may use 5 or more (else unpinned,
-   publisher inline).  waves: the tile's cfg.waves (0: the device's share;
+   publisher inline); copy mode adds the tile's copy helper on a fifth CPU
+   when there are 6 or more (FD_VERIFY_AMD_BENCH_COPY_INLINE: none).  waves: the tile's cfg.waves (0: the device's share;
    ranks that share a GPU in separate processes each pass theirs).  Returns
    0 or an error code. */
 #define FD_VERIFY_AMD_BENCH_ZERO_COPY (1)
@@ -398,6 +406,7 @@ fd_verify_amd_tile_mode( int chunk_mode, int thr, double rate, double rate_hi, d
 #define FD_VERIFY_AMD_BENCH_TXN        (128) /* TXN framing: pool entry k is the wire transaction
                                                 blob[msg_off[k], +msg_sz[k]) (pub, sig unused); expect_err /
                                                 expect_tag per transaction (verdict, first signature's tag) */
+#define FD_VERIFY_AMD_BENCH_COPY_INLINE (256) /* copy mode: no copy helper thread */
 
 int
 fd_verify_amd_bench_stream( int           device,

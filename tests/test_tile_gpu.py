@@ -217,6 +217,21 @@ def test_tile_large_batches_vs_oracle(batch_max, zero_copy):
     assert r["gpu_frags_lat"] <= 8 * r["gpu_chunks_lat"] and r["gpu_frags_thr"] <= 64 * r["gpu_chunks_thr"]
 
 
+def test_tile_copy_without_helper_vs_oracle():
+    """Copy mode with every copy on the stager (cfg.copy_cpu = COPY_INLINE;
+    the bench's default gives copy mode a helper thread when the process has
+    6 CPUs): the same exact published stream."""
+    from firedancer_amd import tango
+    batch_max = 16384
+    pub, sig, off, sz, blob, err, tag = _stream_pool(4096 + batch_max, 8192, 400)
+    nf = 4 * batch_max + 777
+    r = tango.bench_stream(0, batch_max, 0, pub, sig, off, sz, blob, nf, expect_err=err, expect_tag=tag,
+                           copy_inline=True)
+    want = int((err[np.arange(nf) % err.size] == 0).sum())
+    assert r["mismatches"] == 0 and r["ovrn"] == 0
+    assert r["checked"] == r["published"] == want and r["sv_filt"] == nf - want
+
+
 @pytest.mark.parametrize("zero_copy", [False, True])
 def test_tile_txn_framing_vs_oracle(zero_copy):
     """Frags carrying wire transactions (multi-signer, legacy + v0, some
