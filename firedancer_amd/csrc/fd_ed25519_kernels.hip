@@ -1379,7 +1379,15 @@ k_ai( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L ) {
   if( act && (ws[L.ds + 2u*i] | ws[L.ds + 2u*i + 1u]) ) { err[i] = (i8)-2; act = false; }
   size_t N = L.N;
   u32 ii = (i < n) ? i : 0u;
-  i32 * Ail = (i32 *)(ws + L.Ai) + (size_t)ii*384u;
+  /* the wave's 64 tables are written one entry at a time through LDS: lane
+     l stages its 192-B entry, then the wave stores the 64 entries as 12
+     contiguous 1-KB rows (whole 64-B lines; a lane writing its own table
+     touches 64 lines per store and took ~0.36 of k_ai's 0.78 ms).  Lanes past
+     n or inactive write don't-care tables into their own slabs (< N, never
+     read). */
+  __shared__ int4 s_ai[64 * 12];
+  int4 * const s_me = s_ai + threadIdx.x * 12u;
+  int4 * const Ab = (int4 *)((i32 *)(ws + L.Ai) + (size_t)blockIdx.x * 64u * 384u);
   {
     p3 A;
     i32 const * Aw = (i32 const *)(ws + L.A);
@@ -1391,21 +1399,28 @@ k_ai( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L ) {
     }
     fe cZ, cYmX, cYpX, cT2d;
     ge_to_cached( cZ, cYmX, cYpX, cT2d, A );
-#   define AI_ROW( e, r, f ) do {                                                   \
-      int4 * d_ = (int4 *)(Ail + (e)*48 + (r)*12);                                  \
-      d_[0] = make_int4( f.v[0], f.v[1], f.v[2], f.v[3] );                          \
-      d_[1] = make_int4( f.v[4], f.v[5], f.v[6], f.v[7] );                          \
-      d_[2] = make_int4( f.v[8], f.v[9], 0, 0 );                                    \
+#   define AI_ROW( r, f ) do {                                                      \
+      s_me[3*(r)  ] = make_int4( f.v[0], f.v[1], f.v[2], f.v[3] );                  \
+      s_me[3*(r)+1] = make_int4( f.v[4], f.v[5], f.v[6], f.v[7] );                  \
+      s_me[3*(r)+2] = make_int4( f.v[8], f.v[9], 0, 0 );                            \
     } while(0)
-#   define AI_STORE( e ) do { AI_ROW( e, 0, cZ ); AI_ROW( e, 1, cYmX ); AI_ROW( e, 2, cYpX ); AI_ROW( e, 3, cT2d ); } while(0)
-    if( act ) AI_STORE( 0 );
+#   define AI_STORE( e ) do {                                                       \
+      AI_ROW( 0, cZ ); AI_ROW( 1, cYmX ); AI_ROW( 2, cYpX ); AI_ROW( 3, cT2d );     \
+      __syncthreads();                                                              \
+      _Pragma("unroll") for( u32 q=0; q<12u; q++ ) {                                \
+        u32 const x = q*64u + threadIdx.x, sg = x / 12u, c = x - 12u*sg;            \
+        Ab[(size_t)sg*96u + (e)*12u + c] = s_ai[x];                                 \
+      }                                                                             \
+      __syncthreads();                                                              \
+    } while(0)
+    AI_STORE( 0u );
     p1p1 t = ge_dbl( A.X, A.Y, A.Z );
     p3 A2 = ge_p1p1_to_p3( t );
-    for( int e=0; e<7; e++ ) {
+    for( u32 e=0; e<7u; e++ ) {
       p1p1 s2 = ge_add<false>( A2, cZ, cYmX, cYpX, cT2d, false );
       p3 u = ge_p1p1_to_p3( s2 );
       ge_to_cached( cZ, cYmX, cYpX, cT2d, u );
-      if( act ) AI_STORE( e+1 );
+      AI_STORE( e+1u );
     }
 #   undef AI_STORE
 #   undef AI_ROW
