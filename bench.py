@@ -513,20 +513,29 @@ def txn_stream_row(local, args):
     zpub, zsig = np.zeros((toff.size, 32), np.uint8), np.zeros((toff.size, 64), np.uint8)
     pool = (zpub, zsig, toff, tsz, payload)
     nf = args.stream_frags // 4
-    sat = tango.bench_stream(local, 4096, 0, *pool, nf, zero_copy=True, txn=True, expect_err=terr, expect_tag=tag,
-                             sample_bytes=True)
-    half = tango.bench_stream(local, 4096, 0, *pool, int(min(nf, max(20000, 0.5 * sat["frags_per_s"]))),
-                              rate=0.5 * sat["frags_per_s"], zero_copy=True, txn=True)
     sigs_per_txn = float(ed25519.txn_slots(payload, toff, tsz)[1]) / toff.size
-    return {"path": "TXN framing (wire transactions, multi-signer; the tile's batch path: parse, verify, reduce per "
-                    "batch, 4 batches in flight), batch_max 4096, zero copy",
-            "pool": "%d transactions, %.2f signatures each, %d with a flipped signature bit" % (toff.size, sigs_per_txn,
-                                                                                              bad.size),
-            "saturated_txns_per_s": sat["frags_per_s"], "saturated_verifies_per_s": sat["frags_per_s"] * sigs_per_txn,
-            "check_mismatches": int(sat["mismatches"]), "checked": int(sat["checked"]),
-            "published": int(sat["published"]), "sv_filt": int(sat["sv_filt"]),
-            "at_50%": {"offered_txns_per_s": 0.5 * sat["frags_per_s"], "p50_us": half["p50_ns"] / 1e3,
-                       "p99_us": half["p99_ns"] / 1e3}}
+
+    def row(bmax):
+        sat = tango.bench_stream(local, bmax, 0, *pool, nf, zero_copy=True, txn=True, expect_err=terr, expect_tag=tag,
+                                 sample_bytes=True)
+        half = tango.bench_stream(local, bmax, 0, *pool, int(min(nf, max(20000, 0.5 * sat["frags_per_s"]))),
+                                  rate=0.5 * sat["frags_per_s"], zero_copy=True, txn=True)
+        return {"batch_max": bmax, "saturated_txns_per_s": sat["frags_per_s"],
+                "saturated_verifies_per_s": sat["frags_per_s"] * sigs_per_txn,
+                "check_mismatches": int(sat["mismatches"]), "checked": int(sat["checked"]),
+                "published": int(sat["published"]), "sv_filt": int(sat["sv_filt"]),
+                "at_50%": {"offered_txns_per_s": 0.5 * sat["frags_per_s"], "p50_us": half["p50_ns"] / 1e3,
+                           "p99_us": half["p99_ns"] / 1e3}}
+
+    rows = [row(4096), row(16384)]
+    out = {"path": "TXN framing (wire transactions, multi-signer; the tile's batch path: parse, verify, reduce per "
+                   "batch, 4 batches in flight; batch_max = signatures per batch), zero copy",
+           "pool": "%d transactions, %.2f signatures each, %d with a flipped signature bit" % (toff.size, sigs_per_txn,
+                                                                                             bad.size),
+           "rows": rows}
+    out.update({k: rows[0][k] for k in ("saturated_txns_per_s", "saturated_verifies_per_s", "check_mismatches",
+                                        "checked", "published", "sv_filt", "at_50%")})
+    return out
 
 
 def stream_node(local, pub, sig, off, sz, blob, args, rank, world, dist):

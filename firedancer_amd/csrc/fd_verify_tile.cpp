@@ -411,7 +411,7 @@ tile_window( fd_verify_amd_tile_cfg_t const * c ) {
      load shows up as input wait in the tail) */
   if( c->batch_max >= (1UL << 12) ) return 1UL << 18;
   if( c->batch_max >= (1UL << 10) ) return 1UL << 17;
-  return std::max( 64UL * c->batch_max, 1UL << 13 );
+  return std::max( 64UL * c->batch_max, 1UL << 15 );   /* latency chunks at ~18 M frags/s x ~1 ms */
 }
 
 /* The persistent consumer's resources (allocated at the first

@@ -143,7 +143,7 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    at the end of the input, and (batch_wait_ns != 0) once the oldest waited
    batch_wait_ns.  At most `window` frags are in flight (handed over, not
    yet published; 0: 2^18 from batch_max 4096, 2^17 from 1024, else
-   64 x batch_max, >= 2^13).
+   64 x batch_max, >= 2^15).
    TXN framing uses the batch path: up to 4 batches in flight, each on its
    own stream (parse, verify, reduce per batch).
 
@@ -189,7 +189,7 @@ typedef struct {
   int   chunk_mode;       /* FD_VERIFY_AMD_CHUNK_* */
   int   publish_cpu;      /* FD_VERIFY_AMD_PUBLISH_AUTO / _INLINE, or a CPU */
   ulong window;           /* frags in flight; 0: 2^18 from batch_max 4096, 2^17 from 1024,
-                             else max( 64 x batch_max, 2^13 ) */
+                             else max( 64 x batch_max, 2^15 ) */
   ulong lat_fill_ns;
   ulong lat_free_chunks;
   ulong chunk_wait_ns;
