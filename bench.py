@@ -396,8 +396,8 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
     runs check every published frag against the batch engine's verdicts and
     the SHA-512 tags (verdict, tag and order of every frag; the bytes in the
     tile's output dcache of every 16th); paced runs (50 % / 80 % of the
-    row's saturated rate, and a fixed 1 M frags/s) measure latency and its
-    decomposition."""
+    row's saturated rate, three interleaved runs each, medians reported; and
+    a fixed 1 M frags/s) measure latency and its decomposition."""
     from firedancer_amd import ed25519, tango
     m = min(pub.shape[0], 1 << 16)
     p_pub, p_sig, p_sz = pub[:m], sig[:m], sz[:m]
@@ -453,11 +453,22 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
                                   "mac_per_frag": mac_per_sig + MAC_DECOMP,
                                   "note": "saturated frags/s x (DSM MACs per signature of the resident batch + "
                                           "decompression's %d) vs the integer-multiply peak" % MAC_DECOMP}
-            for load in (0.5, 0.8):
-                rr["at_%d%%" % int(load * 100)] = paced(bmax, zc, load * sat["frags_per_s"])
+            # three interleaved rounds of the two loads; each load reports the median p50 and the
+            # median p99 of its three runs (the other fields from its median-p50 run): a single
+            # run's p50 moved by up to 2 % between back-to-back runs on one box
+            runs = {0.5: [], 0.8: []}
+            for _ in range(3):
+                for load in (0.5, 0.8):
+                    runs[load].append(paced(bmax, zc, load * sat["frags_per_s"]))
+            for load, rs in runs.items():
+                med = sorted(rs, key=lambda x: x["p50_us"])[1]
+                r = dict(med)
+                r["p99_us"] = sorted(x["p99_us"] for x in rs)[1]
+                r["p99_over_p50"] = r["p99_us"] / max(r["p50_us"], 1e-3)
+                r["runs"] = [{"p50_us": x["p50_us"], "p99_us": x["p99_us"], "frags_per_s": x["frags_per_s"]} for x in rs]
+                rr["at_%d%%" % int(load * 100)] = r
             lo, hi = rr["at_50%"], rr["at_80%"]
-            # within 1 %: the p50 of one row at a fixed load moves by ~0.5 % run to run
-            # (profiles/r04_bench_tile_*.json), and both loads run throughput chunks
+            # within 1 % (medians of three runs; both loads run throughput chunks above batch_max 256)
             rr["p50_nondecreasing_with_load"] = hi["p50_us"] >= 0.99 * lo["p50_us"]
             rr["p99_within_2_5x_p50"] = max(lo["p99_over_p50"], hi["p99_over_p50"]) <= 2.5
             row[key] = rr
