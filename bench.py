@@ -437,7 +437,9 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
             key = "zero_copy" if zc else "copy"
             sat = tango.bench_stream(local, bmax, 0, *pool, args.stream_frags, zero_copy=zc, expect_err=p_err,
                                      expect_tag=p_tag, sample_bytes=True)
-            rr = {"saturated_frags_per_s": sat["frags_per_s"], "saturated_mean_hand_off": sat["mean_batch"],
+            rr = {"saturated_frags_per_s": sat["frags_per_s"],
+                  "saturated_steady_frags_per_s": sat["steady_frags_per_s"],
+                  "saturated_mean_hand_off": sat["mean_batch"],
                   "published": int(sat["published"]), "sv_filt": int(sat["sv_filt"]), "ovrn": int(sat["ovrn"]),
                   "check_mismatches": int(sat["mismatches"]), "checked": int(sat["checked"]),
                   "saturated_loop": {k: int(sat[k]) for k in ("passes", "hand_offs", "stop_window", "stop_frames",
@@ -449,10 +451,13 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
                                           "consumer_gap_max": sat["consumer_gap_max_ns"] / 1e3}}
             if mac_per_sig:
                 a = sat["frags_per_s"] * (mac_per_sig + MAC_DECOMP) / 1e12
+                a_st = sat["steady_frags_per_s"] * (mac_per_sig + MAC_DECOMP) / 1e12
                 rr["roofline"] = {"achieved": a, "peak": PEAK_TMAC, "unit": "TMAC/s", "frac": a / PEAK_TMAC,
+                                  "frac_steady": a_st / PEAK_TMAC,
                                   "mac_per_frag": mac_per_sig + MAC_DECOMP,
                                   "note": "saturated frags/s x (DSM MACs per signature of the resident batch + "
-                                          "decompression's %d) vs the integer-multiply peak" % MAC_DECOMP}
+                                          "decompression's %d) vs the integer-multiply peak; frac over the whole run (its ramp and "
+                                          "drain included), frac_steady over the input's 10-90 %% span" % MAC_DECOMP}
             # three interleaved rounds of the two loads; each load reports the median p50 and the
             # median p99 of its three runs (the other fields from its median-p50 run): a single
             # run's p50 moved by up to 2 % between back-to-back runs on one box

@@ -1510,6 +1510,7 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
       fd_mcache_publish( in_mc.data(), depth, seq, 0UL, fr * frame_c, sz, 3UL, tso, 0UL );
     }
   } );
+  ulong t10 = 0, t90 = 0, s10 = 0, s90 = 0;   /* check mode: when the consumer reached 10 % / 90 % of the input */
   std::thread cons( [&]() {
     pin_to( 2 );
     ulong seq = 0, fseq = 0;   /* fseq: last value published to out_fseq (every 64 frags, or when idle) */
@@ -1536,6 +1537,9 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
             exp_k = (exp_k + 1UL == pool_n) ? 0UL : exp_k + 1UL;
           }
           last = (long)s_in;
+          /* the steady-state rate: input frags between 10 % and 90 % of the run */
+          if( !t10 && s_in >= frag_cnt / 10UL ) { t10 = now_ns(); s10 = s_in; }
+          if( !t90 && s_in >= 9UL * (frag_cnt / 10UL) ) { t90 = now_ns(); s90 = s_in; }
           uchar const * q = out_chunk0 + (chunk << FD_CHUNK_LG_SZ);
           bool ok = s_in < frag_cnt && !expect_err[k] && tag == expect_tag[k] && sz == frag_sz( k );
           if( ok && !(checked & byte_mask) )
@@ -1573,7 +1577,8 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   free( dcache );
   if( rc ) return rc;
   ulong n = std::min( (ulong)diag.out_cnt, frag_cnt );
-  for( int k=0; k<40; k++ ) out[k] = 0.0;
+  for( int k=0; k<41; k++ ) out[k] = 0.0;
+  if( t90 > t10 && t10 && s90 > s10 ) out[40] = (double)(s90 - s10) / ((double)(t90 - t10) * 1e-9);
   /* decomposition (before lat is sorted: the samples are per published frag) */
   /* paced runs: percentiles over the steady state (n_st samples); the
      all-frags p50 / p99 go to out[38], out[39] */

@@ -389,7 +389,9 @@ fd_verify_amd_tile_mode( int chunk_mode, int thr, double rate, double rate_hi, d
    kernel launch is not part of the stream; their latency percentiles
    (out[1..3], out[17..28]) cover the steady state, the frags scheduled
    20 ms or more after the start, and out[38] / out[39] = p50 / p99 of every
-   frag.  out holds 40 doubles.
+   frag.  out[40] (check mode) = the steady-state rate: input frags between
+   10 % and 90 % of the run over the time the consumer took from one to the
+   other (out[0] includes the run's ramp and drain).  out holds 41 doubles.
    Threads: producer, tile, the tile's publisher and consumer each pinned
    to a CPU of their own when the process may use 5 or more (else unpinned,
    publisher inline); copy mode adds the tile's copy helper on a fifth CPU
