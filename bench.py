@@ -89,7 +89,7 @@ def parse():
     ap.add_argument("--workload", choices=("sigs", "txn"), default="sigs",
                     help="sigs: configs[1] (default bench line); txn: configs[3] multi-signer transactions")
     ap.add_argument("--stream-frags", type=int, default=1 << 22, help="frags per saturated streaming-tile run")
-    ap.add_argument("--paced-seconds", type=float, default=0.25,
+    ap.add_argument("--paced-seconds", type=float, default=0.5,
                     help="length of a paced streaming-tile run (latency over its steady state: after its first 20 ms)")
     ap.add_argument("--txn-full-check", action="store_true",
                     help="--workload txn: re-verify every transaction with the compiled reference (slow)")
