@@ -1385,8 +1385,8 @@ k_ai( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L ) {
      touches 64 lines per store and took ~0.36 of k_ai's 0.78 ms).  Lanes past
      n or inactive write don't-care tables into their own slabs (< N, never
      read). */
-  __shared__ int4 s_ai[64 * 12];
-  int4 * const s_me = s_ai + threadIdx.x * 12u;
+  __shared__ int4 s_ai[64 * 13];                   /* 13: a lane's entry starts 52 dwords after the last one's */
+  int4 * const s_me = s_ai + threadIdx.x * 13u;
   int4 * const Ab = (int4 *)((i32 *)(ws + L.Ai) + (size_t)blockIdx.x * 64u * 384u);
   {
     p3 A;
@@ -1409,7 +1409,7 @@ k_ai( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L ) {
       __syncthreads();                                                              \
       _Pragma("unroll") for( u32 q=0; q<12u; q++ ) {                                \
         u32 const x = q*64u + threadIdx.x, sg = x / 12u, c = x - 12u*sg;            \
-        Ab[(size_t)sg*96u + (e)*12u + c] = s_ai[x];                                 \
+        Ab[(size_t)sg*96u + (e)*12u + c] = s_ai[sg*13u + c];                        \
       }                                                                             \
       __syncthreads();                                                              \
     } while(0)
