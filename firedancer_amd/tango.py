@@ -119,12 +119,13 @@ class VerifyTile:
         return bytes(self.out_region[CHUNK_SZ * int(chunk):CHUNK_SZ * int(chunk) + int(sz)])
 
     def register_dcache(self, region):
-        """Map the numpy data region into the GPU (zero-copy staging)."""
-        self._region = region
+        """Map the numpy data region into the GPU (zero-copy staging).  The
+        previous region stays referenced until the tile has unregistered it."""
         rc = ed25519.lib().fd_verify_amd_tile_register_dcache(self._h, ctypes.c_void_p(region.ctypes.data),
                                                              region.nbytes)
         if rc:
             raise ed25519.EngineError("fd_verify_amd_tile_register_dcache rc=%d" % rc)
+        self._region = region
 
     def set_trace(self, parts):
         """Per-frag latency decomposition of the next runs into parts (uint32 [n][4], or None)."""

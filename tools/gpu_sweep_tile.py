@@ -4,12 +4,13 @@ draw (oracle/vecgen.h), signed on the GPU and given the same 10 % single-bit
 flips as tools/gpu_sweep.py, are laid out as tango frags (pub | sig | msg in
 a dcache, metadata in an mcache) and run through fd_verify_amd_tile_run
 twice -- every chunk forced to 8-lane latency chunks, then to 64-frag
-throughput chunks (cfg.chunk_mode) -- in copy mode.  The tile's verdict log
+throughput chunks (cfg.chunk_mode) -- in copy mode (or zero copy).  The tile's verdict log
 (fd_verify_amd_tile_set_verdict_log) is compared with the CPU oracle on every
 signature, and each stream's code histogram with the reference's histogram
 recorded in oracle/PARITY_LOG.md.
 
-usage: python tools/gpu_sweep_tile.py [stream indices...] > gpurun_out/sweep_tile.jsonl
+usage: python tools/gpu_sweep_tile.py [--zero-copy] [stream indices...] > gpurun_out/sweep_tile.jsonl
+(--zero-copy: the tile's GPU gathers every frag from the mapped region instead of the host copying it)
 """
 import json
 import os
@@ -55,7 +56,7 @@ def frames(pub, sig, o, z, b):
     return region, c.astype(np.uint32), fsz.astype(np.uint16)
 
 
-def run_tile(tile, region, chunk, fsz):
+def run_tile(tile, region, chunk, fsz, zero_copy=False):
     n = chunk.size
     depth = 1
     while depth < n:
@@ -67,6 +68,8 @@ def run_tile(tile, region, chunk, fsz):
     mc["ctl"][:n] = 3
     out = tango.mcache_new(depth)
     log = np.full(n, 99, np.int8)
+    if zero_copy:
+        tile.register_dcache(region)   # the GPU gathers each frag from the mapped region itself
     tile.set_verdict_log(log)
     diag, _ = tile.run(mc, region, 0, out, 0, n)
     tile.set_verdict_log(None)
@@ -109,7 +112,7 @@ def run(k, tiles):
             region, chunk, fsz = frames(pub[s0:s1], sig[s0:s1], o[s0:s1], z[s0:s1], b)
             for mode, name in MODES:
                 t3 = time.time()
-                log, diag = run_tile(tiles[name], region, chunk, fsz)
+                log, diag = run_tile(tiles[name], region, chunk, fsz, ZERO_COPY)
                 t_tile[name] += time.time() - t3
                 got[name][c0 + s0:c0 + s1] = log
                 chunks[name][0] += diag["gpu_chunk_lat_cnt"]
@@ -121,6 +124,7 @@ def run(k, tiles):
         hist = tuple(int((err == -c).sum()) for c in range(4))
         bad = np.nonzero(err != exp)[0]
         out.append({"seed": seed, "szlo": szlo, "szhi": szhi, "signatures": N, "path": "k_tile_persist",
+                    "staging": "zero_copy" if ZERO_COPY else "copy",
                     "chunk_mode": name, "gpu_chunks": {"latency": chunks[name][0], "throughput": chunks[name][1]},
                     "mismatches_vs_oracle": int(bad.size), "first_mismatches": [int(i) for i in bad[:5]],
                     "hist": hist, "hist_equals_reference": hist == ref_hist,
@@ -130,8 +134,10 @@ def run(k, tiles):
     return out
 
 
+ZERO_COPY = "--zero-copy" in sys.argv
+
 if __name__ == "__main__":
-    ks = [int(a) for a in sys.argv[1:]] or list(range(len(STREAMS)))
+    ks = [int(a) for a in sys.argv[1:] if not a.startswith("--")] or list(range(len(STREAMS)))
     tiles = {name: tango.VerifyTile(0, batch_max=16384, tcache_depth=0, chunk_mode=mode) for mode, name in MODES}
     fail = False
     try:
