@@ -249,10 +249,12 @@ decomp_body( u32 t, u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ 
   if( i >= n ) return;
   if( gate && err[i] != 1 ) return;
   u8 * ds = ws + L.ds;
-  u8 const * src = which ? (sig + 64UL*i) : (pub + 32UL*i);
-  u32 w[8];
-  _Pragma("unroll") for( int k=0; k<8; k++ )
-    w[k] = (u32)src[4*k] | ((u32)src[4*k+1] << 8) | ((u32)src[4*k+2] << 16) | ((u32)src[4*k+3] << 24);
+  /* the point as 8 LE dwords in two 16-B loads (sig / pub records are 64- /
+     32-byte aligned, as k_prep reads them; on the latency path these are
+     reads over PCIe from host memory, so fewer, wider loads) */
+  uint4 const * src = (uint4 const *)(which ? (sig + 64UL*i) : (pub + 32UL*i));
+  uint4 const s0 = src[0], s1 = src[1];
+  u32 const w[8] = { s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w };
 
   fe const D = {FD_AMD_FE_D};
   fe const SQRTM1 = {FD_AMD_FE_SQRTM1};

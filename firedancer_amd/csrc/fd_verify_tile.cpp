@@ -234,12 +234,17 @@ extern "C" int
 fd_verify_amd_tile_register_dcache( fd_verify_amd_tile_t * t, void * base, ulong sz ) {
   if( !t || !base || !sz ) return FD_ED25519_AMD_ERR_INVAL;
   if( hipSetDevice( t->eng->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
-  if( t->reg_base ) { (void)hipHostUnregister( t->reg_base ); t->reg_base = NULL; t->reg_dev = NULL; t->reg_sz = 0; }
+  /* an unregister that fails (the range was unregistered elsewhere) must not
+     leave its error pending for the next launch check (hipGetLastError) */
+  if( t->reg_base ) {
+    if( hipHostUnregister( t->reg_base ) != hipSuccess ) (void)hipGetLastError();
+    t->reg_base = NULL; t->reg_dev = NULL; t->reg_sz = 0;
+  }
   uintptr_t lo = (uintptr_t)base & ~(uintptr_t)4095, hi = ((uintptr_t)base + sz + 4095) & ~(uintptr_t)4095;
   if( hipHostRegister( (void *)lo, hi - lo, hipHostRegisterMapped ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
   void * dev = NULL;
   if( hipHostGetDevicePointer( &dev, (void *)lo, 0 ) != hipSuccess ) {
-    (void)hipHostUnregister( (void *)lo );
+    if( hipHostUnregister( (void *)lo ) != hipSuccess ) (void)hipGetLastError();
     return FD_ED25519_AMD_ERR_DEVICE;
   }
   t->reg_base = (uint8_t *)lo; t->reg_sz = hi - lo; t->reg_dev = (uint8_t *)dev;
