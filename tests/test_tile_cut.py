@@ -35,6 +35,7 @@ def test_defaults():
     ed25519.lib().fd_verify_amd_tile_cfg_default(ctypes.byref(c))
     assert (c.batch_max, c.lat_fill_ns, c.chunk_wait_ns, c.halt_grace_ns) == (4096, 20000, 50000, 50000000)
     assert (c.chunk_mode, c.publish_cpu, c.waves, c.window) == (tango.CHUNK_AUTO, tango.PUBLISH_AUTO, 0, 0)
+    assert c.copy_cpu == tango.COPY_INLINE                # the copy helper is opt-in (the last field of the struct)
 
 
 def test_nothing_staged():
