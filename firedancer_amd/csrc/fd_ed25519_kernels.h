@@ -125,7 +125,7 @@ typedef struct {
 } fd_amd_tile_args_t;
 size_t fd_amd_tile_scratch_stride( void );
 /* waves: grid size (wave 0 is the scout that mirrors the host words) */
-int fd_amd_launch_tile_persist( fd_amd_tile_args_t const * a, uint32_t waves, hipStream_t stream );
+int fd_amd_launch_tile_persist( fd_amd_tile_args_t const * a, uint32_t waves, hipStream_t stream );   /* 0, -1 (waves), or a hipError_t */
 
 #ifdef FD_AMD_DIAG
 /* diagnostics build: the chunk pipeline alone, every argument in device memory */

@@ -2222,8 +2222,10 @@ fd_amd_launch_tile_synth( fd_amd_tile_args_t const * a, uint32_t waves, uint32_t
 int
 fd_amd_launch_tile_persist( fd_amd_tile_args_t const * a, uint32_t waves, hipStream_t stream ) {
   if( waves < 2u ) return -1;
+  (void)hipGetLastError();   /* the check below is the launch's own: every earlier call checked its return code */
   hipLaunchKernelGGL( k_tile_persist, dim3(waves), dim3(64), 0, stream, *a );
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  hipError_t const e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;   /* the HIP error, for the caller's message */
 }
 
 /* ------------------------------------------------------------------ */

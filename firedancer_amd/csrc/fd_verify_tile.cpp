@@ -1001,8 +1001,10 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
 #ifdef FD_AMD_DIAG
   { char const * e = getenv( "FD_AMD_TILE_PROF" ); A.prof = e && *e && *e != '0'; }   /* diagnostics build only */
 #endif
-  if( fd_amd_launch_tile_persist( &A, t->waves, t->pst ) || hipEventRecord( t->pdone, t->pst ) != hipSuccess ) {
-    fprintf( stderr, "fd_verify_amd_tile_run: launching the tile kernel failed\n" );
+  int const lrc = fd_amd_launch_tile_persist( &A, t->waves, t->pst );
+  if( lrc || hipEventRecord( t->pdone, t->pst ) != hipSuccess ) {
+    fprintf( stderr, "fd_verify_amd_tile_run: launching the tile kernel failed (%d: %s; %u waves)\n", lrc,
+             lrc > 0 ? hipGetErrorString( (hipError_t)lrc ) : "-", (unsigned)t->waves );
     (void)hipStreamSynchronize( t->pst );
     return FD_ED25519_AMD_ERR_DEVICE;
   }

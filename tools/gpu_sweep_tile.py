@@ -112,8 +112,9 @@ def run(k, tiles):
             region, chunk, fsz = frames(pub[s0:s1], sig[s0:s1], o[s0:s1], z[s0:s1], b)
             for mode, name in MODES:
                 t3 = time.time()
-                if ZERO_COPY:   # one tile per run: a region is registered (mapped into the GPU) by one tile at a time
-                    tiles[name].close()
+                if ZERO_COPY:   # one live tile per run: a region is registered (mapped into the GPU) by one tile
+                    for t in tiles.values():
+                        t.close()
                     tiles[name] = tango.VerifyTile(0, batch_max=16384, tcache_depth=0, chunk_mode=mode)
                 log, diag = run_tile(tiles[name], region, chunk, fsz, ZERO_COPY)
                 t_tile[name] += time.time() - t3
