@@ -1088,6 +1088,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   ulong iter = 0UL, pass_t = now_ns(), pass_max = 0UL, t_halt = 0UL;
   ulong t_chk = pass_t, g_seen = 0UL, t_prog = pass_t, gc_first = 0UL, gc_last = 0UL, gc_host = 0UL;
   ulong r_t0 = pass_t, r_n0 = staged;
+  bool  r_blk = false;                   /* staging stopped on the window / frames / credit this interval */
   double rate = 0.0;
   int thr = fd_verify_amd_tile_mode( t->cfg.chunk_mode, 0, 0.0, t->rate_hi, t->rate_lo );
   bool halted = false;
@@ -1211,6 +1212,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
         staged++;
       }
     }
+    r_blk = r_blk || full;
     n_stop_bmax += staged - handed >= t->batch_max;
     n_stop_pass += staged == stage_end;
     __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
@@ -1221,8 +1223,14 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     ulong const t3 = now_ns();
     if( t3 - r_t0 >= 200000UL ) {
       double inst = (double)(staged - r_n0) * 1e9 / (double)(t3 - r_t0);
+      /* staging that stopped at the window, the frames or the consumer's
+         credit measures the tile's own completions, not the offered load:
+         such an interval never lowers the rate (else a full window reads as
+         light load, the tile drops to latency chunks -- a third of the
+         capacity -- and the backlog grows) */
+      if( r_blk ) inst = std::max( inst, rate );
       rate = rate > 0.0 ? 0.75 * rate + 0.25 * inst : inst;   /* ~0.8 ms memory: a burst does not flip the mode */
-      r_t0 = t3; r_n0 = staged;
+      r_t0 = t3; r_n0 = staged; r_blk = false;
       int nthr = fd_verify_amd_tile_mode( t->cfg.chunk_mode, thr, rate, t->rate_hi, t->rate_lo );
       switches += nthr != thr;
       thr = nthr;
