@@ -98,6 +98,9 @@ def parse():
     ap.add_argument("--multi-engine", action="store_true",
                     help="one process drives --gpus devices through the native multi-device engine "
                          "(fd_ed25519_amd_multi_verify_soa) on host buffers; prints its own JSON line")
+    ap.add_argument("--detail", default=None,
+                    help="where rank 0 writes the full record (default gpurun_out/bench_detail_*.json); stdout "
+                         "carries only the compact line")
     return ap.parse_args()
 
 
@@ -260,6 +263,134 @@ def pmc_traffic(kernel, n):
         return None
 
 
+LINE_MAX = 6000   # the driver parses the final stdout line; round 4's 38 KB line did not parse
+
+
+def write_detail(out, args):
+    """The whole record (every paced run, decompositions, stall clocks) goes
+    to a side file; stdout carries only the compact line."""
+    path = args.detail or os.path.join(ROOT, "gpurun_out", "bench_detail_%s_n%d_%d.json"
+                                       % (out.get("mode", args.workload), out["n_gpus"], int(time.time())))
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+    except OSError as e:
+        return "unwritten (%s)" % e
+    return os.path.relpath(path, ROOT)
+
+
+def _r(x, nd=4):
+    """Round for the compact line: 4 significant digits."""
+    if isinstance(x, float):
+        return float("%.*g" % (nd, x))
+    return x
+
+
+def _pick(d, keys):
+    return {k: _r(d[k]) for k in keys if d is not None and k in d}
+
+
+def tile_summary(st):
+    """One entry per streaming-tile row: saturated whole-run / steady rate,
+    roofline frac, median p50 and the WORST run's p99 / p50 at each load."""
+    rows = []
+    for row in st["rows"]:
+        for key in ("copy", "zero_copy"):
+            if key not in row:
+                continue
+            r = row[key]
+            e = {"bmax": row["batch_max"], "mode": key, "sat": _r(r["saturated_frags_per_s"]),
+                 "steady": _r(r["saturated_steady_frags_per_s"]), "ok": r["check_mismatches"] == 0}
+            if "roofline" in r:
+                e["frac"] = _r(r["roofline"]["frac"], 3)
+                e["frac_steady"] = _r(r["roofline"]["frac_steady"], 3)
+            for load in ("50", "80"):
+                a = r["at_%s%%" % load]
+                e["p50_us_" + load] = _r(a["p50_us"])
+                e["worst_p99_us_" + load] = _r(a["worst_p99_us"])
+                e["worst_x_" + load] = _r(a["worst_p99_over_p50"], 3)
+            rows.append(e)
+    s = {"all_checks_pass": st["all_checks_pass"],
+         "every_row_worst_p99_within_2_5x_p50": st["every_row_p99_within_2_5x_p50"],
+         "every_row_p50_nondecreasing_with_load": st["every_row_p50_nondecreasing_with_load"],
+         "frags_per_run": st["frags_per_run"], "rows": rows}
+    fx = st.get("fixed_1M_frags_per_s_batch_max_4096")
+    if fx:
+        s["fixed_1M_4096"] = {k: {"p50_us": _r(v["p50_us"]), "p99_us": _r(v["p99_us"])} for k, v in fx.items()}
+    tx = st.get("txn_framing")
+    if tx:
+        s["txn_framing"] = []
+        for r in tx["rows"]:
+            e = {"bmax": r["batch_max"], "txns_per_s": _r(r["saturated_txns_per_s"]),
+                 "verifies_per_s": _r(r["saturated_verifies_per_s"]), "ok": r["check_mismatches"] == 0}
+            for ld in ("50", "80"):
+                a = r.get("at_%s%%" % ld)
+                if a:
+                    e["p50_us_" + ld] = _r(a["p50_us"])
+                    e["worst_p99_us_" + ld] = _r(a.get("worst_p99_us", a.get("p99_us")))
+                    e["worst_x_" + ld] = _r(e["worst_p99_us_" + ld] / max(a["p50_us"], 1e-3), 3)
+            s["txn_framing"].append(e)
+    return s
+
+
+def node_summary(nt):
+    return {"ranks": nt["ranks"], "saturated_frags_per_s_node": _r(nt["saturated_frags_per_s_node"]),
+            "at_50%_frags_per_s_node": _r(nt["at_50%_frags_per_s_node"]),
+            "per_rank": [[_r(p["saturated_frags_per_s"]), _r(p["at_50%"]["p50_us"]), _r(p["at_50%"]["p99_us"]),
+                          p["cpus"], p["device"]] for p in nt["per_rank"]],
+            "per_rank_cols": ["saturated_frags_per_s", "p50_us@50%", "p99_us@50%", "cpus", "device"]}
+
+
+def compact_line(out, detail):
+    """The driver's line: the mandated keys, roofline, cpu_baseline,
+    latency_ms_4096 and per-row tile summaries; everything else is in the
+    side file `detail`."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "mode", "txns_per_s")
+    line = {k: _r(out[k], 6) if k in ("value", "ms_per_step") else out[k] for k in keep if k in out}
+    line["config"] = out["config"]
+    if out.get("roofline"):
+        line["roofline"] = _pick(out["roofline"], ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic",
+                                                   "mac_per_sig"))
+        line["roofline"]["traffic_unit"] = "bytes per launch (PMC)"
+    if out.get("cpu_baseline"):
+        cb = out["cpu_baseline"]
+        line["cpu_baseline"] = _pick(cb, ("value", "unit", "cores", "kind", "sample", "verdicts_equal_gpu",
+                                          "us_per_call_1_thread"))
+        line["cpu_baseline"]["cpu_model"] = cb.get("host", {}).get("cpu_model")
+    for k in ("latency_ms_4096", "latency_ms_4096_registered"):
+        if k in out:
+            line[k] = _pick(out[k], ("p50", "p99"))
+    if "dropin_call_us" in out:
+        line["dropin_call_us"] = _pick(out["dropin_call_us"], ("p50", "p99", "reference_us_per_call_this_host"))
+    if "stage_ms" in out:
+        line["stage_ms"] = _pick(out["stage_ms"], ("k_prep", "k_decomp", "k_dsm"))
+    if out.get("dsm_in_pipeline"):
+        line["dsm_in_pipeline_frac"] = _r(out["dsm_in_pipeline"]["frac"])
+    for k in ("host_soa", "host_fed_node"):
+        if out.get(k):
+            line[k + "_verifies_per_s"] = _r(out[k]["verifies_per_s"])
+    if "verdicts" in out:
+        line["verdicts"] = {k: v for k, v in out["verdicts"].items() if not isinstance(v, dict)}
+    if "stream_tile" in out:
+        line["stream_tile"] = tile_summary(out["stream_tile"])
+    if out.get("stream_tile_node"):
+        line["stream_tile_node"] = node_summary(out["stream_tile_node"])
+    line["detail"] = detail
+    s = json.dumps(line, separators=(",", ":"))
+    if len(s) > LINE_MAX:   # never let the line outgrow the driver's parser: drop the bulkiest parts first
+        for k in ("stream_tile_node", "stream_tile"):
+            if k in line and len(s) > LINE_MAX:
+                line[k] = {"dropped": "line over %d B; see detail" % LINE_MAX}
+                s = json.dumps(line, separators=(",", ":"))
+    return s
+
+
+def emit(out, args):
+    print(compact_line(out, write_detail(out, args)), flush=True)
+
+
 def gather_sum(dist, values):
     if not dist:
         return values
@@ -361,7 +492,7 @@ def run_txn(args, rank, world, dist):
             out["verdicts"]["all_txns_rechecked_by_reference"] = {
                 "txns": int(toff.size), "signatures": int(tbase[-1]), "equal": bool(np.array_equal(f_err, terr)),
                 "mismatches": int((f_err != terr).sum()), "threads": nt, "seconds": time.perf_counter() - t1}
-    print(json.dumps(out))
+    emit(out, args)
 
 
 # ---------------------------------------------------------------- configs[4]
@@ -396,7 +527,8 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
     runs check every published frag against the batch engine's verdicts and
     the SHA-512 tags (verdict, tag and order of every frag; the bytes in the
     tile's output dcache of every 16th); paced runs (50 % / 80 % of the
-    row's saturated rate, three interleaved runs each, medians reported; and
+    row's saturated rate, three interleaved runs each: median p50, worst run's
+    p99 / p50; and
     a fixed 1 M frags/s) measure latency and its decomposition."""
     from firedancer_amd import ed25519, tango
     m = min(pub.shape[0], 1 << 16)
@@ -458,24 +590,26 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
                                   "note": "saturated frags/s x (DSM MACs per signature of the resident batch + "
                                           "decompression's %d) vs the integer-multiply peak; frac over the whole run (its ramp and "
                                           "drain included), frac_steady over the input's 10-90 %% span" % MAC_DECOMP}
-            # three interleaved rounds of the two loads; each load reports the median p50 and the
-            # median p99 of its three runs (the other fields from its median-p50 run): a single
-            # run's p50 moved by up to 2 % between back-to-back runs on one box
+            # three interleaved rounds of the two loads (a single run's p50 moved by up to 2 %
+            # between back-to-back runs on one box)
             runs = {0.5: [], 0.8: []}
             for _ in range(3):
                 for load in (0.5, 0.8):
                     runs[load].append(paced(bmax, zc, load * sat["frags_per_s"]))
             for load, rs in runs.items():
+                # p50 is the median of the three runs' p50; the tail is the WORST run's p99 / p50 (a
+                # single bad run must fail the row: VERDICT r04 weak 2, 9); every run is kept whole
                 med = sorted(rs, key=lambda x: x["p50_us"])[1]
-                r = dict(med)
-                r["p99_us"] = sorted(x["p99_us"] for x in rs)[1]
-                r["p99_over_p50"] = r["p99_us"] / max(r["p50_us"], 1e-3)
-                r["runs"] = [{"p50_us": x["p50_us"], "p99_us": x["p99_us"], "frags_per_s": x["frags_per_s"]} for x in rs]
+                worst = max(rs, key=lambda x: x["p99_over_p50"])
+                r = {"p50_us": med["p50_us"], "frags_per_s": med["frags_per_s"],
+                     "offered_frags_per_s": med["offered_frags_per_s"],
+                     "worst_p99_us": worst["p99_us"], "worst_p99_over_p50": worst["p99_over_p50"],
+                     "worst_run": rs.index(worst), "runs": rs}
                 rr["at_%d%%" % int(load * 100)] = r
             lo, hi = rr["at_50%"], rr["at_80%"]
-            # within 1 % (medians of three runs; both loads run throughput chunks above batch_max 256)
-            rr["p50_nondecreasing_with_load"] = hi["p50_us"] >= 0.99 * lo["p50_us"]
-            rr["p99_within_2_5x_p50"] = max(lo["p99_over_p50"], hi["p99_over_p50"]) <= 2.5
+            # medians of three runs, no slack
+            rr["p50_nondecreasing_with_load"] = hi["p50_us"] >= lo["p50_us"]
+            rr["p99_within_2_5x_p50"] = max(lo["worst_p99_over_p50"], hi["worst_p99_over_p50"]) <= 2.5
             row[key] = rr
         rows.append(row)
     fixed = {}
@@ -483,6 +617,8 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
         for zc in (False, True):
             fixed["zero_copy" if zc else "copy"] = paced(4096, zc, 1e6)
     allr = [r[k] for r in rows for k in ("copy", "zero_copy") if k in r]
+    for k, r in fixed.items():
+        r["p99_within_2_5x_p50"] = r["p99_over_p50"] <= 2.5
     out = {"path": "producer (metadata only; frames pre-placed in the data region as a NIC would) -> in "
                    "mcache/dcache -> verify tile (one persistent GPU kernel fed through mapped ring/descriptor "
                    "memory; latency chunks of 8 frags below the rate switch, 64-frag chunks above; copy: frag copied "
@@ -660,7 +796,7 @@ def run_multi_engine(args):
     finally:
         m.close()
     nodes = [ed25519.device_numa_node(d) for d in sorted(set(devices))]
-    print(json.dumps({
+    emit({
         "metric": METRIC, "value": g * n * args.steps / dt, "unit": "verifies/s", "n_gpus": g,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": DTYPE,
@@ -674,7 +810,7 @@ def run_multi_engine(args):
         "verdicts_match_single_engine": bool(all(np.array_equal(err[k * n:(k + 1) * n], err1) for k in range(g))),
         "path": "host SoA -> fd_ed25519_amd_multi_verify_soa: per device one NUMA-bound thread, pinned staging (2 "
                 "chunks in flight) -> H2D -> kernels -> mapped verdicts",
-    }))
+    }, args)
 
 
 # ---------------------------------------------------------------- configs[1]
@@ -929,7 +1065,7 @@ def main():
                                            args.cpu_seconds)
         if "dropin_call_us" in out:
             out["dropin_call_us"]["reference_us_per_call_this_host"] = out["cpu_baseline"]["us_per_call_1_thread"]
-    print(json.dumps(out))
+    emit(out, args)
 
 
 if __name__ == "__main__":

@@ -44,7 +44,7 @@ def _stale(out, deps):
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build_engine(force=False, verbose=False, out=None, defines=()):
+def build_engine(force=False, verbose=False, out=None, defines=(), vgpr_guard=True):
     """Compile every source to an object in parallel (one hipcc per file),
     then link the shared library."""
     consts = os.path.join(CSRC, "fd_ed25519_consts.h")
@@ -70,7 +70,7 @@ def build_engine(force=False, verbose=False, out=None, defines=()):
     with ThreadPoolExecutor(max_workers=min(len(SOURCES), max(1, min(8, os.cpu_count() or 1)))) as ex:
         list(ex.map(cc, range(len(SOURCES))))
     v = kernel_vgprs(objs[0], "_Z14k_tile_persist18fd_amd_tile_args_t")
-    if v is not None and v > TILE_VGPR_LIMIT:
+    if vgpr_guard and v is not None and v > TILE_VGPR_LIMIT:
         raise RuntimeError("k_tile_persist compiled to %d VGPRs (limit %d): at 256 its scout wave stops; "
                            "see profiles/r04_tile_scout_vgpr_ab.txt" % (v, TILE_VGPR_LIMIT))
     cmd = [_hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib + ".tmp"] + objs + ["-lpthread"]
@@ -107,7 +107,10 @@ def kernel_vgprs(obj, kernel):
 
 
 # k_tile_persist at 256 VGPRs: its scout wave stopped ~0.7 ms into every run
-# (round-4 A/B, profiles/r04_tile_scout_vgpr_ab.txt) -- refuse such a build
+# (round-4 A/B, profiles/r04_tile_scout_vgpr_ab.txt); round 5 showed the
+# scout's call and frame are not the cause (an inlined scout stops too) and
+# narrowed it to the 256-VGPR worker code (profiles/r05_scout_stop_cause.txt)
+# -- refuse such a build
 TILE_VGPR_LIMIT = 255
 
 
@@ -154,6 +157,7 @@ if __name__ == "__main__":
     elif "--variant" in sys.argv:
         k = sys.argv.index("--variant")
         out, defs = sys.argv[k + 1], [d for d in sys.argv[k + 2].split(",") if d]
-        print(build_engine(force=True, verbose=True, out=os.path.abspath(out), defines=defs))
+        print(build_engine(force=True, verbose=True, out=os.path.abspath(out), defines=defs,
+                           vgpr_guard="--no-vgpr-guard" not in sys.argv))
     else:
         print(build(force="--force" in sys.argv, verbose=True))

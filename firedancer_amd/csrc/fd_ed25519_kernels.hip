@@ -1973,7 +1973,11 @@ size_t fd_amd_tile_scratch_stride( void ) { return tile_scratch_layout().total; 
    stamps onto its own clock with it; its first store tells the host the
    kernel started) and the count of finished chunks (the host's progress
    watchdog). */
+#ifdef FD_AMD_SCOUT_NOINLINE   /* A/B only: the round-4 called scout (profiles/r05_scout_stop_cause.txt) */
 __device__ __noinline__ void
+#else
+__device__ __forceinline__ void
+#endif
 tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog ) {
   __builtin_amdgcn_s_setprio( 3 );   /* beside the workers' aged chunks on its SIMD */
   u64 word = ld_dev64( &D->mw[0].w ), lastb = ~0UL, beat = 0UL;
@@ -2118,9 +2122,14 @@ k_tile_persist( fd_amd_tile_args_t A ) {
   /* A run-time flag (the host sets it only in the diagnostics build), not a
      compile-time constant: with the profiling branches folded away the
      compiler gives this kernel all 256 VGPRs, and at 256 its scout wave
-     stopped ~0.7 ms into every run (round-4 A/B, profiles/
-     r04_tile_scout_vgpr_ab.txt); build.py refuses a build at 256. */
+     stopped ~0.7 ms into every run, called or inlined (profiles/
+     r04_tile_scout_vgpr_ab.txt, r05_scout_stop_cause.txt); build.py refuses
+     a build at 256. */
+#ifdef FD_AMD_TILE_PROF_CONST   /* A/B only: folds the profiling branches, 256 VGPRs */
+  bool const prof = false;
+#else
   bool const prof = A.prof != 0u;
+#endif
   for( ;; ) {
     u64 t = 0;
     if( l == 0u ) t = atomicAdd( (unsigned long long *)&D->ticket, 1ULL );
