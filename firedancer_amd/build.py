@@ -69,16 +69,56 @@ def build_engine(force=False, verbose=False, out=None, defines=(), vgpr_guard=Tr
 
     with ThreadPoolExecutor(max_workers=min(len(SOURCES), max(1, min(8, os.cpu_count() or 1)))) as ex:
         list(ex.map(cc, range(len(SOURCES))))
-    v = kernel_vgprs(objs[0], "_Z14k_tile_persist18fd_amd_tile_args_t")
-    if vgpr_guard and v is not None and v > TILE_VGPR_LIMIT:
-        raise RuntimeError("k_tile_persist compiled to %d VGPRs (limit %d): at 256 its scout wave stops; "
-                           "see profiles/r04_tile_scout_vgpr_ab.txt" % (v, TILE_VGPR_LIMIT))
+    n = loop_spill_stores(objs[0], TILE_KERNEL)
+    if vgpr_guard and n:
+        raise RuntimeError("k_tile_persist spills VGPRs to scratch inside its persistent loop (%d scratch stores after "
+                           "the first s_sleep): every such build lost its scout wave on hardware; see "
+                           "profiles/r05_scout_stop_cause.txt" % n)
     cmd = [_hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib + ".tmp"] + objs + ["-lpthread"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd, cwd=CSRC)
     os.replace(lib + ".tmp", lib)
     return lib
+
+
+def _device_object(obj):
+    """Extract the gfx950 code object of a compiled .hip object; returns
+    (path, cleanup paths), or None when the LLVM tools are missing."""
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not os.path.exists(os.path.join(llvm, "llvm-objdump")):
+        return None
+    subprocess.check_call([os.path.join(llvm, "llvm-objdump"), "--offloading", obj], stdout=subprocess.DEVNULL,
+                          stderr=subprocess.DEVNULL)
+    co = obj + ".0.hipv4-amdgcn-amd-amdhsa--" + ARCH
+    return co, (co, obj + ".0.host-x86_64-unknown-linux-gnu-")
+
+
+def loop_spill_stores(obj, kernel):
+    """scratch_store instructions of `kernel` after its first s_sleep (the
+    persistent loop's wait): 0 when the kernel spills only in its prologue,
+    None when the LLVM tools are missing."""
+    d = _device_object(obj)
+    if d is None:
+        return None
+    co, tmp = d
+    try:
+        dis = subprocess.check_output(["/opt/rocm/lib/llvm/bin/llvm-objdump", "-d", co], text=True)
+    finally:
+        for f in tmp:
+            if os.path.exists(f):
+                os.remove(f)
+    lines, inside = [], False
+    for ln in dis.splitlines():
+        if ln.endswith(">:") and " <" in ln:
+            if inside:
+                break
+            inside = ln.split(" <", 1)[1][:-2] == kernel
+            continue
+        if inside:
+            lines.append(ln)
+    first = next((i for i, ln in enumerate(lines) if "s_sleep" in ln), len(lines))
+    return sum("scratch_store" in ln for ln in lines[first:])
 
 
 def kernel_vgprs(obj, kernel):
@@ -106,12 +146,12 @@ def kernel_vgprs(obj, kernel):
     return int(m.group(1)) if m else None
 
 
-# k_tile_persist at 256 VGPRs: its scout wave stopped ~0.7 ms into every run
-# (round-4 A/B, profiles/r04_tile_scout_vgpr_ab.txt); round 5 showed the
-# scout's call and frame are not the cause (an inlined scout stops too) and
-# narrowed it to the 256-VGPR worker code (profiles/r05_scout_stop_cause.txt)
-# -- refuse such a build
-TILE_VGPR_LIMIT = 255
+# k_tile_persist's scout wave stopped ~0.7 ms into every run of the builds
+# that spill VGPRs inside the persistent loop (round 4: every 256-VGPR build,
+# profiles/r04_tile_scout_vgpr_ab.txt; round 5: an inlined scout stops too,
+# while a 256-VGPR build that spills only in its prologue runs clean,
+# profiles/r05_scout_stop_cause.txt) -- refuse such a build
+TILE_KERNEL = "_Z14k_tile_persist18fd_amd_tile_args_t"
 
 
 def build_diag(force=False, verbose=False):

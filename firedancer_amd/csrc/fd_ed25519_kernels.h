@@ -56,16 +56,6 @@ int fd_amd_launch_txn_reduce( uint32_t txn_cnt, uint32_t const * d_fp, uint32_t 
 int fd_amd_launch_sign( uint32_t n, uint8_t const * d_prv, uint32_t const * d_off, uint32_t const * d_sz,
                         uint8_t const * d_blob, uint8_t * d_pub, uint8_t * d_sig, hipStream_t stream );
 
-/* Streaming-tile staging (k_tile_gather).  d_meta = [ichunk n | ochunk n |
-   fsz n] (u32): frag i is copied from d_src + 64*ichunk[i] (mapped host data
-   region) into frame i of d_mir (stride bytes apart, device) and, when
-   d_out != NULL, to d_out + 64*ochunk[i] (mapped output dcache).  txn == 0
-   (pub|sig|msg): d_pub/d_sig planes + msg_off/msg_sz into d_mir; txn == 1:
-   payload offset/size into d_mir in d_off/d_sz. */
-int fd_amd_launch_tile_gather( uint32_t n, uint32_t const * d_meta, uint8_t const * d_src, uint8_t * d_out,
-                               uint8_t * d_mir, uint32_t stride, int txn, uint8_t * d_pub, uint8_t * d_sig,
-                               uint32_t * d_off, uint32_t * d_sz, hipStream_t stream );
-
 /* Streaming tile, persistent consumer (k_tile_persist).  One launch per
    tile run; its waves take chunk descriptors the tile's host thread
    publishes in mapped host memory and verify them, so the GPU never drains
@@ -73,10 +63,12 @@ int fd_amd_launch_tile_gather( uint32_t n, uint32_t const * d_meta, uint8_t cons
 
    ring entry (host -> GPU): the frag's chunk in the source region, its
    output frame's chunk (zero-copy: the GPU writes the verified bytes
-   there), its size.  Entry of ring index j at ent[j & mask]. */
-typedef struct { uint32_t src_chunk, out_chunk, sz, pad; } fd_amd_tile_ent_t;
+   there), its size, and (TXN framing) its signature slots
+   (fd_amd_txn_slots1).  Entry of ring index j at ent[j & mask]. */
+typedef struct { uint32_t src_chunk, out_chunk, sz, slots; } fd_amd_tile_ent_t;
 /* chunk descriptor (host -> GPU): ring entries [first, first + count),
-   count <= 64 | FD_AMD_TILE_LAT (8 lanes per signature) */
+   count <= 64 | FD_AMD_TILE_LAT (8 lanes per signature); the entries'
+   signature slots total <= 64 (<= 8 in a latency chunk) */
 typedef struct { uint64_t first; uint32_t count; uint32_t pad; } fd_amd_tile_desc_t;
 #define FD_AMD_TILE_LAT (0x80000000u)
 /* result of ring index j (GPU -> host), two arrays of R words: tag[j & mask]
@@ -122,6 +114,7 @@ typedef struct {
   uint8_t *                  scratch;  /* per-wave scratch, fd_amd_tile_scratch_stride() bytes apart */
   uint64_t                   watchdog; /* s_memrealtime ticks (100 MHz) without a host heartbeat before the kernel gives up */
   uint32_t                   prof;     /* diagnostics build only: sum per-phase time stamps into dctl->prof */
+  uint32_t                   txn;      /* TXN framing: entries are wire transactions, results per transaction */
 } fd_amd_tile_args_t;
 size_t fd_amd_tile_scratch_stride( void );
 /* waves: grid size (wave 0 is the scout that mirrors the host words) */

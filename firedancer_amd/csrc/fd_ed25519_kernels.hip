@@ -39,6 +39,7 @@
 
 #include "fd_ed25519_dev.h"
 #include "fd_ed25519_kernels.h"
+#include "fd_txn_dev.h"
 #include <stdlib.h>
 
 typedef int8_t i8;
@@ -1850,55 +1851,6 @@ k_fin( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
 }
 
 /* ------------------------------------------------------------------ */
-/* k_tile_gather: the streaming tile's staging.  Frag i (fsz[i] bytes at
-   chunk ichunk[i] of `src`, host memory mapped into the GPU: the input
-   dcache in zero-copy mode, the tile's own output dcache in copy mode) is
-   copied into frame i of the slot's device frame buffer `mir` (stride B
-   apart) and, when `out` != NULL (zero-copy mode), into chunk ochunk[i] of
-   the tile-owned output dcache, so the bytes the tile publishes are the
-   bytes it verified.  PUB_SIG_MSG frags also get their SoA planes (pub,
-   sig; the message stays in `mir`), TXN frags their payload offset/size in
-   `mir`.  One wave per frag (4 per block), 16 B per lane: the frames are
-   chunk-aligned, so every 16-B word is whole; the tail word past fsz stays
-   inside the frag's chunk pair. */
-__global__ void __launch_bounds__(256)
-k_tile_gather( u32 n, u32 const * __restrict__ meta, u8 const * __restrict__ src, u8 * __restrict__ out,
-               u8 * __restrict__ mir, u32 stride, int txn, u8 * __restrict__ pub, u8 * __restrict__ sig,
-               u32 * __restrict__ moff, u32 * __restrict__ msz ) {
-  u32 i = blockIdx.x * 4u + (threadIdx.x >> 6), l = threadIdx.x & 63u;
-  if( i >= n ) return;
-  u32 ic = meta[i], oc = meta[n + i], sz = meta[2u*n + i];
-  uint4 const * s = (uint4 const *)(src + ((size_t)ic << 6));
-  uint4 * m = (uint4 *)(mir + (size_t)i * stride);
-  uint4 * o = out ? (uint4 *)(out + ((size_t)oc << 6)) : (uint4 *)0;
-  u32 nv = (sz + 15u) >> 4;
-  uint4 v0 = make_uint4( 0u, 0u, 0u, 0u );
-  for( u32 k = l; k < nv; k += 64u ) {
-    uint4 v = s[k];
-    if( k == l ) v0 = v;
-    m[k] = v;
-    if( o ) o[k] = v;
-  }
-  if( txn ) {
-    if( !l ) { moff[i] = i * stride; msz[i] = sz; }
-  } else {
-    if( l < 2u )      ((uint4 *)(pub + 32UL*i))[l]      = v0;     /* host checked fsz >= 96 */
-    else if( l < 6u ) ((uint4 *)(sig + 64UL*i))[l - 2u] = v0;
-    if( !l ) { moff[i] = i * stride + 96u; msz[i] = sz - 96u; }
-  }
-}
-
-int
-fd_amd_launch_tile_gather( uint32_t n, uint32_t const * d_meta, uint8_t const * d_src, uint8_t * d_out,
-                           uint8_t * d_mir, uint32_t stride, int txn, uint8_t * d_pub, uint8_t * d_sig,
-                           uint32_t * d_off, uint32_t * d_sz, hipStream_t stream ) {
-  if( !n ) return 0;
-  hipLaunchKernelGGL( k_tile_gather, dim3((n + 3u)/4u), dim3(256), 0, stream, n, d_meta, d_src, d_out, d_mir, stride, txn,
-                      d_pub, d_sig, d_off, d_sz );
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-/* ------------------------------------------------------------------ */
 /* k_tile_persist: the streaming tile's persistent consumer.
  *
  * The reference verify tile (src/app/frank/load/fd_frank_verify_synth_load.c:
@@ -1953,7 +1905,7 @@ __device__ __forceinline__ u64 rfl64( u64 v ) {
 #define TILE_MW_STOP     (1UL << 63)
 
 /* per-wave scratch: an N = 64 workspace, then the chunk's frames and planes */
-struct tile_scratch_t { size_t mir, pub, sig, off, sz, err, total; };
+struct tile_scratch_t { size_t mir, pub, sig, off, sz, err, skp, tx, total; };
 __host__ __device__ constexpr tile_scratch_t tile_scratch_layout( void ) {
   tile_scratch_t S = {}; size_t o = ws_al( ws_layout_const( 64 ).total );
   S.mir = o; o = ws_al( o + 64UL*TILE_FRAME );
@@ -1962,6 +1914,8 @@ __host__ __device__ constexpr tile_scratch_t tile_scratch_layout( void ) {
   S.off = o; o = ws_al( o + 64UL*4UL );
   S.sz  = o; o = ws_al( o + 64UL*4UL );
   S.err = o; o = ws_al( o + 64UL );
+  S.skp = o; o = ws_al( o + 64UL );          /* TXN: per slot, nonzero = its transaction failed to parse */
+  S.tx  = o; o = ws_al( o + 64UL*4UL );      /* TXN: per entry, first slot | slots << 8 | parsed << 31 */
   S.total = o;
   return S;
 }
@@ -2008,8 +1962,82 @@ tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog ) {
   }
 }
 
+/* nw little-endian words from an unaligned address inside a frame: nw + 1
+   aligned dword loads funnel-shifted by the misalignment (the frame has
+   room for the extra word: frames are FD_VERIFY_AMD_FRAME_SZ >= MTU + 4). */
+template<int NW>
+__device__ __forceinline__ void
+ld_words_unaligned( u8 const * p, u32 (&o)[NW] ) {
+  u32 const * a = (u32 const *)((size_t)p & ~(size_t)3);
+  u32 const sh = (u32)(size_t)p & 3u;
+  u32 w[NW + 1];
+  _Pragma("unroll") for( int k=0; k<=NW; k++ ) w[k] = a[k];
+  _Pragma("unroll") for( int k=0; k<NW; k++ ) o[k] = __builtin_amdgcn_alignbyte( w[k+1], w[k], sh );   /* byte shift */
+}
+
+/* TXN framing: the chunk's k ring entries are wire transactions (frames
+   0..k-1 of mir) carrying e_k signature slots each (the host's count,
+   fd_amd_txn_slots1; the chunk's total <= 64).  Lane q < k parses
+   transaction q (fd_txn_parse semantics, fd_txn_dev.h); lane s < n then
+   lays slot s out for the verify bodies: signature i of its transaction
+   with account address i over the shared message bytes in mir
+   (fd_txn.h:159-217), or skip = FD_TXN_AMD_ERR_PARSE when the transaction
+   failed to parse (or parsed to a signature count other than the host's:
+   fail closed).  tx[q] keeps the entry's first slot, slot count and parse
+   flag for the per-transaction reduce.  lds: >= 64 x 5 words of scratch
+   LDS (the DSM bodies' event rows, unused until then).  Returns n, the
+   chunk's signature slots (wave-uniform). */
+__device__ __forceinline__ u32
+tile_txn_layout( u32 l, u32 k, u32 e_sz, u32 e_k, u8 const * __restrict__ mir, u8 * __restrict__ pub,
+                 u8 * __restrict__ sig, u32 * __restrict__ off, u32 * __restrict__ sz, i8 * __restrict__ skp,
+                 u32 * __restrict__ tx, u32 * __restrict__ lds ) {
+  u32 const kk = l < k ? e_k : 0u;
+  u32 inc = kk;
+  _Pragma("unroll") for( int d=1; d<64; d<<=1 ) {
+    u32 const o = (u32)__shfl_up( (int)inc, (unsigned)d );
+    if( l >= (u32)d ) inc += o;
+  }
+  u32 const base = inc - kk;
+  u32 const n = min( (u32)__shfl( (int)inc, 63 ), 64u );
+  u32 * own  = lds;            /* [64]: slot -> entry */
+  u32 * info = lds + 64;       /* [64][5]: sig_off, acct_off, msg_off (~0: not parsed), frag size, first slot */
+  if( l < k ) {
+    u32 nsig = 0u, sig_off = 0u, acct_off = 0u, msg_off = 0u;
+    u32 const fp = fd_txn_dev::txn_parse( mir + (size_t)l * TILE_FRAME, e_sz, (u8 *)0, &nsig, &sig_off, &acct_off, &msg_off );
+    u32 const ok = fp != 0u && nsig == kk && base + kk <= 64u;   /* the host packs <= 64 slots per chunk */
+    for( u32 i=0u; i<kk && base + i < 64u; i++ ) own[base + i] = l;
+    u32 * in = info + 5u*l;
+    in[0] = sig_off; in[1] = acct_off; in[2] = ok ? msg_off : 0xFFFFFFFFu; in[3] = e_sz; in[4] = base;
+    tx[l] = base | (kk << 8) | (ok << 31);
+  }
+  __syncthreads();
+  if( l < n ) {
+    u32 const q = own[l];
+    u32 const * in = info + 5u*q;
+    u32 const i = l - in[4];
+    u32 const msg_off = in[2];
+    if( msg_off != 0xFFFFFFFFu ) {
+      u8 const * f = mir + (size_t)q * TILE_FRAME;
+      u32 a[8], g[16];
+      ld_words_unaligned<8>( f + in[1] + 32u*i, a );
+      ld_words_unaligned<16>( f + in[0] + 64u*i, g );
+      uint4 * P = (uint4 *)(pub + 32u*l);
+      uint4 * G = (uint4 *)(sig + 64u*l);
+      P[0] = make_uint4( a[0], a[1], a[2], a[3] );   P[1] = make_uint4( a[4], a[5], a[6], a[7] );
+      G[0] = make_uint4( g[0], g[1], g[2], g[3] );   G[1] = make_uint4( g[4], g[5], g[6], g[7] );
+      G[2] = make_uint4( g[8], g[9], g[10], g[11] ); G[3] = make_uint4( g[12], g[13], g[14], g[15] );
+      off[l] = q * TILE_FRAME + msg_off; sz[l] = in[3] - msg_off; skp[l] = 0;
+    } else {
+      off[l] = 0u; sz[l] = 0u; skp[l] = (i8)TXN_ERR_PARSE;
+    }
+  }
+  return n;
+}
+
 /* Verify ring entries [c0, c0 + k) (k <= 64) on this wave, claimed at
-   s_memrealtime tc. */
+   s_memrealtime tc.  PUB_SIG_MSG: entry q is signature slot q.  TXN
+   (A.txn): entry q is a wire transaction whose slots tile_txn_layout lays
+   out, and its result is the transaction's verdict. */
 __device__ __forceinline__ void
 tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __restrict__ scr, ws_layout_t L,
             tile_scratch_t const & S, i32 (* __restrict__ bi)[48], u64 (* __restrict__ evl)[33], u64 * pt, u64 tc ) {
@@ -2031,11 +2059,12 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __rest
   u32 * off = (u32 *)(scr + S.off); u32 * sz = (u32 *)(scr + S.sz); i8 * err = (i8 *)(scr + S.err);
 
   /* 1. the chunk's ring entries, lane q holds entry q (host memory: system-scope loads) */
-  u32 e_src = 0u, e_out = 0u, e_sz = 96u;
+  bool const txn = A.txn != 0u;
+  u32 e_src = 0u, e_out = 0u, e_sz = 96u, e_k = 0u;
   if( l < k ) {
     u64 const * ep = (u64 const *)(A.ent + ((c0 + l) & A.mask));
     u64 w0 = ld_sys64( ep ), w1 = ld_sys64( ep + 1 );
-    e_src = (u32)w0; e_out = (u32)(w0 >> 32); e_sz = (u32)w1;
+    e_src = (u32)w0; e_out = (u32)(w0 >> 32); e_sz = (u32)w1; e_k = (u32)(w1 >> 32);
   }
   /* 2. copy the frags in: four frags per round, 16 lanes each, up to six
         16-B words per lane issued before any is stored (frames <= 1328 B =
@@ -2060,36 +2089,54 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __rest
         u32 w = j + 16u*(u32)r;
         if( w < nv ) { m[w] = v[r]; if( o ) o[w] = v[r]; }
       }
-      if( q < k ) {
+      if( q < k && !txn ) {
         if( j < 2u )      ((uint4 *)(pub + 32u*q))[j]      = v[0];
         else if( j < 6u ) ((uint4 *)(sig + 64u*q))[j - 2u] = v[0];
       }
     }
-    if( l < k ) { off[l] = l * TILE_FRAME + 96u; sz[l] = e_sz - 96u; }
+    if( l < k && !txn ) { off[l] = l * TILE_FRAME + 96u; sz[l] = e_sz - 96u; }
   }
   __syncthreads();
+  /* TXN: parse and lay the chunk's signature slots out (n of them) */
+  i8 * skp = (i8 *)(scr + S.skp);
+  u32 * tx = (u32 *)(scr + S.tx);
+  u32 const n = txn ? tile_txn_layout( l, k, e_sz, e_k, mir, pub, sig, off, sz, skp, tx, (u32 *)&evl[0][0] ) : k;
+  if( txn ) __syncthreads();
   TILE_STAMP( 0 );
   /* 3. the verify pipeline on the chunk (k_prep, k_decomp, k_dsm8 / k_dsm bodies) */
-  prep_body( l, k, pub, sig, off, sz, mir, err, ws, L, (i8 const *)0 );
+  prep_body( l, n, pub, sig, off, sz, mir, err, ws, L, txn ? (i8 const *)skp : (i8 const *)0 );
   __syncthreads();
   TILE_STAMP( 6 );
-  decomp_body( l, k, pub, sig, err, ws, L, true );                 /* points 0..63: signatures 0..31 */
-  if( k > 32u ) decomp_body( l + 64u, k, pub, sig, err, ws, L, true );
+  decomp_body( l, n, pub, sig, err, ws, L, true );                 /* points 0..63: signatures 0..31 */
+  if( n > 32u ) decomp_body( l + 64u, n, pub, sig, err, ws, L, true );
   __syncthreads();
   TILE_STAMP( 1 );
-  if( eight ) dsm8_body( l, k, err, ws, L, 0, bi, evl, tc );
-  else        dsm_lane_body( l, k, err, ws, L, 0, bi, evl, tc );
+  if( eight ) dsm8_body( l, n, err, ws, L, 0, bi, evl, tc );
+  else        dsm_lane_body( l, n, err, ws, L, 0, bi, evl, tc );
   __builtin_amdgcn_s_setprio( 0 );
   __syncthreads();
   TILE_STAMP( 2 );
   /* 4. results: tags (and, zero-copy, the output frames above) first, one
-        system-scope release, then the words the host polls */
+        system-scope release, then the words the host polls.  TXN: an entry's
+        verdict is its parse failure, else the first failing signature's
+        code in signature order, else 0 (k_txn_reduce); its tag is its first
+        signature's */
   u64 const idx = c0 + l, j = idx & A.mask;
-  if( l < k ) st_sys64( A.res_tag + j, ((u64 const *)(ws + L.tag))[l] );
+  u64 tag = 0UL; i8 v = 0;
+  if( l < k ) {
+    if( !txn ) { tag = ((u64 const *)(ws + L.tag))[l]; v = err[l]; }
+    else {
+      u32 const w = tx[l], b = w & 0xffu, kk = (w >> 8) & 0xffu;
+      if( !(w >> 31) ) v = (i8)TXN_ERR_PARSE;
+      else for( u32 i=0u; i<kk; i++ ) { i8 const e = err[b + i]; if( e ) { v = e; break; } }
+      if( kk ) tag = ((u64 const *)(ws + L.tag))[b];
+    }
+    st_sys64( A.res_tag + j, tag );
+  }
   if( A.res_time && l < k ) st_sys64( A.res_time + j, (u64)(u32)tc | ((u64)(u32)__builtin_amdgcn_s_memrealtime() << 32) );
   __builtin_amdgcn_fence( __ATOMIC_RELEASE, "" );
   asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
-  u64 const wd = ((idx + 1UL) << 8) | (u64)(u8)err[l];
+  u64 const wd = ((idx + 1UL) << 8) | (u64)(u8)v;
   if( l < k ) st_sys64( A.res_word + j, wd );
   TILE_STAMP( 3 );
 # undef TILE_STAMP

@@ -5,8 +5,8 @@
  *
  * The reference verify tile (src/app/frank/load/fd_frank_verify_synth_load.c:
  * 219-437) verifies one frag per fd_ed25519_verify call.  Here the run loop
- * is split into a host side that never blocks on the GPU and a GPU side that
- * verifies whole chunks of frags:
+ * is split into a host side that never blocks on the GPU and ONE persistent
+ * GPU kernel per run (k_tile_persist) that verifies whole chunks of frags:
  *
  *   poll    -- read the next input frag metadata (seq-checked, overrun-aware)
  *   dedup   -- HA tag cache (tag = first 8 signature bytes), FD_TCACHE_INSERT
@@ -15,14 +15,17 @@
  *   stage   -- reserve a frame of the tile-owned output dcache; copy mode:
  *              copy the frag into it, re-check the mcache line, release the
  *              input frag; zero-copy: hand the GPU (chunk, size) only
- *   hand    -- PUB_SIG_MSG framing: cut staged frags into chunks for the
- *              persistent GPU consumer (k_tile_persist) by the load; TXN
- *              framing: launch batches, up to 4 in flight on 4 streams
+ *   hand    -- cut staged frags into chunks for the persistent kernel by the
+ *              load.  PUB_SIG_MSG framing: a frag is one signature slot;
+ *              TXN framing: a frag is a wire transaction whose signature
+ *              count the host reads from its first byte, chunks are packed
+ *              by signature slots and the GPU parses, verifies every
+ *              signature and reduces per transaction
  *   publish -- in arrival order (fd_mcache_publish protocol) out of the
  *              output dcache, with the GPU's SHA-512-derived dedup tag as
  *              meta.sig; failures count SV_FILT; zero-copy releases input
- *              frags only now.  The persistent path publishes from a second
- *              host thread when the tile has a CPU for it.
+ *              frags only now.  Publishing runs on a second host thread when
+ *              the tile has a CPU for it.
  *
  * The output data region follows the reference tile's ownership model: the
  * tile publishes frags from a dcache it owns (fd_frank_verify_synth_load.c:
@@ -34,6 +37,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <dirent.h>
+#include <unistd.h>
+#include <sys/syscall.h>
 #include <x86intrin.h>
 #include <thread>
 #include <sched.h>
@@ -44,6 +50,7 @@
 #include <algorithm>
 
 #include "../../include/fd_ed25519_amd.h"
+#include "../../include/fd_txn_amd.h"
 #include "../../include/fd_tango_amd.h"
 #include "fd_ed25519_engine.h"
 #include "fd_ed25519_kernels.h"
@@ -104,14 +111,15 @@ struct tcache_t {
   }
 };
 
-struct pending_t {            /* one staged / in-flight frag */
+struct pending_t {            /* one staged / in-flight frag (ring entry) */
   ulong  seq;                 /* input sequence number */
-  ulong  frame;               /* output frame reservation (monotonic) */
   ushort sz, ctl;
   uint   tsorig;
-  uint   fidx;                /* frame % frame_cnt (kept incrementally: no division per frag) */
+  uint   fidx;                /* its output frame */
   uint   t_stage;             /* host clock (low 32 bits of ns) when staged */
-  uint   t_hand;              /* ... when its chunk was handed over (persistent path) */
+  uint   t_hand;              /* ... when its chunk was handed over (bit 0: latency chunk) */
+  uint   sl_end;              /* signature slots staged up to and including this entry (mod 2^32) */
+  uint   slots;               /* its signature slots (PUB_SIG_MSG: 1; TXN: fd_amd_txn_slots1) */
   uint   pad;
 };
 
@@ -146,27 +154,122 @@ inline ulong now_ns( void ) {
 #define FRAME_CHUNKS ((uint)(FD_VERIFY_AMD_FRAME_SZ >> FD_CHUNK_LG_SZ))
 #define FRAME_FREE   (~0UL)
 #define TXN_SIG_MAX_AT_MTU (19UL)   /* most signatures fd_amd_txn_slots1 reserves for a 1232-B payload */
-#define TILE_NSLOT   (4)            /* TXN batches in flight (6 or 8 measured: higher p50 at every batch_max) */
-#define STAGE_PASS   (256UL)        /* frags staged per pass of the persistent loop before it hands over */
+#define STAGE_PASS   (256UL)        /* frags staged per pass of the run loop before it hands over */
+#define CHUNK_SLOTS  (64UL)         /* signature slots of a throughput chunk (one lane each) */
+#define LAT_SLOTS    (8UL)          /* ... of a latency chunk (8 lanes each) */
 
-struct tile_slot_t {
-  uint32_t * h_meta;             /* pinned, mapped: [ichunk n | ochunk n | fsz n | tbase n+1] of the batch */
-  uint32_t * m_meta;             /* its device address (the kernels read it in place) */
-  uint8_t  * d_mir;              /* device frames of the batch, FD_VERIFY_AMD_FRAME_SZ apart */
-  std::vector<pending_t> pend;
-  std::vector<uint32_t>  ich, fsz, tb;
-  ulong seq_lo;                  /* first input seq of the batch (zero-copy release point) */
-  ulong frame_hi;                /* frame reservation counter after the batch's last frame */
-  ulong nsig;                    /* signature slots (TXN) */
+/* Copy mode's helper protocol (below) */
+#define CP_BLK      (8UL)                    /* frags per claimed copy block */
+#define CP_NJ       (4UL)                    /* job arrays in the helper's ring */
+#define CP_NB       (STAGE_PASS / CP_BLK)    /* blocks per pass at most */
+#define CP_STEAL_NS (30000UL)                /* a helper block still unfinished this long after the stager ran out of
+                                                blocks is re-copied by the stager into fresh frames */
+#define COPY_SPLIT_MIN (32UL)                /* passes of fewer frags are copied on the stager alone */
+
+/* Copy mode's staging copy: whole 16-B words (a frag's chunks are 64-B
+   granular, so the rounded-up tail stays inside its own chunks) with
+   non-temporal stores -- the frame is read next by the GPU over PCIe, not by
+   this CPU, so it skips the read-for-ownership of every destination line and
+   stays out of the cache.  Weakly ordered: the stager fences (sfence) before
+   it publishes the head that hands the frames over. */
+static inline void
+stage_copy_nt( uchar * dst, uchar const * src, ulong sz ) {
+  ulong const n = (sz + 15UL) >> 4;
+  __m128i const * s = (__m128i const *)src;
+  __m128i * d = (__m128i *)dst;
+  ulong k = 0;
+  for( ; k + 4UL <= n; k += 4UL ) {
+    __m128i const a = _mm_loadu_si128( s + k ), b = _mm_loadu_si128( s + k + 1 );
+    __m128i const c = _mm_loadu_si128( s + k + 2 ), e = _mm_loadu_si128( s + k + 3 );
+    _mm_stream_si128( d + k, a ); _mm_stream_si128( d + k + 1, b );
+    _mm_stream_si128( d + k + 2, c ); _mm_stream_si128( d + k + 3, e );
+  }
+  for( ; k < n; k++ ) _mm_stream_si128( d + k, _mm_loadu_si128( s + k ) );
+}
+
+/* Copy mode's deferred staging: a pass first reserves a frame per frag and
+   lists the copies, then copies them, and only then re-checks each frag's
+   mcache line and stages it (a frag lapped during its copy leaves its frame
+   unused). */
+struct copy_job_t {
+  uchar *                dst;
+  uchar const *          src;
+  fd_frag_meta_t const * m;
+  ulong                  seq, sz, tag;   /* tag: the HA dedup tag, read from the source before the copy */
+  uint                   f, tsorig, slots;
+  ushort                 ctl;
 };
+
+static void
+copy_jobs( copy_job_t const * j, ulong lo, ulong hi ) {
+  for( ulong k=lo; k<hi; k++ ) {
+    if( k + 2UL < hi ) for( ulong o = 0; o < j[k+2].sz; o += 64UL ) __builtin_prefetch( j[k+2].src + o );
+    stage_copy_nt( j[k].dst, j[k].src, j[k].sz );
+  }
+}
+
+/* The copy helper (cfg.copy_cpu).  A pass posts its job list as a
+   generation g into job array g % CP_NJ; the stager and the helper both
+   claim blocks of CP_BLK frags by CAS on `claim` (g << 16 | next block),
+   and the helper marks each block it copied in done[g % CP_NJ][b] = g.
+   The stager never waits on a helper that stopped running (a descheduled
+   pinned thread held a pass for up to 9 ms, profiles/r05_bench_a_detail.json):
+   a helper block still unfinished CP_STEAL_NS after the stager ran out of
+   blocks is copied again by the stager into FRESH frames, and the frames the
+   helper may still write stay reserved ("orphaned") until its done mark
+   shows up -- nothing ever reads them, so a late helper write (its source
+   possibly rewritten by then) cannot reach a published frag.  A job array
+   is reused only when none of its blocks is orphaned. */
+struct copier_t {
+  alignas(64) std::atomic<ulong> claim;
+  alignas(64) std::atomic<int>   quit;
+  alignas(64) std::atomic<ulong> done[CP_NJ][CP_NB];
+  std::atomic<ulong>             nj[CP_NJ];
+  copy_job_t                     jobs[CP_NJ][STAGE_PASS];
+};
+
+static void
+copier_loop( copier_t * cp, int cpu ) {
+  cpu_set_t one; CPU_ZERO( &one ); CPU_SET( cpu, &one );
+  (void)pthread_setaffinity_np( pthread_self(), sizeof one, &one );
+  for( ;; ) {
+    ulong c = cp->claim.load( std::memory_order_acquire );
+    ulong const g = c >> 16, b = c & 0xffffUL;
+    if( g ) {
+      ulong const s = g % CP_NJ, nj = cp->nj[s].load( std::memory_order_relaxed );
+      if( b * CP_BLK < nj ) {
+        if( cp->claim.compare_exchange_weak( c, c + 1UL, std::memory_order_acq_rel ) ) {
+          copy_jobs( cp->jobs[s], b * CP_BLK, std::min( nj, (b + 1UL) * CP_BLK ) );
+          _mm_sfence();   /* the copies before the done mark */
+          cp->done[s][b].store( g, std::memory_order_release );
+        }
+        continue;
+      }
+    }
+    if( cp->quit.load( std::memory_order_acquire ) ) break;
+    _mm_pause();
+  }
+}
+
+struct orphan_t { ulong g, s, b; std::vector<uint> frames; };
+
+/* The window rule: frags handed over and not yet published */
+static ulong
+tile_window( fd_verify_amd_tile_cfg_t const * c ) {
+  if( c->window ) return c->window;
+  /* in flight = rate x latency: ~1.3 ms at up to ~55 M frags/s under load,
+     plus a hand-off's worth of head-of-line wait (a window that binds at 80 %
+     load shows up as input wait in the tail) */
+  if( c->batch_max >= (1UL << 12) ) return 1UL << 18;
+  if( c->batch_max >= (1UL << 10) ) return 1UL << 17;
+  return std::max( 64UL * c->batch_max, 1UL << 15 );   /* latency chunks at ~18 M frags/s x ~1 ms */
+}
 
 struct fd_verify_amd_tile {
   fd_verify_amd_tile_cfg_t cfg;
-  fd_ed25519_amd_t * eng;
+  int                device;
   ulong              batch_max;
-  ulong              wait_ns;
   tcache_t           tc;
-  int                nslot;
   int                framing;   /* FD_VERIFY_AMD_FRAMING_* */
   int                cus;
   uint8_t *          reg_base;  /* host data region mapped into the GPU (zero copy) */
@@ -177,12 +280,10 @@ struct fd_verify_amd_tile {
   uint8_t *          out_dev;
   ulong              frame_cnt;
   std::vector<ulong> frame_pub;  /* out seq of the frag a frame last carried (FRAME_FREE: none) */
-  ulong              frame_next, frame_retired;
-  ulong              frame_next_idx;   /* frame_next % frame_cnt */
+  uint8_t *          frame_busy; /* 1 while a frame is staged, in flight, or orphaned (stager sets, publisher clears) */
+  ulong              frame_next_idx;   /* next frame to reserve (cyclic) */
   ulong              out_seq_end;   /* out seq after the last run's last publish (a run continuing it keeps frame_pub) */
-  bool               slots_ok;      /* the batch path's slots are allocated */
-  tile_slot_t        ts[FD_AMD_SLOT_MAX];
-  /* persistent consumer (PUB_SIG_MSG framing, k_tile_persist) */
+  /* persistent consumer (k_tile_persist) */
   bool                 persist_ok;  /* its resources are allocated */
   hipStream_t          pst;
   hipEvent_t           pdone;
@@ -198,7 +299,7 @@ struct fd_verify_amd_tile {
   ulong                window;     /* frags in flight at most (handed to the GPU, not yet published) */
   uint32_t             waves;      /* grid of a run (the share), fixed at the first run */
   double               rate_hi, rate_lo;
-  bool                 counted;       /* in the per-device PUB_SIG_MSG tile count */
+  bool                 counted;       /* in the per-device tile count */
   ulong                desc_seq;      /* descriptors published, monotonic over the tile's life */
   std::vector<pending_t> ppend;    /* per ring slot */
   std::vector<ulong>   desc_end;   /* per descriptor: ring index after its last frag */
@@ -206,10 +307,10 @@ struct fd_verify_amd_tile {
   ulong                pass_max_ns;   /* longest pass of the last run's loop (stall diagnosis) */
   uint *               trace;  ulong trace_max;
   schar *              vlog;   ulong vlog_max;
-  /* the last persistent run's loop: passes, hand-offs, and the passes whose
-     staging stopped at the window, the output frames, batch_max staged,
-     or the STAGE_PASS bound (bench diagnostics) */
-  ulong                n_pass, n_hand, n_stop_window, n_stop_frames, n_stop_bmax, n_stop_pass;
+  /* the last run's loop: passes, hand-offs, and the passes whose staging
+     stopped at the window, the output frames, batch_max staged, or the
+     STAGE_PASS bound; copy blocks the stager re-copied (helper stalls) */
+  ulong                n_pass, n_hand, n_stop_window, n_stop_frames, n_stop_bmax, n_stop_pass, n_steal;
   volatile int         started;    /* the current run's kernel wrote its first clock word */
 };
 
@@ -233,7 +334,7 @@ fd_verify_amd_tile_cfg_default( fd_verify_amd_tile_cfg_t * c ) {
 extern "C" int
 fd_verify_amd_tile_register_dcache( fd_verify_amd_tile_t * t, void * base, ulong sz ) {
   if( !t || !base || !sz ) return FD_ED25519_AMD_ERR_INVAL;
-  if( hipSetDevice( t->eng->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
+  if( hipSetDevice( t->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
   /* an unregister that fails (the range was unregistered elsewhere) must not
      leave its error pending for the next launch check (hipGetLastError) */
   if( t->reg_base ) {
@@ -251,30 +352,43 @@ fd_verify_amd_tile_register_dcache( fd_verify_amd_tile_t * t, void * base, ulong
   return FD_ED25519_AMD_OK;
 }
 
-/* Live PUB_SIG_MSG tiles per device (process-wide): a run's persistent
-   kernel takes 8 x CUs / (such tiles on its device) wave slots unless the
-   tile's cfg.waves fixes its share. */
+/* Live tiles per device (process-wide).  A run's persistent kernel takes
+   8 x CUs / (tiles on its device) wave slots unless cfg.waves fixes its
+   share.  Each tile's kernel occupies a hardware queue of the high-priority
+   pool for the whole run, and HIP shares GPU_MAX_HW_QUEUES queues per
+   priority among a process's streams: a tile beyond that count would queue
+   its kernel behind another tile's until that run ends, so creation refuses
+   it (tile_queue_max). */
 namespace {
 std::mutex g_tile_mu;
 int        g_tile_cnt[64];
 }
 
-static void
+static int
+tile_queue_max( void ) {
+  char const * e = getenv( "GPU_MAX_HW_QUEUES" );
+  int v = e && *e ? atoi( e ) : 0;
+  return v > 0 ? v : 4;   /* HIP's default */
+}
+
+static bool
 tile_count( fd_verify_amd_tile_t * t, bool in ) {
-  int device = t->eng->device;
-  if( device < 0 || device >= 64 || t->counted == in ) return;
+  int device = t->device;
+  if( device < 0 || device >= 64 || t->counted == in ) return true;
   std::lock_guard<std::mutex> g( g_tile_mu );
+  if( in && g_tile_cnt[device] >= tile_queue_max() ) return false;
   g_tile_cnt[device] += in ? 1 : -1;
   t->counted = in;
+  return true;
 }
 
 static uint32_t
 tile_share( fd_verify_amd_tile_t const * t ) {
   if( t->cfg.waves ) return (uint32_t)t->cfg.waves;
   int n = 1;
-  if( t->eng->device >= 0 && t->eng->device < 64 ) {
+  if( t->device >= 0 && t->device < 64 ) {
     std::lock_guard<std::mutex> g( g_tile_mu );
-    n = std::max( 1, g_tile_cnt[t->eng->device] );
+    n = std::max( 1, g_tile_cnt[t->device] );
   }
   return std::max( 2u, (uint32_t)(8 * t->cus) / (uint32_t)n );
 }
@@ -283,10 +397,9 @@ extern "C" int
 fd_verify_amd_tile_set_framing( fd_verify_amd_tile_t * t, int framing ) {
   if( !t || (framing != FD_VERIFY_AMD_FRAMING_PUB_SIG_MSG && framing != FD_VERIFY_AMD_FRAMING_TXN) )
     return FD_ED25519_AMD_ERR_INVAL;
-  /* every transaction must fit an empty batch, else the tile could never stage it */
+  /* every transaction must fit one hand-off */
   if( framing == FD_VERIFY_AMD_FRAMING_TXN && t->batch_max < TXN_SIG_MAX_AT_MTU ) return FD_ED25519_AMD_ERR_INVAL;
   t->framing = framing;
-  tile_count( t, framing == FD_VERIFY_AMD_FRAMING_PUB_SIG_MSG );
   return FD_ED25519_AMD_OK;
 }
 
@@ -327,22 +440,10 @@ tile_kernel_busy( fd_verify_amd_tile_t * t ) {
   return 0;
 }
 
-extern "C" void
-fd_verify_amd_tile_delete( fd_verify_amd_tile_t * t ) {
-  if( !t ) return;
-  tile_count( t, false );
-  (void)hipSetDevice( t->eng->device );
-  if( t->pending && t->hctl ) {   /* an abandoned kernel: ask it to exit, then wait for it */
-    __atomic_store_n( &t->hctl->stop, 1u, __ATOMIC_RELEASE );
-    (void)hipEventSynchronize( t->pdone );
-  }
-  fd_ed25519_amd_delete( t->eng );   /* synchronises every slot stream first */
-  if( t->reg_base ) (void)hipHostUnregister( t->reg_base );
-  for( int k=0; k<FD_AMD_SLOT_MAX; k++ ) {
-    if( t->ts[k].h_meta ) (void)hipHostFree( t->ts[k].h_meta );
-    if( t->ts[k].d_mir  ) (void)hipFree( t->ts[k].d_mir );
-  }
-  if( t->out_base ) (void)hipHostFree( t->out_base );
+/* Free the persistent consumer's resources (all of them, or what a failed
+   allocation got): a later run allocates them afresh. */
+static void
+tile_persist_free( fd_verify_amd_tile_t * t ) {
   if( t->pst )     (void)hipStreamDestroy( t->pst );
   if( t->pdone )   (void)hipEventDestroy( t->pdone );
   if( t->hctl )    (void)hipHostFree( t->hctl );
@@ -351,77 +452,32 @@ fd_verify_amd_tile_delete( fd_verify_amd_tile_t * t ) {
   if( t->res )     (void)hipHostFree( t->res );
   if( t->dctl )    (void)hipFree( t->dctl );
   if( t->scratch ) (void)hipFree( t->scratch );
+  t->pst = NULL; t->pdone = NULL; t->hctl = NULL; t->ring = NULL; t->desc = NULL; t->res = NULL;
+  t->dctl = NULL; t->scratch = NULL;
+  t->persist_ok = false;
+}
+
+extern "C" void
+fd_verify_amd_tile_delete( fd_verify_amd_tile_t * t ) {
+  if( !t ) return;
+  (void)tile_count( t, false );
+  (void)hipSetDevice( t->device );
+  if( t->pending && t->hctl ) {   /* an abandoned kernel: ask it to exit, then wait for it */
+    __atomic_store_n( &t->hctl->stop, 1u, __ATOMIC_RELEASE );
+    (void)hipEventSynchronize( t->pdone );
+  }
+  if( t->pst ) (void)hipStreamSynchronize( t->pst );
+  if( t->reg_base ) (void)hipHostUnregister( t->reg_base );
+  if( t->out_base ) (void)hipHostFree( t->out_base );
+  tile_persist_free( t );
+  free( t->frame_busy );
   delete t;
 }
 
-/* Copy mode's staging copy: whole 16-B words (a frag's chunks are 64-B
-   granular, so the rounded-up tail stays inside its own chunks) with
-   non-temporal stores -- the frame is read next by the GPU over PCIe, not by
-   this CPU, so it skips the read-for-ownership of every destination line and
-   stays out of the cache.  Weakly ordered: the stager fences (sfence) before
-   it publishes the head that hands the frames over. */
-static inline void
-stage_copy_nt( uchar * dst, uchar const * src, ulong sz ) {
-  ulong const n = (sz + 15UL) >> 4;
-  __m128i const * s = (__m128i const *)src;
-  __m128i * d = (__m128i *)dst;
-  ulong k = 0;
-  for( ; k + 4UL <= n; k += 4UL ) {
-    __m128i const a = _mm_loadu_si128( s + k ), b = _mm_loadu_si128( s + k + 1 );
-    __m128i const c = _mm_loadu_si128( s + k + 2 ), e = _mm_loadu_si128( s + k + 3 );
-    _mm_stream_si128( d + k, a ); _mm_stream_si128( d + k + 1, b );
-    _mm_stream_si128( d + k + 2, c ); _mm_stream_si128( d + k + 3, e );
-  }
-  for( ; k < n; k++ ) _mm_stream_si128( d + k, _mm_loadu_si128( s + k ) );
-}
-
-/* Copy mode's deferred staging: a pass first reserves a frame per frag and
-   lists the copies, then copies them -- half on the copy helper thread when
-   the tile has one and the pass is large enough -- and only then re-checks
-   each frag's mcache line and stages it (a frag lapped during its copy
-   leaves its frame unused). */
-struct copy_job_t {
-  uchar *                dst;
-  uchar const *          src;
-  fd_frag_meta_t const * m;
-  ulong                  seq, fr, sz, tag;   /* tag: the HA dedup tag, read from the source */
-  uint                   f, tsorig;
-  ushort                 ctl;
-};
-
-#define COPY_SPLIT_MIN (32UL)   /* passes of fewer frags are copied on the stager alone */
-
-struct copier_t {
-  alignas(64) std::atomic<ulong> gen;    /* stager -> helper: a new job range */
-  alignas(64) std::atomic<ulong> done;   /* helper -> stager: the range of gen `done` is copied */
-  alignas(64) copy_job_t const * jobs;
-  ulong                          lo, hi;
-  std::atomic<int>               quit;
-};
-
-static void
-copy_jobs( copy_job_t const * j, ulong lo, ulong hi ) {
-  for( ulong k=lo; k<hi; k++ ) {
-    if( k + 2UL < hi ) for( ulong o = 0; o < j[k+2].sz; o += 64UL ) __builtin_prefetch( j[k+2].src + o );
-    stage_copy_nt( j[k].dst, j[k].src, j[k].sz );
-  }
-}
-
-/* The persistent window rule: frags handed over and not yet published */
-static ulong
-tile_window( fd_verify_amd_tile_cfg_t const * c ) {
-  if( c->window ) return c->window;
-  /* in flight = rate x latency: ~1.3 ms at up to ~55 M frags/s under load,
-     plus a hand-off's worth of head-of-line wait (a window that binds at 80 %
-     load shows up as input wait in the tail) */
-  if( c->batch_max >= (1UL << 12) ) return 1UL << 18;
-  if( c->batch_max >= (1UL << 10) ) return 1UL << 17;
-  return std::max( 64UL * c->batch_max, 1UL << 15 );   /* latency chunks at ~18 M frags/s x ~1 ms */
-}
-
-/* The persistent consumer's resources (allocated at the first
-   PUB_SIG_MSG run): control words, ring, descriptors and results in mapped
-   coherent host memory, the device control block, per-wave scratch. */
+/* The persistent consumer's resources (allocated at the first run):
+   control words, ring, descriptors and results in mapped coherent host
+   memory, the device control block, per-wave scratch.  A failure frees
+   what was allocated (ERR_DEVICE), so a retry starts clean. */
 static int
 tile_persist_alloc( fd_verify_amd_tile_t * t ) {
   if( t->persist_ok ) return FD_ED25519_AMD_OK;
@@ -431,11 +487,11 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
   uint32_t waves = tile_share( t );
   if( waves < 2u || waves > 65536u ) return FD_ED25519_AMD_ERR_INVAL;
   t->window = W; t->R = R; t->waves = waves;
-  /* latency chunks' capacity: one 8-frag chunk per SIMD at ~0.45 ms, and
+  /* latency chunks' capacity: one 8-slot chunk per SIMD at ~0.45 ms, and
      the window over their ~0.55 ms in flight.  Throughput chunks keep a frag
      in flight 1.3-2.2 ms, so a small window caps them at W / 2 ms: when that
      is below the latency chunks' capacity the tile stays in latency chunks
-     (batch_max 256: 8 M vs 18 M frags/s) */
+     (batch_max 256: 8 M vs 18 M frags/s).  Rates are signature slots/s. */
   double const cap  = std::min( (double)std::min( (ulong)waves - 1UL, 4UL * (ulong)t->cus ) * 8.0 / 450e-6,
                                 (double)W / 550e-6 );
   bool const   thr_ok = (double)W / 2e-3 > cap;
@@ -447,8 +503,8 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
      multiplexes streams onto a few hardware queues per priority
      (GPU_MAX_HW_QUEUES, 4 by default): a normal stream that landed on the
      same queue would wait behind the persistent kernel until the run ends.
-     A high-priority stream comes from the other pool, so engine calls and
-     the tile's own batch streams never queue behind it. */
+     A high-priority stream comes from the other pool, so engine calls never
+     queue behind it (tiles themselves are capped per device: tile_count). */
   int prio_lo = 0, prio_hi = 0;
   if( hipDeviceGetStreamPriorityRange( &prio_lo, &prio_hi ) != hipSuccess ) prio_hi = 0;
   if( hipStreamCreateWithPriority( &t->pst, hipStreamNonBlocking, prio_hi ) != hipSuccess ||
@@ -462,8 +518,11 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
       hipHostMalloc( (void **)&t->res, 3UL * R * sizeof(uint64_t), hf ) != hipSuccess ||
       hipHostGetDevicePointer( &t->res_dev, t->res, 0 ) != hipSuccess ||
       hipMalloc( (void **)&t->dctl, sizeof(fd_amd_tile_dctl_t) ) != hipSuccess ||
-      hipMalloc( (void **)&t->scratch, waves * fd_amd_tile_scratch_stride() ) != hipSuccess )
+      hipMalloc( (void **)&t->scratch, waves * fd_amd_tile_scratch_stride() ) != hipSuccess ) {
+    (void)hipGetLastError();
+    tile_persist_free( t );
     return FD_ED25519_AMD_ERR_DEVICE;
+  }
   memset( t->hctl, 0, sizeof(fd_amd_tile_hctl_t) );
   memset( t->ring, 0, R * sizeof(fd_amd_tile_ent_t) );
   memset( t->desc, 0, R * sizeof(fd_amd_tile_desc_t) );
@@ -473,22 +532,6 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
   t->desc_end.assign( R, 0UL );
   t->ring_seq = 0UL;
   t->persist_ok = true;
-  return FD_ED25519_AMD_OK;
-}
-
-static int
-tile_slots_alloc( fd_verify_amd_tile_t * t ) {
-  if( t->slots_ok ) return FD_ED25519_AMD_OK;
-  for( int k=0; k<t->nslot; k++ ) {
-    tile_slot_t & s = t->ts[k];
-    if( fd_amd_slot_alloc_aux( &t->eng->slot[k], t->batch_max ) ||
-        hipHostMalloc( (void **)&s.h_meta, 4UL*(4UL*t->batch_max + 1UL), hipHostMallocMapped ) != hipSuccess ||
-        hipHostGetDevicePointer( (void **)&s.m_meta, s.h_meta, 0 ) != hipSuccess ||
-        hipMalloc( (void **)&s.d_mir, t->batch_max * FD_VERIFY_AMD_FRAME_SZ + 64UL ) != hipSuccess )
-      return FD_ED25519_AMD_ERR_DEVICE;
-    s.pend.resize( t->batch_max ); s.ich.resize( t->batch_max ); s.fsz.resize( t->batch_max ); s.tb.resize( t->batch_max + 1UL );
-  }
-  t->slots_ok = true;
   return FD_ED25519_AMD_OK;
 }
 
@@ -503,30 +546,29 @@ fd_verify_amd_tile_new_cfg( fd_verify_amd_tile_cfg_t const * cfg ) {
   if( c.publish_cpu < FD_VERIFY_AMD_PUBLISH_AUTO || c.publish_cpu >= CPU_SETSIZE ) return NULL;
   if( c.copy_cpu < FD_VERIFY_AMD_COPY_INLINE || c.copy_cpu >= CPU_SETSIZE ) return NULL;
   if( c.waves == 1UL || c.waves > 65536UL ) return NULL;
-  int cus = 0;
+  int cnt = 0, cus = 0;
+  if( hipGetDeviceCount( &cnt ) != hipSuccess || c.device < 0 || c.device >= cnt ) return NULL;
+  if( hipSetDevice( c.device ) != hipSuccess ) return NULL;
   if( hipDeviceGetAttribute( &cus, hipDeviceAttributeMultiprocessorCount, c.device ) != hipSuccess || cus <= 0 ) return NULL;
   if( !c.lat_free_chunks ) c.lat_free_chunks = (ulong)cus / 2UL;
-  if( !c.out_frame_cnt ) {   /* the frags in flight + the staging group + the consumer's lag */
-    ulong fly = c.framing == FD_VERIFY_AMD_FRAMING_TXN ? (ulong)TILE_NSLOT * c.batch_max : tile_window( &c );
-    c.out_frame_cnt = 4096UL + c.batch_max + fly;
-  }
+  if( !c.out_frame_cnt ) c.out_frame_cnt = 4096UL + c.batch_max + tile_window( &c );   /* in flight + a pass + the consumer's lag */
   if( c.out_frame_cnt > (0xFFFFFFFFUL / FRAME_CHUNKS) ) return NULL;   /* chunk indices are 32-bit */
-  /* the engine's own staging is unused by the tile (frags reach the GPU
-     through the output frames), so it is sized for a single message */
-  fd_ed25519_amd_t * eng = fd_amd_engine_new( c.device, c.batch_max, FD_ED25519_AMD_MSG_MAX, TILE_NSLOT );
-  if( !eng ) return NULL;
   fd_verify_amd_tile_t * t = new fd_verify_amd_tile_t();
-  t->cfg = c; t->eng = eng; t->batch_max = c.batch_max; t->wait_ns = c.batch_wait_ns; t->nslot = TILE_NSLOT;
+  t->cfg = c; t->device = c.device; t->batch_max = c.batch_max;
   t->framing = c.framing; t->cus = cus;
   t->tc.init( c.tcache_depth );
   bool ok = hipHostMalloc( (void **)&t->out_base, c.out_frame_cnt * FD_VERIFY_AMD_FRAME_SZ, hipHostMallocMapped ) == hipSuccess &&
             hipHostGetDevicePointer( (void **)&t->out_dev, t->out_base, 0 ) == hipSuccess;
   t->frame_cnt = c.out_frame_cnt;
   t->frame_pub.assign( c.out_frame_cnt, FRAME_FREE );
+  t->frame_busy = (uint8_t *)calloc( c.out_frame_cnt, 1 );
   t->out_seq_end = ~0UL;
-  if( ok && t->framing == FD_VERIFY_AMD_FRAMING_TXN ) ok = !tile_slots_alloc( t );
-  if( !ok ) { fd_verify_amd_tile_delete( t ); return NULL; }
-  tile_count( t, t->framing == FD_VERIFY_AMD_FRAMING_PUB_SIG_MSG );
+  if( !ok || !t->frame_busy || !tile_count( t, true ) ) {
+    if( ok && t->frame_busy ) fprintf( stderr, "fd_verify_amd_tile_new: device %d already runs %d tiles in this process "
+                                       "(one hardware queue each, GPU_MAX_HW_QUEUES)\n", c.device, tile_queue_max() );
+    fd_verify_amd_tile_delete( t );
+    return NULL;
+  }
   return t;
 }
 
@@ -540,253 +582,15 @@ fd_verify_amd_tile_new( int device, ulong batch_max, ulong batch_wait_ns, ulong 
 }
 
 /* ------------------------------------------------------------------ */
-/* TXN framing: the multi-stream batch path                             */
+/* the run: stager (the caller's thread), publisher, persistent kernel  */
 
-/* Launch the staged batch of tile slot k (n transactions, nsig signature
-   slots).  src: the mapped region the GPU copies the frags from (input
-   dcache in zero-copy mode, the output dcache in copy mode); out: the
-   mapped output dcache when the GPU must fill the output frames. */
-static int
-tile_launch( fd_verify_amd_tile_t * t, int k, ulong n, uint8_t const * src, uint8_t * out ) {
-  slot_t *      s  = &t->eng->slot[k];
-  tile_slot_t & ts = t->ts[k];
-  uint32_t * hm = ts.h_meta;
-  memcpy( hm, ts.ich.data(), 4UL*n );
-  for( ulong i=0; i<n; i++ ) hm[n + i] = ts.pend[i].fidx * FRAME_CHUNKS;
-  memcpy( hm + 2UL*n, ts.fsz.data(), 4UL*n );
-  uint32_t const * m_tbase = ts.m_meta + 3UL*n;
-  memcpy( hm + 3UL*n, ts.tb.data(), 4UL*(n + 1UL) );
-  if( fd_amd_launch_tile_gather( (uint32_t)n, ts.m_meta, src, out, ts.d_mir, (uint32_t)FD_VERIFY_AMD_FRAME_SZ, 1,
-                                 s->d_pub, s->d_sig, s->d_toff, s->d_tsz, s->stream ) )
-    return FD_ED25519_AMD_ERR_DEVICE;
-  /* up to 12 signatures per frag: the size rule of the batch engine
-     (profiles/r01_tile_policy_ab.txt, r02_tile_dsm8_ab.txt) */
-  int mode = fd_amd_batch_dsm_mode( (uint32_t)ts.nsig, 0xFFFFFFFFu );
-  ulong nsig = ts.nsig;
-  if( fd_amd_launch_txn_parse( (uint32_t)n, ts.d_mir, s->d_toff, s->d_tsz, s->d_fp, NULL, 0, m_tbase,
-                               s->d_pub, s->d_sig, s->d_off, s->d_sz, s->d_skip, s->stream ) )
-    return FD_ED25519_AMD_ERR_DEVICE;
-  if( nsig && fd_amd_launch_verify( (uint32_t)nsig, s->d_pub, s->d_sig, s->d_off, s->d_sz, ts.d_mir, s->d_err,
-                                    s->d_ws, s->stream, 0, NULL, s->d_skip, mode ) )
-    return FD_ED25519_AMD_ERR_DEVICE;
-  if( fd_amd_launch_txn_reduce( (uint32_t)n, s->d_fp, m_tbase, s->d_err, s->d_terr, s->stream ) )
-    return FD_ED25519_AMD_ERR_DEVICE;
-  if( fd_amd_slot_out( s, s->h_terr, s->d_terr, n ) ) return FD_ED25519_AMD_ERR_DEVICE;
-  if( nsig ) {
-    ws_layout_t L = fd_amd_ws_layout( nsig );
-    if( fd_amd_slot_out( s, s->h_tag, (uint8_t *)s->d_ws + L.tag, 8UL*nsig ) ) return FD_ED25519_AMD_ERR_DEVICE;
-  }
-  if( hipEventRecord( s->done, s->stream ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
-  s->out = s->t_out = s->s_out = NULL;
-  s->n = n; s->t_n = n; s->busy = 1;
-  s->chk_err = 0; s->chk_terr = n;
-  return FD_ED25519_AMD_OK;
-}
-
-/* Error exit of the batch path: wait for every batch still in flight (a
-   queued k_tile_gather reads its slot's mapped metadata in place, which the
-   next run rewrites) and forget them. */
-static int
-tile_quiesce( fd_verify_amd_tile_t * t, int rc ) {
-  for( int k=0; k<t->nslot; k++ ) {
-    slot_t * s = &t->eng->slot[k];
-    if( s->busy ) (void)hipEventSynchronize( s->done );
-    s->out = s->t_out = s->s_out = NULL;
-    s->busy = 0;
-  }
-  return rc;
-}
-
-static int
-tile_run_batched( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ulong in_depth, void const * in_chunk0,
-                  ulong in_seq0, ulong * in_fseq, fd_frag_meta_t * out_mcache, ulong out_depth, ulong out_seq0,
-                  ulong const * out_fseq, ulong frag_cnt, int const * stop, fd_verify_amd_diag_t * diag, uint * lat,
-                  ulong lat_max, uint8_t const * zc_dev, ulong zc_lim ) {
-  fd_ed25519_amd_t * e = t->eng;
-  ulong const F = t->frame_cnt;
-  ulong in_seq = in_seq0, out_seq = out_seq0, lat_n = 0;
-  int   K = t->nslot;
-  int   stage = 0;                 /* slot being filled; slots are used round robin, so the */
-  int   oldest = 0, nfly = 0;      /* in-flight ones are oldest, oldest+1, ... (mod K)      */
-  ulong staged = 0, slots = 0, stage_t0 = 0, t_halt = 0;
-  int   rc = FD_ED25519_AMD_OK;
-  bool  halted = false;
-  /* Flow-control state shared with other threads is exchanged in strides,
-     not per frag (the reference's tiles publish fseq and refresh credits
-     in housekeeping, fd_fctl): diag->in_cnt and in_fseq are published per
-     staging pass; out_fseq is re-read only when a cached value runs out. */
-  ulong in_cnt = diag->in_cnt, out_cr = 0, cons = out_seq0, fseq_pub = ~0UL;
-
-  auto stopped = [&]() -> bool { return stop && __atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0; };
-
-  /* publish the retired batch of slot k; false when the halt grace ran out
-     while the output was backpressured */
-  auto publish = [&]( int k ) -> bool {
-    slot_t *      s  = &e->slot[k];
-    tile_slot_t & ts = t->ts[k];
-    ulong cnt = s->n;
-    for( ulong i=0; i<cnt; i++ ) {
-      pending_t const & m = ts.pend[i];
-      /* zero copy: the GPU read the frag some time before now; if its mcache
-         line has been lapped since, the producer may have rewritten it */
-      if( zc_dev && __atomic_load_n( &in_mcache[ m.seq & (in_depth-1UL) ].seq, __ATOMIC_ACQUIRE ) != m.seq ) {
-        diag->ovrn_cnt++;
-        continue;
-      }
-      if( s->h_terr[i] ) { diag->sv_filt_cnt++; diag->sv_filt_sz += m.sz; continue; }
-      /* dedup tag: the verify's SHA-512 tag of the first signature */
-      ulong tag = s->h_tag[ ts.tb[i] ];
-      if( out_fseq && (long)(out_seq - out_cr) >= 0 ) {   /* credit check against the slowest consumer */
-        out_cr = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) + out_depth;
-        if( (long)(out_seq - out_cr) >= 0 ) {
-          diag->backp_cnt++;
-          for( ;; ) {   /* backpressured: keep the halt check running (fd_frank_verify_synth_load.c:223-274) */
-            out_cr = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE ) + out_depth;
-            if( (long)(out_seq - out_cr) < 0 ) break;
-            if( stopped() ) {
-              ulong tn = now_ns();
-              if( !t_halt ) t_halt = tn;
-              if( tn - t_halt > t->cfg.halt_grace_ns ) { diag->halt_drop_cnt += cnt - i; return false; }
-            }
-          }
-        }
-      }
-      ulong f = m.fidx;
-      t->frame_pub[f] = out_seq;
-      uint tspub = fd_verify_amd_tickcount();
-      fd_mcache_publish( out_mcache, out_depth, out_seq, tag, f * FRAME_CHUNKS, m.sz, m.ctl, m.tsorig, tspub );
-      if( lat && lat_n < lat_max ) lat[lat_n++] = tspub - m.tsorig;
-      out_seq++; diag->out_cnt++; diag->out_sz += m.sz;
-    }
-    t->frame_retired = ts.frame_hi;
-    return true;
-  };
-
-  for( ;; ) {
-    /* 1. retire the oldest batch if it is done (publication stays in
-          arrival order: batches retire in launch order) */
-    while( nfly ) {
-      int r = fd_amd_slot_ready( &e->slot[oldest] );
-      if( r < 0 ) { rc = r; break; }
-      if( !r ) break;
-      if( (rc = fd_amd_slot_drain( &e->slot[oldest] )) ) break;
-      if( !publish( oldest ) ) { halted = true; break; }
-      oldest = (oldest + 1) % K; nfly--;
-    }
-    if( rc || halted ) break;
-    /* producer credit: copy mode is done with a frag once it is copied;
-       zero copy only once the batch holding it has retired */
-    if( in_fseq ) {
-      ulong rel = !zc_dev ? in_seq : nfly ? t->ts[oldest].seq_lo : staged ? t->ts[stage].seq_lo : in_seq;
-      if( rel != fseq_pub ) { __atomic_store_n( in_fseq, rel, __ATOMIC_RELEASE ); fseq_pub = rel; }
-    }
-    bool done_in = (frag_cnt && in_seq - in_seq0 >= frag_cnt) || stopped();
-    if( done_in && !staged && !nfly ) break;
-    if( nfly == K ) continue;   /* every slot in flight: the staging slot is busy */
-
-    /* 2. stage input frags into the free slot */
-    tile_slot_t & ts = t->ts[stage];
-    bool idle_in = false, full = false;
-    while( !done_in && staged < t->batch_max ) {
-      if( frag_cnt && in_seq - in_seq0 >= frag_cnt ) break;
-      fd_frag_meta_t const * m = in_mcache + (in_seq & (in_depth-1UL));
-      ulong seq_found = __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE );
-      long  d = (long)(seq_found - in_seq);
-      if( d < 0 ) { idle_in = true; break; }                             /* not yet published */
-      if( d > 0 ) { diag->ovrn_cnt += (ulong)d; in_seq = seq_found; continue; }   /* overrun: resync */
-      ulong chunk = m->chunk, sz = m->sz, ctl = m->ctl, tsorig = m->tsorig;
-      __atomic_thread_fence( __ATOMIC_ACQUIRE );
-      if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != in_seq ) { diag->ovrn_cnt++; in_seq++; continue; }
-      if( !sz || sz > FD_ED25519_AMD_MSG_MAX ||
-          (zc_dev && (chunk << FD_CHUNK_LG_SZ) + ((sz + 63UL) & ~63UL) > zc_lim) ) {
-        diag->bad_frag_cnt++; in_seq++; in_cnt++; continue;
-      }
-      /* reserve the next output frame: not staged or in flight, and no
-         longer read by a consumer that honours flow control */
-      ulong fr = t->frame_next, f = t->frame_next_idx;
-      if( fr - t->frame_retired >= F ) { full = true; break; }
-      if( out_fseq && t->frame_pub[f] != FRAME_FREE && (long)(t->frame_pub[f] - cons) >= 0 ) {
-        cons = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE );
-        if( (long)(t->frame_pub[f] - cons) >= 0 ) { diag->backp_cnt++; full = true; break; }
-      }
-      uchar const * p = (uchar const *)fd_chunk_to_laddr_const( in_chunk0, chunk );
-      if( !zc_dev ) {
-        /* copy mode: the frame is the tile's copy; a frag lapped while it
-           was copied is dropped (speculative read, then seq re-check) */
-        uint8_t * dst = t->out_base + f * FD_VERIFY_AMD_FRAME_SZ;
-        stage_copy_nt( dst, p, sz );
-        __atomic_thread_fence( __ATOMIC_ACQUIRE );
-        if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != in_seq ) { diag->ovrn_cnt++; in_seq++; continue; }
-        p = dst;
-      }
-      /* wire transaction (fd_txn.h layout): dedup on its first signature */
-      ulong k2 = fd_amd_txn_slots1( p, sz );
-      if( slots + k2 > t->batch_max ) { full = true; break; }        /* no room for its signatures: next batch */
-      in_seq++; in_cnt++;
-      ulong ha_tag = 0;
-      if( k2 ) memcpy( &ha_tag, p + 1, 8 );
-      if( k2 && t->tc.insert( ha_tag ) ) { diag->ha_filt_cnt++; diag->ha_filt_sz += sz; continue; }
-      t->frame_pub[f] = FRAME_FREE;
-      t->frame_next++;
-      if( ++t->frame_next_idx == F ) t->frame_next_idx = 0UL;
-      ts.ich[staged] = zc_dev ? (uint32_t)chunk : (uint32_t)(f * FRAME_CHUNKS);
-      ts.fsz[staged] = (uint32_t)sz;
-      ts.tb[staged]  = (uint32_t)slots;
-      slots += k2;
-      ts.pend[staged] = pending_t{ in_seq - 1UL, fr, (ushort)sz, (ushort)ctl, (uint)tsorig, (uint)f, 0u, 0u, 0u };
-      if( !staged ) { stage_t0 = now_ns(); ts.seq_lo = in_seq - 1UL; }
-      staged++;
-    }
-    __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
-    if( in_fseq && !zc_dev && in_seq != fseq_pub ) { __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE ); fseq_pub = in_seq; }
-    done_in = (frag_cnt && in_seq - in_seq0 >= frag_cnt) || stopped();
-
-    /* 3. adaptive launch (a free slot exists here): full batch, input
-          momentarily drained (greedy: under light load batches stay small
-          and latency low; under load every slot is busy and batches grow
-          toward batch_max), end of input, no frame or signature room left,
-          or the oldest staged frag waited batch_wait_ns.  A nonzero
-          batch_wait_ns turns the greedy rule off while another batch is in
-          flight. */
-    bool greedy = idle_in && (!t->wait_ns || !nfly);
-    if( staged && ( staged == t->batch_max || full || greedy || done_in ||
-                    (t->wait_ns && now_ns() - stage_t0 >= t->wait_ns) ) ) {
-      ts.tb[staged] = (uint32_t)slots;
-      ts.nsig = slots;
-      ts.frame_hi = t->frame_next;
-      uint8_t const * src = zc_dev ? zc_dev : t->out_dev;
-      if( (rc = tile_launch( t, stage, staged, src, zc_dev ? t->out_dev : NULL )) ) break;
-      diag->batch_sig_cnt += slots;
-      diag->batch_cnt++;
-      nfly++;
-      stage = (stage + 1) % K; staged = 0; slots = 0;
-    }
-  }
-  if( rc || halted ) {
-    /* batches still in flight and staged frags are dropped: the next run
-       starts clean (its own slots, frames of unpublished frags are free).
-       A halt inside publish() counted the rest of the oldest batch. */
-    if( halted ) {
-      for( int q = 1; q < nfly; q++ ) diag->halt_drop_cnt += e->slot[(oldest + q) % K].n;
-      diag->halt_drop_cnt += staged;
-    }
-    (void)tile_quiesce( t, rc );
-  }
-  __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
-  if( in_fseq ) __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE );
-  t->out_seq_end = out_seq;
-  return rc;
-}
-
-/* ------------------------------------------------------------------ */
-/* PUB_SIG_MSG framing: the persistent consumer                         */
-
-/* The hand-off rule (header).  Pure; the CPU tests call it. */
+/* The hand-off rule (header).  Pure; the CPU tests call it.  Units:
+   signature slots (PUB_SIG_MSG: frags). */
 extern "C" ulong
 fd_verify_amd_tile_cut( fd_verify_amd_tile_cfg_t const * c, ulong staged, ulong handed, ulong chunks_in_flight,
                         int thr, ulong waited_ns, int flush ) {
   if( staged == handed ) return handed;
-  ulong const n = staged - handed, K = thr ? 64UL : 8UL;
+  ulong const n = staged - handed, K = thr ? CHUNK_SLOTS : LAT_SLOTS;
   if( flush || n >= c->batch_max || (c->batch_wait_ns && waited_ns >= c->batch_wait_ns) ) return staged;
   bool const rest = thr ? waited_ns >= c->chunk_wait_ns
                         : ( waited_ns >= c->lat_fill_ns || chunks_in_flight < c->lat_free_chunks );
@@ -800,11 +604,32 @@ fd_verify_amd_tile_mode( int chunk_mode, int thr, double rate, double rate_hi, d
   return thr ? rate >= rate_lo : rate > rate_hi;
 }
 
+/* Chunk packing (pure; the CPU tests call it): from ring entries with
+   slots[0..cnt) signature slots each, the next chunk starting at entry 0:
+   returns its entry count and sets *nsl to its slots.  Up to 64 entries
+   and K slots (64, or 8 for a latency chunk); an entry is never split, so
+   an entry of more than K slots (a transaction of > 8 signatures in latency
+   mode) makes a chunk of its own -- the caller verifies that one 1 lane per
+   signature (slots > 8). */
+extern "C" ulong
+fd_verify_amd_tile_pack( uint const * slots, ulong cnt, int thr, ulong * nsl ) {
+  ulong const K = thr ? CHUNK_SLOTS : LAT_SLOTS;
+  ulong n = 0UL, s = 0UL;
+  while( n < cnt && n < 64UL ) {
+    ulong const k = slots[n];
+    if( n && s + k > K ) break;
+    s += k; n++;
+    if( s >= K ) break;
+  }
+  *nsl = s;
+  return n;
+}
+
 namespace {
 
-/* One persistent run, shared by the stager (the caller's thread) and the
-   publisher (a second thread, or the stager itself between passes).  Each
-   atomic on its own line: the two threads exchange ring positions only. */
+/* One run, shared by the stager (the caller's thread) and the publisher (a
+   second thread, or the stager itself between passes).  Each atomic on its
+   own line: the two threads exchange ring positions only. */
 struct prun_t {
   fd_verify_amd_tile_t * t;
   fd_frag_meta_t const * in_mcache; ulong in_depth, in_seq0;
@@ -816,17 +641,18 @@ struct prun_t {
   ulong                  mask, R;
   fd_amd_tile_hctl_t *   H;
   /* publisher-owned */
-  ulong pubd, retired, out_seq, lat_n, out_cr, t_halt;
+  ulong pubd, out_seq, lat_n, out_cr, t_halt;
   long  g_off;                   /* host ns - GPU ticks x 10 (the best sample of the current window) */
   long  g_off_cur; ulong g_win;  /* the window being sampled, and its start */
   ulong g_last;                  /* latest full GPU clock sample */
   bool  g_ok;
-  fd_verify_amd_diag_t d;        /* publisher's counters (out, sv_filt, ovrn, backp, halt_drop) */
+  fd_verify_amd_diag_t d;        /* publisher's counters (out, sv_filt, ovrn, backp) */
   alignas(64) std::atomic<ulong> handed;    /* stager -> publisher: ring indices [.., handed) were handed over */
   alignas(64) std::atomic<ulong> pubd_a;    /* publisher -> stager: [.., pubd) are published or dropped */
-  alignas(64) std::atomic<ulong> retired_a; /* publisher -> stager: frame reservations [.., retired) are free */
   alignas(64) std::atomic<ulong> end;       /* stager -> publisher: the final ring index (~0 while staging) */
-  alignas(64) std::atomic<int>   quit;      /* stager -> publisher: stop now (error, or the halt grace ran out) */
+  alignas(64) std::atomic<int>   quit;      /* stager -> publisher: stop now (error, or halted) */
+  alignas(64) std::atomic<int>   halt;      /* publisher -> stager: *stop was raised and the output stayed
+                                               backpressured for halt_grace_ns: give up the rest */
 };
 
 inline void beat( fd_amd_tile_hctl_t * H ) { __atomic_fetch_add( &H->beat, 1UL, __ATOMIC_RELAXED ); }
@@ -856,9 +682,10 @@ gclock_ns( prun_t const & r, uint ticks32 ) {   /* low 32 bits of a recent GPU c
    in, then (zero copy) check once that the oldest of them was not lapped --
    lapping goes in sequence order, so if its mcache line is intact now,
    after the GPU read every frag of the pass, so are the newer ones' --
-   then publish them with one timestamp.  Returns whether anything moved;
-   returns early (leaving the rest) when quit is raised or the halt grace
-   ran out while backpressured. */
+   then publish them with one timestamp.  Every published or dropped frag
+   frees its output frame.  Returns whether anything moved; returns early
+   (leaving the rest) when quit is raised or, after *stop, the output stayed
+   backpressured for halt_grace_ns (then raises r.halt). */
 bool
 publish_pass( prun_t & r ) {
   fd_verify_amd_tile_t * t = r.t;
@@ -888,7 +715,8 @@ publish_pass( prun_t & r ) {
        line has been lapped since, the producer may have rewritten it */
     if( !lap_ok && __atomic_load_n( &r.in_mcache[ m.seq & (r.in_depth-1UL) ].seq, __ATOMIC_ACQUIRE ) != m.seq ) {
       r.d.ovrn_cnt++;
-      r.pubd++; r.retired = m.frame + 1UL;
+      __atomic_store_n( &t->frame_busy[m.fidx], (uint8_t)0, __ATOMIC_RELEASE );
+      r.pubd++;
       continue;
     }
     schar const v = (schar)(uchar)(w & 0xffUL);
@@ -896,8 +724,9 @@ publish_pass( prun_t & r ) {
     if( t->vlog && rs < t->vlog_max ) t->vlog[rs] = v;
     if( v ) {
       r.d.sv_filt_cnt++; r.d.sv_filt_sz += m.sz;
-      if( v >= -3 ) r.d.sv_filt_code_cnt[-v - 1]++;
-      r.pubd++; r.retired = m.frame + 1UL;
+      if( v >= -3 && v <= -1 ) r.d.sv_filt_code_cnt[-v - 1]++;   /* TXN parse failures (-4) count SV_FILT only */
+      __atomic_store_n( &t->frame_busy[m.fidx], (uint8_t)0, __ATOMIC_RELEASE );
+      r.pubd++;
       continue;
     }
     if( r.out_fseq && (long)(r.out_seq - r.out_cr) >= 0 ) {   /* credit check against the slowest consumer */
@@ -908,7 +737,6 @@ publish_pass( prun_t & r ) {
            the reference tile keeps its housekeeping (fd_frank_verify_synth_load.c:
            223-274); let the stager see what was published so far */
         r.pubd_a.store( r.pubd, std::memory_order_release );
-        r.retired_a.store( r.retired, std::memory_order_release );
         ulong spin = 0;
         for( ;; ) {
           r.out_cr = __atomic_load_n( r.out_fseq, __ATOMIC_ACQUIRE ) + r.out_depth;
@@ -917,19 +745,23 @@ publish_pass( prun_t & r ) {
             beat( r.H );
             if( r.quit.load( std::memory_order_acquire ) ) { ok = false; break; }
             if( r.stop && __atomic_load_n( r.stop, __ATOMIC_ACQUIRE ) ) {
+              /* the halt grace runs only while backpressured (it restarts
+                 with every new backpressure episode) */
               ulong const t2 = now_ns();
               if( !r.t_halt ) r.t_halt = t2;
-              if( t2 - r.t_halt > t->cfg.halt_grace_ns ) { ok = false; break; }
+              if( t2 - r.t_halt > t->cfg.halt_grace_ns ) { r.halt.store( 1, std::memory_order_release ); ok = false; break; }
             }
           }
           _mm_pause();
         }
+        r.t_halt = 0UL;
         if( !ok ) break;
       }
     }
     ulong const f = m.fidx;
     t->frame_pub[f] = r.out_seq;
     fd_mcache_publish( r.out_mcache, r.out_depth, r.out_seq, t->res[j], f * FRAME_CHUNKS, m.sz, m.ctl, m.tsorig, tspub );
+    __atomic_store_n( &t->frame_busy[f], (uint8_t)0, __ATOMIC_RELEASE );
     if( r.lat_n < r.lat_max ) {
       if( r.lat ) r.lat[r.lat_n] = tspub - m.tsorig;
       if( t->trace && r.lat_n < t->trace_max ) {
@@ -946,10 +778,9 @@ publish_pass( prun_t & r ) {
       r.lat_n++;
     }
     r.out_seq++; r.d.out_cnt++; r.d.out_sz += m.sz;
-    r.pubd++; r.retired = m.frame + 1UL;
+    r.pubd++;
   }
   r.pubd_a.store( r.pubd, std::memory_order_release );
-  r.retired_a.store( r.retired, std::memory_order_release );
   return true;
 }
 
@@ -966,6 +797,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     fprintf( stderr, "fd_verify_amd_tile_run: the kernel of an earlier run of this tile has not finished\n" );
     return FD_ED25519_AMD_ERR_DEVICE;
   }
+  bool const txn = t->framing == FD_VERIFY_AMD_FRAMING_TXN;
   ulong const F = t->frame_cnt, mask = t->R - 1UL, W = t->window, base = t->ring_seq;
   fd_amd_tile_hctl_t * H = t->hctl;
 
@@ -998,6 +830,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   A.dctl = t->dctl;
   A.scratch = t->scratch;
   A.watchdog = 500000000UL;   /* 5 s of s_memrealtime (100 MHz) without a heartbeat */
+  A.txn = txn ? 1u : 0u;
 #ifdef FD_AMD_DIAG
   { char const * e = getenv( "FD_AMD_TILE_PROF" ); A.prof = e && *e && *e != '0'; }   /* diagnostics build only */
 #endif
@@ -1016,10 +849,10 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   r.zc = zc_dev != NULL; r.lat = lat; r.lat_max = (lat || t->trace) ? std::max( lat ? lat_max : 0UL, t->trace_max ) : 0UL;
   if( lat && t->trace ) r.lat_max = std::min( lat_max, t->trace_max );
   r.mask = mask; r.R = t->R; r.H = H;
-  r.pubd = base; r.retired = 0UL; r.out_seq = out_seq0; r.lat_n = 0UL; r.out_cr = 0UL; r.t_halt = 0UL;
+  r.pubd = base; r.out_seq = out_seq0; r.lat_n = 0UL; r.out_cr = 0UL; r.t_halt = 0UL;
   r.g_off = r.g_off_cur = 0L; r.g_win = 0UL; r.g_last = 0UL; r.g_ok = false;
   memset( &r.d, 0, sizeof r.d );
-  r.handed.store( base ); r.pubd_a.store( base ); r.retired_a.store( 0UL ); r.end.store( ~0UL ); r.quit.store( 0 );
+  r.handed.store( base ); r.pubd_a.store( base ); r.end.store( ~0UL ); r.quit.store( 0 ); r.halt.store( 0 );
 
   /* the publisher: a thread of its own when the tile has a CPU for it */
   std::thread pub;
@@ -1039,7 +872,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
           (void)pthread_setaffinity_np( pthread_self(), sizeof cs, &cs );
           for( ;; ) {
             bool any = publish_pass( r );
-            if( r.quit.load( std::memory_order_acquire ) ) break;
+            if( r.quit.load( std::memory_order_acquire ) || r.halt.load( std::memory_order_acquire ) ) break;
             if( r.pubd == r.end.load( std::memory_order_acquire ) ) break;
             if( !any ) _mm_pause();
           }
@@ -1050,50 +883,64 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   bool const inline_pub = !pub.joinable();
 
   /* copy mode's helper: a thread of its own when cfg.copy_cpu names a CPU */
-  copier_t cpy;
-  cpy.gen.store( 0UL ); cpy.done.store( 0UL ); cpy.quit.store( 0 ); cpy.jobs = NULL; cpy.lo = cpy.hi = 0UL;
+  copier_t * cp = NULL;
   std::thread cth;
   if( !zc_dev && t->cfg.copy_cpu >= 0 ) {
-    int const cpu = t->cfg.copy_cpu;
-    try {
-      cth = std::thread( [&cpy, cpu]() {
-        cpu_set_t one; CPU_ZERO( &one ); CPU_SET( cpu, &one );
-        (void)pthread_setaffinity_np( pthread_self(), sizeof one, &one );
-        ulong seen = 0UL;
-        for( ;; ) {
-          ulong const g = cpy.gen.load( std::memory_order_acquire );
-          if( g != seen ) {
-            seen = g;
-            copy_jobs( cpy.jobs, cpy.lo, cpy.hi );
-            _mm_sfence();   /* the copies before the stager sees them done */
-            cpy.done.store( g, std::memory_order_release );
-            continue;
-          }
-          if( cpy.quit.load( std::memory_order_acquire ) ) break;
-          _mm_pause();
-        }
-      } );
-    } catch( ... ) {}
+    cp = new (std::nothrow) copier_t();
+    if( cp ) {
+      cp->claim.store( 0UL ); cp->quit.store( 0 );
+      for( ulong s=0; s<CP_NJ; s++ ) { cp->nj[s].store( 0UL ); for( ulong b=0; b<CP_NB; b++ ) cp->done[s][b].store( 0UL ); }
+      try { cth = std::thread( copier_loop, cp, t->cfg.copy_cpu ); } catch( ... ) { delete cp; cp = NULL; }
+    }
   }
-  copier_t * const cp = cth.joinable() ? &cpy : NULL;
-  ulong cgen = 0UL;
-  std::vector<copy_job_t> jobs( zc_dev ? 0UL : STAGE_PASS );
+  ulong cgen = 0UL;                       /* the helper's last posted generation */
+  std::vector<orphan_t> orphans;
+  ulong orphan_cnt[CP_NJ] = { 0, 0, 0, 0 };
+  std::vector<copy_job_t> ljobs( zc_dev ? 0UL : STAGE_PASS );   /* a pass copied without the helper */
 
   ulong in_seq = in_seq0, staged = base, handed = base;
+  ulong staged_sl = 0UL, handed_sl = 0UL;   /* signature slots staged / handed over in this run */
   ulong in_cnt = diag->in_cnt, cons = out_seq0, fseq_pub = ~0UL;
   ulong ovrn = 0, bad = 0, ha = 0, ha_sz = 0, backp = 0, nbatch = 0, nsig = 0, switches = 0;
   ulong cdone = dbase;                   /* first descriptor not known to be finished */
-  ulong n_pass = 0, n_hand = 0, n_stop_window = 0, n_stop_frames = 0, n_stop_bmax = 0, n_stop_pass = 0;
+  ulong n_pass = 0, n_hand = 0, n_stop_window = 0, n_stop_frames = 0, n_stop_bmax = 0, n_stop_pass = 0, n_steal = 0;
   t->started = 0;
-  ulong iter = 0UL, pass_t = now_ns(), pass_max = 0UL, t_halt = 0UL;
+  ulong iter = 0UL, pass_t = now_ns(), pass_max = 0UL;
   ulong t_chk = pass_t, g_seen = 0UL, t_prog = pass_t, gc_first = 0UL, gc_last = 0UL, gc_host = 0UL;
-  ulong r_t0 = pass_t, r_n0 = staged;
+  ulong r_t0 = pass_t, r_n0 = 0UL;
   bool  r_blk = false;                   /* staging stopped on the window / frames / credit this interval */
   double rate = 0.0;
   int thr = fd_verify_amd_tile_mode( t->cfg.chunk_mode, 0, 0.0, t->rate_hi, t->rate_lo );
   bool halted = false;
   uchar const * in_chunk0b = (uchar const *)in_chunk0;
   fd_verify_amd_tile_cfg_t cc = t->cfg;   /* the cut rule's parameters */
+  std::vector<uint> pk_slots( 64 );
+
+  /* reserve the next output frame (cyclic): free -- not staged, in flight
+     or orphaned -- and no longer read by a consumer that honours flow
+     control.  false (and why) when there is none. */
+  auto reserve = [&]( uint * fo, bool * credit ) -> bool {
+    ulong const f = t->frame_next_idx;
+    *credit = false;
+    if( __atomic_load_n( &t->frame_busy[f], __ATOMIC_ACQUIRE ) ) return false;
+    if( out_fseq && t->frame_pub[f] != FRAME_FREE && (long)(t->frame_pub[f] - cons) >= 0 ) {
+      cons = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE );
+      if( (long)(t->frame_pub[f] - cons) >= 0 ) { *credit = true; return false; }
+    }
+    t->frame_busy[f] = 1u;
+    t->frame_pub[f] = FRAME_FREE;
+    if( ++t->frame_next_idx == F ) t->frame_next_idx = 0UL;
+    *fo = (uint)f;
+    return true;
+  };
+  auto unreserve = [&]( uint f ) { __atomic_store_n( &t->frame_busy[f], (uint8_t)0, __ATOMIC_RELEASE ); };
+  /* copy mode's producer credit: everything copied -- but never past a frag
+     whose source an orphaned helper block may still be reading */
+  auto copy_rel = [&]() -> ulong {
+    ulong rel = in_seq;
+    for( orphan_t const & o : orphans ) rel = std::min( rel, cp->jobs[o.s][o.b * CP_BLK].seq );
+    return rel;
+  };
 
   for( ;; ) {
     /* the kernel's watchdog needs a heartbeat now and then, not every
@@ -1107,31 +954,42 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     /* 1. publish (inline), then the publisher's progress */
     if( inline_pub ) (void)publish_pass( r );
     ulong const pubd = r.pubd_a.load( std::memory_order_acquire );
-    ulong const retired = r.retired_a.load( std::memory_order_acquire );
+    /* orphaned copy blocks the helper has finished since: their frames are free */
+    for( ulong k = 0; k < orphans.size(); ) {
+      orphan_t & o = orphans[k];
+      if( cp->done[o.s][o.b].load( std::memory_order_acquire ) == o.g ) {
+        for( uint f : o.frames ) unreserve( f );
+        orphan_cnt[o.s]--;
+        orphans[k] = std::move( orphans.back() ); orphans.pop_back();
+      } else k++;
+    }
     /* producer credit: copy mode is done with a frag once it is copied,
        zero copy once it is published (or dropped) */
     if( in_fseq ) {
-      ulong rel = ( !zc_dev || pubd == staged ) ? in_seq : t->ppend[pubd & mask].seq;
+      ulong rel = !zc_dev ? copy_rel() : pubd == staged ? in_seq : t->ppend[pubd & mask].seq;
       if( rel != fseq_pub ) { __atomic_store_n( in_fseq, rel, __ATOMIC_RELEASE ); fseq_pub = rel; }
     }
+    /* after *stop: drain what was taken in; give up only if the publisher
+       reports the output backpressured past the halt grace */
     bool const stopping = stop && __atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0;
-    /* (inline: the publish pass may have seen the stop first, while it
-       spun backpressured) */
-    if( stopping && !t_halt ) t_halt = inline_pub && r.t_halt ? r.t_halt : tn;
     bool done_in = (frag_cnt && in_seq - in_seq0 >= frag_cnt) || stopping;
     if( done_in && pubd == staged ) break;
-    if( t_halt && tn - t_halt > t->cfg.halt_grace_ns ) { halted = true; break; }
+    if( r.halt.load( std::memory_order_acquire ) ) { halted = true; break; }
 
     /* 2. stage (at most STAGE_PASS frags, so hand-offs keep flowing).  Copy
           mode lists the pass's copies first (a frame reserved per frag),
-          copies them -- half on the copy helper when there is one -- and
-          then re-checks and stages each frag in input order */
+          copies them -- with the helper when there is one -- and then
+          re-checks and stages each frag in input order */
     bool full = false;
     ulong const stage_end = staged + STAGE_PASS;
     n_pass++;
     uint const ts32 = (uint)tn;
     ulong nj = 0UL;
-    while( !done_in && staged + nj - handed < t->batch_max && staged + nj != stage_end ) {
+    /* the helper's next job array, when it is free of orphans */
+    ulong const gnext = cgen + 1UL, snext = gnext % CP_NJ;
+    copy_job_t * jobs = ( cp && !orphan_cnt[snext] ) ? cp->jobs[snext] : ljobs.data();
+    ulong sl_pass = 0UL;                   /* slots listed in this pass (copy mode) */
+    while( !done_in && staged_sl + sl_pass - handed_sl < t->batch_max && staged + nj != stage_end ) {
       if( frag_cnt && in_seq - in_seq0 >= frag_cnt ) break;
       if( staged + nj - pubd >= W ) { full = true; n_stop_window++; break; }
       fd_frag_meta_t const * m = in_mcache + (in_seq & (in_depth-1UL));
@@ -1143,86 +1001,133 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       ulong chunk = m->chunk, sz = m->sz, ctl = m->ctl, tsorig = m->tsorig;
       __atomic_thread_fence( __ATOMIC_ACQUIRE );
       if( __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE ) != in_seq ) { ovrn++; in_seq++; continue; }
-      if( sz < 96UL || sz - 96UL > FD_ED25519_AMD_MSG_MAX ||
-          (zc_dev && (chunk << FD_CHUNK_LG_SZ) + ((sz + 63UL) & ~63UL) > zc_lim) ) {
+      bool const sz_ok = txn ? ( sz >= 1UL && sz <= FD_TXN_AMD_MTU ) : ( sz >= 96UL && sz - 96UL <= FD_ED25519_AMD_MSG_MAX );
+      if( !sz_ok || (zc_dev && (chunk << FD_CHUNK_LG_SZ) + ((sz + 63UL) & ~63UL) > zc_lim) ) {
         bad++; in_seq++; in_cnt++; continue;
       }
-      /* reserve the next output frame: not in flight, and no longer read
-         by a consumer that honours flow control */
-      ulong fr = t->frame_next, f = t->frame_next_idx;
-      if( fr - retired >= F ) { full = true; n_stop_frames++; break; }
-      if( out_fseq && t->frame_pub[f] != FRAME_FREE && (long)(t->frame_pub[f] - cons) >= 0 ) {
-        cons = __atomic_load_n( out_fseq, __ATOMIC_ACQUIRE );
-        if( (long)(t->frame_pub[f] - cons) >= 0 ) { backp++; full = true; break; }
-      }
       uchar const * p = (uchar const *)fd_chunk_to_laddr_const( in_chunk0b, chunk );
-      if( !zc_dev || t->tc.depth ) {
-        /* the frag 8 ahead: its bytes are read next (copy, or the HA tag) */
+      if( !zc_dev || t->tc.depth || txn ) {
+        /* the frag 8 ahead: its bytes are read next (copy; the HA tag; TXN's signature count) */
         fd_frag_meta_t const * m8 = in_mcache + ((in_seq + 8UL) & (in_depth-1UL));
         uchar const * p8 = (uchar const *)fd_chunk_to_laddr_const( in_chunk0b, __atomic_load_n( &m8->chunk, __ATOMIC_RELAXED ) );
         ulong const n8 = zc_dev ? 1UL : std::min( (ulong)__atomic_load_n( &m8->sz, __ATOMIC_RELAXED ), (ulong)FD_VERIFY_AMD_FRAME_SZ );
         for( ulong o = 0; o < n8; o += 64UL ) __builtin_prefetch( p8 + o );
       }
+      /* read from the source before any copy (the seq re-check after the
+         copy, or at publish in zero copy, covers them): the signature
+         slots (TXN: fd_amd_txn_slots1 on the first byte) and the HA tag
+         (the first 8 bytes of the first signature) */
+      ulong const k2 = txn ? fd_amd_txn_slots1( p, sz ) : 1UL;
+      ulong tag = 0UL;
+      if( t->tc.depth && k2 ) memcpy( &tag, p + (txn ? 1UL : 32UL), 8 );
+      uint f; bool credit;
+      if( !reserve( &f, &credit ) ) { full = true; if( credit ) backp++; else n_stop_frames++; break; }
       if( !zc_dev ) {
-        /* copy mode: the frame is the tile's copy.  The HA tag is read from
-           the source now (the seq re-check after the copy covers it too) */
-        ulong tag = 0UL;
-        if( t->tc.depth ) memcpy( &tag, p + 32, 8 );
-        jobs[nj++] = copy_job_t{ t->out_base + f * FD_VERIFY_AMD_FRAME_SZ, p, m, in_seq, fr, sz, tag, (uint)f,
-                                 (uint)tsorig, (ushort)ctl };
-        t->frame_pub[f] = FRAME_FREE;
-        t->frame_next++;
-        if( ++t->frame_next_idx == F ) t->frame_next_idx = 0UL;
+        /* copy mode: the frame is the tile's copy */
+        jobs[nj++] = copy_job_t{ t->out_base + (ulong)f * FD_VERIFY_AMD_FRAME_SZ, p, m, in_seq, sz, tag, f, (uint)tsorig,
+                                 (uint)k2, (ushort)ctl };
+        sl_pass += k2;
         in_seq++;
         continue;
       }
       in_seq++; in_cnt++;
-      if( t->tc.depth ) {   /* HA dedup on the first 8 signature bytes (reads the frag: a cache miss in zero copy) */
-        ulong ha_tag; memcpy( &ha_tag, p + 32, 8 );
-        if( t->tc.insert( ha_tag ) ) { ha++; ha_sz += sz; continue; }
-      }
-      t->frame_pub[f] = FRAME_FREE;
-      t->frame_next++;
-      if( ++t->frame_next_idx == F ) t->frame_next_idx = 0UL;
+      if( t->tc.depth && t->tc.insert( tag ) ) { ha++; ha_sz += sz; unreserve( f ); continue; }
       fd_amd_tile_ent_t * en = t->ring + (staged & mask);
       en->src_chunk = (uint32_t)chunk;
       en->out_chunk = (uint32_t)(f * FRAME_CHUNKS);
       en->sz        = (uint32_t)sz;
-      t->ppend[staged & mask] = pending_t{ in_seq - 1UL, fr, (ushort)sz, (ushort)ctl, (uint)tsorig, (uint)f, ts32, 0u, 0u };
+      en->slots     = (uint32_t)k2;
+      staged_sl += k2;
+      t->ppend[staged & mask] = pending_t{ in_seq - 1UL, (ushort)sz, (ushort)ctl, (uint)tsorig, f, ts32, 0u, (uint)staged_sl,
+                                           (uint)k2, 0u };
       staged++;
     }
     if( nj ) {
-      ulong const half = ( cp && nj >= COPY_SPLIT_MIN ) ? nj / 2UL : nj;
-      if( half < nj ) { cp->jobs = jobs.data(); cp->lo = half; cp->hi = nj; cp->gen.store( ++cgen, std::memory_order_release ); }
-      copy_jobs( jobs.data(), 0UL, half );
-      if( half < nj ) while( cp->done.load( std::memory_order_acquire ) != cgen ) _mm_pause();
+      if( jobs != ljobs.data() && nj >= COPY_SPLIT_MIN ) {
+        /* post the pass to the helper; claim blocks beside it */
+        ulong const g = gnext, s = snext, nb = (nj + CP_BLK - 1UL) / CP_BLK;
+        cgen = g;
+        cp->nj[s].store( nj, std::memory_order_relaxed );
+        cp->claim.store( g << 16, std::memory_order_release );
+        ulong mine = 0UL;   /* bit b: the stager copied block b */
+        for( ;; ) {
+          ulong c = cp->claim.load( std::memory_order_acquire );
+          ulong const b = c & 0xffffUL;
+          if( b >= nb ) break;
+          if( cp->claim.compare_exchange_weak( c, c + 1UL, std::memory_order_acq_rel ) ) {
+            copy_jobs( jobs, b * CP_BLK, std::min( nj, (b + 1UL) * CP_BLK ) );
+            mine |= 1UL << b;
+          }
+        }
+        /* the helper's blocks: wait a little, then re-copy what is still
+           missing into fresh frames (the old ones become orphans) */
+        ulong const tw = now_ns();
+        for( ulong b = 0; b < nb; b++ ) {
+          if( mine >> b & 1UL ) continue;
+          while( cp->done[s][b].load( std::memory_order_acquire ) != g && now_ns() - tw < CP_STEAL_NS ) _mm_pause();
+          if( cp->done[s][b].load( std::memory_order_acquire ) == g ) continue;
+          orphan_t o; o.g = g; o.s = s; o.b = b;
+          ulong const lo = b * CP_BLK, hi = std::min( nj, lo + CP_BLK );
+          bool okb = true;
+          std::vector<uint> fresh;
+          for( ulong k = lo; k < hi && okb; k++ ) {
+            uint f2; bool credit;
+            okb = reserve( &f2, &credit );
+            if( okb ) fresh.push_back( f2 );
+          }
+          if( !okb ) {   /* no frames to re-copy into: wait for the helper after all */
+            for( uint f2 : fresh ) unreserve( f2 );
+            while( cp->done[s][b].load( std::memory_order_acquire ) != g ) _mm_pause();
+            continue;
+          }
+          for( ulong k = lo; k < hi; k++ ) {
+            copy_job_t & jb = jobs[k];
+            o.frames.push_back( jb.f );
+            jb.f = fresh[k - lo];
+            jb.dst = t->out_base + (ulong)jb.f * FD_VERIFY_AMD_FRAME_SZ;
+            stage_copy_nt( jb.dst, jb.src, jb.sz );
+          }
+          orphan_cnt[s]++;
+          orphans.push_back( std::move( o ) );
+          n_steal++;
+        }
+      } else {
+        copy_jobs( jobs, 0UL, nj );
+      }
       __atomic_thread_fence( __ATOMIC_ACQUIRE );
       for( ulong k=0; k<nj; k++ ) {
         copy_job_t const & j = jobs[k];
         /* a frag lapped while it was copied is dropped (speculative read,
-           then seq re-check); its frame stays unused */
-        if( __atomic_load_n( &j.m->seq, __ATOMIC_ACQUIRE ) != j.seq ) { ovrn++; continue; }
+           then seq re-check); its frame is free again */
+        if( __atomic_load_n( &j.m->seq, __ATOMIC_ACQUIRE ) != j.seq ) { ovrn++; unreserve( j.f ); continue; }
         in_cnt++;
-        if( t->tc.depth && t->tc.insert( j.tag ) ) { ha++; ha_sz += j.sz; continue; }
+        if( t->tc.depth && t->tc.insert( j.tag ) ) { ha++; ha_sz += j.sz; unreserve( j.f ); continue; }
         fd_amd_tile_ent_t * en = t->ring + (staged & mask);
         en->src_chunk = (uint32_t)(j.f * FRAME_CHUNKS);
         en->out_chunk = (uint32_t)(j.f * FRAME_CHUNKS);
         en->sz        = (uint32_t)j.sz;
-        t->ppend[staged & mask] = pending_t{ j.seq, j.fr, (ushort)j.sz, j.ctl, j.tsorig, j.f, ts32, 0u, 0u };
+        en->slots     = j.slots;
+        staged_sl += j.slots;
+        t->ppend[staged & mask] = pending_t{ j.seq, (ushort)j.sz, j.ctl, j.tsorig, j.f, ts32, 0u, (uint)staged_sl, j.slots, 0u };
         staged++;
       }
     }
     r_blk = r_blk || full;
-    n_stop_bmax += staged - handed >= t->batch_max;
+    n_stop_bmax += staged_sl - handed_sl >= t->batch_max;
     n_stop_pass += staged == stage_end;
     __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
-    if( in_fseq && !zc_dev && in_seq != fseq_pub ) { __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE ); fseq_pub = in_seq; }
+    /* copy mode releases what it copied -- but never past a frag whose copy
+       an orphaned helper block may still be reading */
+    if( in_fseq && !zc_dev ) {
+      ulong const rel = copy_rel();
+      if( rel != fseq_pub ) { __atomic_store_n( in_fseq, rel, __ATOMIC_RELEASE ); fseq_pub = rel; }
+    }
     done_in = done_in || (frag_cnt && in_seq - in_seq0 >= frag_cnt);
 
-    /* 3. chunk mode by the staging rate (mean over ~0.4 ms) */
+    /* 3. chunk mode by the staging rate (slots/s, mean over ~0.4 ms) */
     ulong const t3 = now_ns();
     if( t3 - r_t0 >= 200000UL ) {
-      double inst = (double)(staged - r_n0) * 1e9 / (double)(t3 - r_t0);
+      double inst = (double)(staged_sl - r_n0) * 1e9 / (double)(t3 - r_t0);
       /* staging that stopped at the window, the frames or the consumer's
          credit measures the tile's own completions, not the offered load:
          such an interval never lowers the rate (else a full window reads as
@@ -1230,33 +1135,42 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
          capacity -- and the backlog grows) */
       if( r_blk ) inst = std::max( inst, rate );
       rate = rate > 0.0 ? 0.75 * rate + 0.25 * inst : inst;   /* ~0.8 ms memory: a burst does not flip the mode */
-      r_t0 = t3; r_n0 = staged; r_blk = false;
+      r_t0 = t3; r_n0 = staged_sl; r_blk = false;
       int nthr = fd_verify_amd_tile_mode( t->cfg.chunk_mode, thr, rate, t->rate_hi, t->rate_lo );
       switches += nthr != thr;
       thr = nthr;
     }
 
-    /* 4. hand over: cut staged frags into chunks and publish their
-          descriptors (x86 stores are ordered: entries and descriptors are
-          visible before the head) */
+    /* 4. hand over: cut staged slots into chunks (whole entries, packed by
+          slots) and publish their descriptors (x86 stores are ordered:
+          entries and descriptors are visible before the head) */
     if( staged != handed ) {
       while( cdone != t->desc_seq && t->desc_end[cdone & mask] <= pubd ) cdone++;
       ulong const waited = (ulong)(uint)((uint)t3 - t->ppend[handed & mask].t_stage);
-      ulong const upto = fd_verify_amd_tile_cut( &cc, staged, handed, t->desc_seq - cdone, thr, waited, full || done_in );
+      ulong const upto_sl = fd_verify_amd_tile_cut( &cc, staged_sl, handed_sl, t->desc_seq - cdone, thr, waited, full || done_in );
+      /* whole entries up to that slot count */
+      ulong upto = handed;
+      if( upto_sl == staged_sl ) upto = staged;
+      else while( upto != staged && (uint)(t->ppend[upto & mask].sl_end - (uint)handed_sl) <= (uint)(upto_sl - handed_sl) ) upto++;
       if( upto != handed ) {
-        ulong const K = thr ? 64UL : 8UL;
         ulong ds = t->desc_seq;
         uint const th = (uint)t3 & ~1u;
-        for( ulong c = handed; c < upto; c += K, ds++ ) {
-          ulong const cnt = std::min( K, upto - c );
+        for( ulong c = handed; c < upto; ) {
+          ulong const avail = std::min( 64UL, upto - c );
+          for( ulong q = 0; q < avail; q++ ) pk_slots[q] = t->ppend[(c + q) & mask].slots;
+          ulong nsl = 0UL;
+          ulong const cnt = fd_verify_amd_tile_pack( pk_slots.data(), avail, thr, &nsl );
+          bool const lat_chunk = !thr && nsl <= LAT_SLOTS;
           fd_amd_tile_desc_t * dd = t->desc + (ds & mask);
           dd->first = c;
-          dd->count = (uint32_t)cnt | (thr ? 0u : FD_AMD_TILE_LAT);
+          dd->count = (uint32_t)cnt | (lat_chunk ? FD_AMD_TILE_LAT : 0u);
           t->desc_end[ds & mask] = c + cnt;
+          for( ulong q = 0; q < cnt; q++ ) t->ppend[(c + q) & mask].t_hand = th | (lat_chunk ? 1u : 0u);   /* bit 0: latency chunk */
+          c += cnt; ds++;
         }
-        for( ulong c = handed; c < upto; c++ ) t->ppend[c & mask].t_hand = th | (thr ? 0u : 1u);   /* bit 0: latency chunk */
         t->desc_seq = ds;
-        nbatch++; nsig += upto - handed; n_hand++;
+        nbatch++; nsig += (ulong)(uint)(t->ppend[(upto - 1UL) & mask].sl_end - (uint)handed_sl); n_hand++;
+        handed_sl += (ulong)(uint)(t->ppend[(upto - 1UL) & mask].sl_end - (uint)handed_sl);
         handed = upto;
         r.handed.store( handed, std::memory_order_release );
         if( !zc_dev ) _mm_sfence();   /* the staged copies (non-temporal stores) before the head */
@@ -1293,13 +1207,18 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     }
   }
 
-  /* end: stop the publisher, then the kernel (its waves exit once nothing
-     is left to claim; chunks already claimed finish) */
+  /* end: stop the publisher, the helper, then the kernel (its waves exit
+     once nothing is left to claim; chunks already claimed finish) */
   r.end.store( staged, std::memory_order_release );
   if( rc || halted ) r.quit.store( 1, std::memory_order_release );
   if( pub.joinable() ) pub.join();
-  cpy.quit.store( 1, std::memory_order_release );
-  if( cth.joinable() ) cth.join();
+  if( cp ) {
+    cp->quit.store( 1, std::memory_order_release );
+    if( cth.joinable() ) cth.join();   /* it finishes the block it holds first */
+    for( orphan_t const & o : orphans ) for( uint f : o.frames ) unreserve( f );
+    orphans.clear();
+    delete cp;
+  }
   __atomic_store_n( &H->stop, 1u, __ATOMIC_RELEASE );
   {
     /* a kernel that never started is not waited for (it exits at once
@@ -1326,6 +1245,9 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     fprintf( stderr, "fd_verify_amd_tile_run: the tile kernel's watchdog fired (no host heartbeat for 5 s)\n" );
     rc = FD_ED25519_AMD_ERR_DEVICE;
   }
+  /* frags staged or in flight that were neither published nor filtered
+     (halted, or an error): their frames are free for the next run */
+  for( ulong q = r.pubd; q != staged; q++ ) unreserve( t->ppend[q & mask].fidx );
   diag->gpu_chunk_lat_cnt += st[0]; diag->gpu_chunk_thr_cnt += st[1];
   diag->gpu_frag_lat_cnt  += st[2]; diag->gpu_frag_thr_cnt  += st[3];
   diag->ovrn_cnt += ovrn + r.d.ovrn_cnt; diag->bad_frag_cnt += bad;
@@ -1340,7 +1262,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   t->ring_seq = staged;
   t->pass_max_ns = pass_max;
   t->n_pass = n_pass; t->n_hand = n_hand; t->n_stop_window = n_stop_window; t->n_stop_frames = n_stop_frames;
-  t->n_stop_bmax = n_stop_bmax; t->n_stop_pass = n_stop_pass;
+  t->n_stop_bmax = n_stop_bmax; t->n_stop_pass = n_stop_pass; t->n_steal = n_steal;
   __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
   if( in_fseq ) __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE );
   t->out_seq_end = r.out_seq;
@@ -1354,9 +1276,7 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
                         fd_verify_amd_diag_t * diag, uint * lat, ulong lat_max ) {
   if( !t || !in_mcache || !in_depth || (in_depth & (in_depth-1UL)) || !in_chunk0 || !out_mcache || !out_depth ||
       (out_depth & (out_depth-1UL)) || !diag || (!frag_cnt && !stop) ) return FD_ED25519_AMD_ERR_INVAL;
-  if( hipSetDevice( t->eng->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
-  bool txn = t->framing == FD_VERIFY_AMD_FRAMING_TXN;
-  if( txn && (t->batch_max < TXN_SIG_MAX_AT_MTU || tile_slots_alloc( t )) ) return FD_ED25519_AMD_ERR_INVAL;
+  if( hipSetDevice( t->device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
 
   /* Output session.  A run whose out_seq0 continues the previous run's
      output keeps the frames' publication record, so a frame a lagging
@@ -1364,7 +1284,7 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
      other out_seq0 starts a new session (a new consumer), with every frame
      free. */
   if( out_seq0 != t->out_seq_end ) std::fill( t->frame_pub.begin(), t->frame_pub.end(), FRAME_FREE );
-  t->frame_next = t->frame_retired = t->frame_next_idx = 0UL;
+  t->frame_next_idx = 0UL;
 
   /* zero copy: the input data region is mapped into the GPU; frags are
      handed over as (chunk, size) and copied on the device.  zc_lim: bytes
@@ -1378,15 +1298,35 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
     zc_dev = t->reg_dev + ((uint8_t const *)in_chunk0 - t->reg_base);
     zc_lim = t->reg_sz - (ulong)((uint8_t const *)in_chunk0 - t->reg_base);
   }
-  if( !txn )
-    return tile_run_persist( t, in_mcache, in_depth, in_chunk0, in_seq0, in_fseq, out_mcache, out_depth, out_seq0, out_fseq,
-                             frag_cnt, stop, diag, lat, lat_max, zc_dev, zc_lim );
-  return tile_run_batched( t, in_mcache, in_depth, in_chunk0, in_seq0, in_fseq, out_mcache, out_depth, out_seq0, out_fseq,
+  return tile_run_persist( t, in_mcache, in_depth, in_chunk0, in_seq0, in_fseq, out_mcache, out_depth, out_seq0, out_fseq,
                            frag_cnt, stop, diag, lat, lat_max, zc_dev, zc_lim );
 }
 
 /* ------------------------------------------------------------------ */
 /* streaming benchmark and end-to-end check: producer -> tile -> consumer */
+
+/* Move every other thread of this process off the given CPUs (those
+   whose mask would not become empty); returns the threads moved and their
+   old masks. */
+static std::vector<std::pair<pid_t, cpu_set_t>>
+tile_isolate_cpus( int const * cpus, int n ) {
+  std::vector<std::pair<pid_t, cpu_set_t>> moved;
+  pid_t const me = (pid_t)syscall( SYS_gettid );
+  DIR * d = opendir( "/proc/self/task" );
+  if( !d ) return moved;
+  for( struct dirent * e; (e = readdir( d )); ) {
+    pid_t const tid = (pid_t)atoi( e->d_name );
+    if( tid <= 0 || tid == me ) continue;
+    cpu_set_t old, nw; CPU_ZERO( &old );
+    if( sched_getaffinity( tid, sizeof old, &old ) ) continue;
+    nw = old;
+    for( int k=0; k<n; k++ ) if( cpus[k] >= 0 ) CPU_CLR( cpus[k], &nw );
+    if( !CPU_COUNT( &nw ) || CPU_EQUAL( &nw, &old ) ) continue;
+    if( !sched_setaffinity( tid, sizeof nw, &nw ) ) moved.emplace_back( tid, old );
+  }
+  closedir( d );
+  return moved;
+}
 
 extern "C" int
 fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, double rate, int flags,
@@ -1457,6 +1397,11 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
     cpu_set_t one; CPU_ZERO( &one ); CPU_SET( cpus[k], &one );
     (void)pthread_setaffinity_np( pthread_self(), sizeof one, &one );
   };
+  /* the process's other threads (HIP runtime, interpreter) stay off the
+     spinning threads' CPUs while the run lasts (as a deployed tile owns its
+     cores); their masks are restored afterwards */
+  std::vector<std::pair<pid_t, cpu_set_t>> moved;
+  if( pin ) moved = tile_isolate_cpus( cpus, ncpu );
 
   fd_verify_amd_tile_cfg_t cfg;
   fd_verify_amd_tile_cfg_default( &cfg );
@@ -1475,7 +1420,7 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   }
   uchar const * out_chunk0 = (uchar const *)fd_verify_amd_tile_out_chunk0( tile );
   std::vector<uint> parts;
-  if( !check && !txn ) { parts.resize( 4UL * frag_cnt ); fd_verify_amd_tile_set_trace( tile, parts.data(), frag_cnt ); }
+  if( !check ) { parts.resize( 4UL * frag_cnt ); fd_verify_amd_tile_set_trace( tile, parts.data(), frag_cnt ); }
 
   ulong in_fseq = 0UL;                                   /* the tile's credit to the producer */
   std::atomic<ulong> out_fseq( 0UL );                    /* consumer progress (the tile's output credit) */
@@ -1493,8 +1438,8 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
     pin_to( 1 );
     /* start once the tile's kernel runs (+2 ms): the launch of a run's
        persistent kernel is not part of the stream's latency (a deployed
-       tile runs until halted); the TXN batch path has no kernel to wait for */
-    if( !txn ) {
+       tile runs until halted) */
+    {
       ulong const w0 = now_ns();
       while( !tile->started && !__atomic_load_n( &tile_rc, __ATOMIC_ACQUIRE ) && now_ns() - w0 < 5000000000UL ) { /* spin */ }
       ulong const w1 = now_ns(); while( now_ns() - w1 < 2000000UL ) { /* spin */ }
@@ -1586,13 +1531,16 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   if( rc ) __atomic_store_n( &in_fseq, ~0UL >> 1, __ATOMIC_RELEASE );   /* unblock the producer */
   prod.join(); cons.join();
   if( pin ) (void)pthread_setaffinity_np( pthread_self(), sizeof saved, &saved );
+  for( auto const & mv : moved ) (void)sched_setaffinity( mv.first, sizeof mv.second, &mv.second );
   ulong const pass_max = tile->pass_max_ns;
   ulong const stg[6] = { tile->n_pass, tile->n_hand, tile->n_stop_window, tile->n_stop_frames, tile->n_stop_bmax, tile->n_stop_pass };
+  ulong const n_steal = tile->n_steal;
   fd_verify_amd_tile_delete( tile );
   free( dcache );
   if( rc ) return rc;
   ulong n = std::min( (ulong)diag.out_cnt, frag_cnt );
-  for( int k=0; k<41; k++ ) out[k] = 0.0;
+  for( int k=0; k<42; k++ ) out[k] = 0.0;
+  out[41] = (double)n_steal;
   if( t90 > t10 && t10 && s90 > s10 ) out[40] = (double)(s90 - s10) / ((double)(t90 - t10) * 1e-9);
   /* decomposition (before lat is sorted: the samples are per published frag) */
   /* paced runs: percentiles over the steady state (n_st samples); the

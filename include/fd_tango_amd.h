@@ -97,17 +97,18 @@ typedef struct {
   ulong out_sz;
   ulong ovrn_cnt;      /* input frags lost to producer overrun (skipped, or lapped before the tile was done) */
   ulong backp_cnt;     /* times the output was backpressured */
-  ulong batch_cnt;     /* GPU batches launched (persistent path: hand-offs to the GPU) */
-  ulong batch_sig_cnt; /* signatures in those batches (persistent path: frags handed over) */
+  ulong batch_cnt;     /* hand-offs to the GPU */
+  ulong batch_sig_cnt; /* signature slots handed over (PUB_SIG_MSG: frags; TXN: the transactions' signatures) */
   ulong bad_frag_cnt;  /* frags too short / too long to carry a signature, or (zero copy) reaching past the mapped region */
-  ulong gpu_chunk_lat_cnt;   /* persistent path: chunks the GPU verified 8 lanes per signature (latency mode) */
+  ulong gpu_chunk_lat_cnt;   /* chunks the GPU verified 8 lanes per signature (latency mode) */
   ulong gpu_chunk_thr_cnt;   /* ... 1 lane per signature (throughput mode) */
   ulong gpu_frag_lat_cnt;    /* frags in those chunks */
   ulong gpu_frag_thr_cnt;
-  ulong sv_filt_code_cnt[3]; /* SV_FILT by verdict: FD_ED25519_ERR_SIG, _PUBKEY, _MSG (PUB_SIG_MSG framing) */
+  ulong sv_filt_code_cnt[3]; /* SV_FILT by verdict: FD_ED25519_ERR_SIG, _PUBKEY, _MSG (a TXN parse failure,
+                                FD_TXN_AMD_ERR_PARSE, counts in sv_filt_cnt only) */
   ulong halt_drop_cnt;       /* frags taken in but neither published nor filtered: the run halted (*stop) while
                                 its output stayed backpressured past the halt grace */
-  ulong mode_switch_cnt;     /* persistent path: switches between latency and throughput chunks */
+  ulong mode_switch_cnt;     /* switches between latency and throughput chunks */
 } fd_verify_amd_diag_t;
 
 typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
@@ -115,22 +116,28 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
 /* Tile configuration (fd_verify_amd_tile_new_cfg).  Fill it with
    fd_verify_amd_tile_cfg_default, then change what differs.
 
-   GPU side (PUB_SIG_MSG framing): ONE persistent kernel per run
+   GPU side (both framings): ONE persistent kernel per run
    (k_tile_persist) holds `waves` wave slots of the GPU while the run lasts
-   (0: 8 x CUs divided by the PUB_SIG_MSG tiles that exist on the device --
-   create a GPU's tiles before running any; tiles in different processes
-   set their share here) and verifies what the tile's host side hands over
-   through mapped host memory -- ring entries (frag chunk, output frame,
-   size) and chunk descriptors -- on one stream, so it needs one hardware
-   queue and the GPU never drains between hand-offs.  Its share must be
-   free when the run starts: a run whose kernel does not start within 2 s
-   (another kernel holds the slots) or stops making progress returns
-   FD_ED25519_AMD_ERR_DEVICE instead of waiting.
+   (0: 8 x CUs divided by the tiles that exist on the device -- create a
+   GPU's tiles before running any; tiles in different processes set their
+   share here) and verifies what the tile's host side hands over through
+   mapped host memory -- ring entries (frag chunk, output frame, size,
+   signature slots) and chunk descriptors -- on one high-priority stream,
+   so it needs one hardware queue and the GPU never drains between
+   hand-offs.  A process gets GPU_MAX_HW_QUEUES (default 4) such queues:
+   creating more tiles than that on one device fails (NULL).  Its share
+   must be free when the run starts: a run whose kernel does not start
+   within 2 s (another kernel holds the slots) or stops making progress
+   returns FD_ED25519_AMD_ERR_DEVICE instead of waiting.
 
-   Chunks.  A chunk takes one wave whatever its size.  Latency chunks hold
-   up to 8 frags verified 8 lanes per signature (~0.45 ms on a SIMD of its
-   own); throughput chunks up to 64 frags, 1 lane per signature (~1.2 ms
-   alone, ~2.2 ms with every wave slot busy), 3-4x the frags per wave-ms.
+   Chunks.  A chunk takes one wave whatever its size and holds whole frags.
+   Latency chunks hold up to 8 signature slots verified 8 lanes per
+   signature (~0.45 ms on a SIMD of its own); throughput chunks up to 64
+   slots, 1 lane per signature (~1.2 ms alone, ~2.2 ms with every wave slot
+   busy), 3-4x the signatures per wave-ms.  A PUB_SIG_MSG frag is one slot;
+   a TXN frag takes as many slots as its signature count (its first byte),
+   and one of more than 8 signatures makes a 1-lane chunk of its own even
+   in latency mode.  All rates and counts below are in slots.
    chunk_mode AUTO picks by the staging rate (EWMA over ~0.8 ms): throughput
    chunks above thr_rate_hi frags/s, latency chunks again below thr_rate_lo
    (0: 55 % / 40 % of the latency chunks' capacity, min(min(waves, 4 x CUs)
@@ -144,26 +151,25 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    batch_wait_ns.  At most `window` frags are in flight (handed over, not
    yet published; 0: 2^18 from batch_max 4096, 2^17 from 1024, else
    64 x batch_max, >= 2^15).
-   TXN framing uses the batch path: up to 4 batches in flight, each on its
-   own stream (parse, verify, reduce per batch).
-
    Host side.  The caller's thread polls, dedups and stages; publishing
    runs on a second host thread when publish_cpu >= 0 (pinned there) or,
    with FD_VERIFY_AMD_PUBLISH_AUTO, when the caller's CPU set holds another
    CPU (the thread gets that set minus the caller's current CPU);
    FD_VERIFY_AMD_PUBLISH_INLINE keeps both on the caller's thread.  In copy
-   mode a third thread, pinned to copy_cpu (>= 0), copies half of each
+   mode a third thread, pinned to copy_cpu (>= 0), copies blocks of each
    staging pass's frags beside the caller's thread (passes of 32 frags or
-   more; FD_VERIFY_AMD_COPY_INLINE, the default: the caller copies all).  After
-   *stop the run publishes what completes, for at most halt_grace_ns while
-   its output is backpressured, then returns (halt_drop_cnt).
+   more; FD_VERIFY_AMD_COPY_INLINE, the default: the caller copies all); a
+   block the helper has not finished 30 us after the caller ran out of
+   blocks is copied again by the caller into fresh frames, so a descheduled
+   helper never stalls the tile.  After *stop the run publishes everything
+   it took in; only while its output is backpressured does a grace of
+   halt_grace_ns run, after which it returns (halt_drop_cnt).
 
    Output data region.  Like the reference verify tile, which publishes
    frags out of a dcache it owns (fd_frank_verify_synth_load.c:324,409-411),
    the tile owns its output dcache: out_frame_cnt frames of
-   FD_VERIFY_AMD_FRAME_SZ bytes (0: 4096 + batch_max + the frags it can
-   hold in flight -- the PUB_SIG_MSG window, or 4 x batch_max for TXN
-   framing; pinned host memory, ~370 MB at the 2^18 window).  Every
+   FD_VERIFY_AMD_FRAME_SZ bytes (0: 4096 + batch_max + the window; pinned
+   host memory, ~370 MB at the 2^18 window).  Every
    published frag's chunk is relative to fd_verify_amd_tile_out_chunk0 and
    its bytes are the bytes that were verified.  A frame is reused only once
    the consumer's out_fseq has passed the frag it last carried
@@ -232,8 +238,13 @@ fd_verify_amd_tile_out_data_sz( fd_verify_amd_tile_t * tile );
    against its account address (multi-signer) and publishes the transaction
    iff it parses and all its signatures pass; HA dedup uses its first
    signature, the published tag is that signature's SHA-512 tag.  A frag
-   that fails to parse counts as SV_FILT.  TXN needs batch_max >= 19 (the
-   most signatures a 1232-B transaction can carry), else ERR_INVAL. */
+   that fails to parse counts as SV_FILT (its verdict is
+   FD_TXN_AMD_ERR_PARSE); an empty or over-MTU frag is a bad frag.  The
+   same persistent kernel verifies both framings (the host reads each
+   transaction's signature count; a chunk's lanes parse its transactions,
+   verify their signatures and reduce per transaction).  TXN needs
+   batch_max >= 19 (the most signatures a 1232-B transaction can carry),
+   else ERR_INVAL. */
 #define FD_VERIFY_AMD_FRAMING_PUB_SIG_MSG (0)
 #define FD_VERIFY_AMD_FRAMING_TXN         (1)
 int
@@ -319,9 +330,10 @@ fd_verify_amd_tile_set_trace( fd_verify_amd_tile_t * tile, uint * parts, ulong p
 void
 fd_verify_amd_tile_set_verdict_log( fd_verify_amd_tile_t * tile, schar * log, ulong log_max );
 
-/* The persistent path's hand-off rule (pure; what fd_verify_amd_tile_run
-   applies to its staged frags [handed, staged)): returns how far to hand
-   over now.  thr: throughput chunks (64 frags) else latency chunks (8).
+/* The hand-off rule (pure; what fd_verify_amd_tile_run applies to its
+   staged signature slots [handed, staged)): returns how far to hand over
+   now (the run then hands over the whole frags below that).  thr:
+   throughput chunks (64 slots) else latency chunks (8).
    Whole chunks go at once; a partial latency chunk once waited_ns (its
    oldest frag's wait) >= lat_fill_ns or while chunks_in_flight <
    lat_free_chunks; a partial throughput chunk once waited_ns >=
@@ -336,6 +348,14 @@ fd_verify_amd_tile_cut( fd_verify_amd_tile_cfg_t const * cfg, ulong staged, ulon
    back when rate < rate_lo; the other modes are fixed. */
 int
 fd_verify_amd_tile_mode( int chunk_mode, int thr, double rate, double rate_hi, double rate_lo );
+
+/* The chunk packing rule (pure): of cnt staged frags carrying slots[i]
+   signature slots each, the next chunk takes the first n (returned; *nsl =
+   their slots): at most 64 frags and 64 slots (thr) or 8 slots (latency),
+   whole frags only, so a frag of more slots than that is a chunk of its
+   own (verified 1 lane per signature). */
+ulong
+fd_verify_amd_tile_pack( uint const * slots, ulong cnt, int thr, ulong * nsl );
 
 /* Streaming benchmark and end-to-end check (config 5): a producer thread
    publishes frags public_key | signature | message cyclically from the
@@ -372,8 +392,8 @@ fd_verify_amd_tile_mode( int chunk_mode, int thr, double rate, double rate_hi, d
    (SV_FILT), out[7] = overrun frags, out[8] = check mismatches (published
    frags that fail a check, plus frags that should have been published and
    were not, overrun ones excepted), out[9] = frags checked, out[10..13] =
-   the persistent path's GPU chunks in latency / throughput mode and the
-   frags in each (0 on the batch path), out[14] = the paced producer's
+   the GPU chunks in latency / throughput mode and the frags in each,
+   out[14] = the paced producer's
    largest lateness behind its schedule (ns; its stalls count as latency),
    out[15] = the tile thread's longest pass of its run loop (ns; a stall of
    the host thread shows here), out[16] = the consumer's longest gap between
@@ -391,7 +411,9 @@ fd_verify_amd_tile_mode( int chunk_mode, int thr, double rate, double rate_hi, d
    20 ms or more after the start, and out[38] / out[39] = p50 / p99 of every
    frag.  out[40] (check mode) = the steady-state rate: input frags between
    10 % and 90 % of the run over the time the consumer took from one to the
-   other (out[0] includes the run's ramp and drain).  out holds 41 doubles.
+   other (out[0] includes the run's ramp and drain); out[41] = copy blocks
+   the tile's stager re-copied because its helper had stalled.  out holds
+   42 doubles.
    Threads: producer, tile, the tile's publisher and consumer each pinned
    to a CPU of their own when the process may use 5 or more (else unpinned,
    publisher inline); copy mode adds the tile's copy helper on a fifth CPU

@@ -296,6 +296,94 @@ def test_tile_txn_framing_vs_oracle(zero_copy):
         assert int(mc_out[o]["sig"]) == tag
 
 
+def _txn_through_tile(pays, chunk_mode=0, zero_copy=False, batch_max=4096, depth=1 << 16):
+    """Wire transactions as frags (one per frame, in order) through a TXN
+    tile with HA dedup off: (diag, verdict log, published frames, tags,
+    published input seqs)."""
+    from firedancer_amd import tango
+    mtu_chunks = ((1232 + 127) >> 7) << 1
+    n = len(pays)
+    dcache = tango._aligned((64 * mtu_chunks * (n + 2) + 4095) & ~4095, 4096)
+    mc_in, mc_out = tango.mcache_new(depth), tango.mcache_new(depth)
+    for seq, p in enumerate(pays):
+        c = seq * mtu_chunks
+        if len(p):
+            dcache[64 * c:64 * c + len(p)] = np.frombuffer(p, np.uint8)
+        tango.publish(mc_in, seq, 0, c, len(p), 3, seq, 0)
+    tile = tango.VerifyTile(0, batch_max=batch_max, tcache_depth=0, framing=tango.VerifyTile.FRAMING_TXN,
+                            chunk_mode=chunk_mode)
+    if zero_copy:
+        tile.register_dcache(dcache)
+    log = np.full(n, 99, np.int8)
+    tile.set_verdict_log(log)
+    try:
+        diag, _ = tile.run(mc_in, dcache, 0, mc_out, 0, n)
+        k = int(diag["out_cnt"])
+        frames = [tile.out_frame(mc_out[o]["chunk"], mc_out[o]["sz"]) for o in range(k)]
+        tags = [int(mc_out[o]["sig"]) for o in range(k)]
+        seqs = [int(mc_out[o]["tsorig"]) for o in range(k)]
+    finally:
+        tile.close()
+    return diag, log, frames, tags, seqs
+
+
+def _txn_tag(p):
+    """First signature's SHA-512 tag of a well-formed transaction (the
+    synthetic and fixture ones have < 128 accounts: one-byte compact-u16)."""
+    m = 1 + 64 * p[0]
+    a = m + (1 if p[m] & 0x80 else 0) + 4
+    return int.from_bytes(hashlib.sha512(p[1:33] + p[a:a + 32] + p[m:]).digest()[:8], "little")
+
+
+@pytest.mark.parametrize("zero_copy", [False, True])
+def test_tile_txn_reference_mutations_vs_oracle(zero_copy):
+    """Every mutation of the reference's three fixture transactions
+    (tests/golden/txn_mutations.bin: footprints from the COMPILED reference
+    fd_txn_parse) as TXN frags through the persistent kernel: every frag's
+    verdict equals the oracle's (-4 exactly where the reference's footprint
+    is 0), and the published frags are the accepted ones, in order, with
+    their bytes and first-signature tags."""
+    import _txn
+    for f in _txn.load_fixtures():
+        allm = _txn.mutation_list(f.payload)
+        keep = [i for i, m in enumerate(allm) if 1 <= len(m) <= 1232]   # an empty frag is a bad frag, not a txn
+        muts = [allm[i] for i in keep]
+        fps = f.footprint[keep]
+        blob, off, sz = _txn.pack(muts)
+        eterr, _, _ = _oracle.txn_verify_batch(blob, off, sz)
+        assert np.array_equal(eterr == -4, fps == 0)
+        diag, log, frames, tags, seqs = _txn_through_tile(muts, zero_copy=zero_copy)
+        bad = np.nonzero(log != eterr)[0]
+        assert bad.size == 0, [(int(i), int(log[i]), int(eterr[i])) for i in bad[:10]]
+        acc = np.nonzero(eterr == 0)[0].tolist()
+        assert seqs == acc and diag["out_cnt"] == len(acc) and diag["sv_filt_cnt"] == len(muts) - len(acc)
+        assert all(frames[o] == muts[i] for o, i in enumerate(acc))
+        assert tags == [_txn_tag(muts[i]) for i in acc]
+
+
+@pytest.mark.parametrize("chunk_mode", [0, 1, 2])   # AUTO, LATENCY (8 slots; > 8 signers alone, 1 lane each), THROUGHPUT
+def test_tile_txn_mixed_vs_oracle_per_chunk_mode(chunk_mode):
+    """1500 multi-signer transactions (1..12 signers, 64..1232 B, legacy and
+    v0) with corrupted signatures, signer keys, headers and truncations,
+    through the persistent kernel with each chunk mode: every transaction's
+    verdict equals the oracle's; accepted ones publish in order with their
+    first signature's tag; slots are packed <= 64 (<= 8 in latency chunks)."""
+    import test_txn_gpu
+    pays = test_txn_gpu._mixed_batch(77 + chunk_mode, 1500)
+    blob, off, sz = __import__("_txn").pack(pays)
+    eterr, _, _ = _oracle.txn_verify_batch(blob, off, sz)
+    diag, log, frames, tags, seqs = _txn_through_tile(pays, chunk_mode=chunk_mode, zero_copy=chunk_mode == 2)
+    bad = np.nonzero(log != eterr)[0]
+    assert bad.size == 0, [(int(i), int(log[i]), int(eterr[i])) for i in bad[:10]]
+    acc = np.nonzero(eterr == 0)[0].tolist()
+    assert seqs == acc and tags == [_txn_tag(pays[i]) for i in acc]
+    assert set(np.unique(eterr).tolist()) >= {0, -3, -4}
+    if chunk_mode == 2:
+        assert diag["gpu_chunk_lat_cnt"] == 0
+    if chunk_mode == 1:
+        assert diag["gpu_chunk_lat_cnt"] > 0
+
+
 def test_tile_txn_framing_needs_room_for_a_full_transaction():
     """TXN framing with batch_max < 19 could never stage a 19-signer
     transaction: refused up front instead of spinning."""
@@ -492,6 +580,71 @@ def test_tile_halts_while_backpressured():
     diag, _ = res["r"]
     assert diag["out_cnt"] == 256 and diag["halt_drop_cnt"] > 0
     assert diag["out_cnt"] + diag["sv_filt_cnt"] + diag["halt_drop_cnt"] == diag["in_cnt"]
+
+
+def test_tile_stop_drains_a_slow_share_without_drops():
+    """*stop while the GPU is slow to drain (a 16-wave share, a full window)
+    but the output is NOT backpressured (no out_fseq): the halt grace (here
+    1 ms) never starts, the run publishes everything it took in, and
+    halt_drop_cnt stays 0 (the grace runs only while
+    backpressured)."""
+    import ctypes
+    import threading
+    import time
+    from firedancer_amd import tango
+    n = 6000
+    pub, sig, msgs, (mc_in, dc, _, _, _) = _signed_feed(3737, n, 8192)
+    mc_out = tango.mcache_new(8192)
+    tile = tango.VerifyTile(0, batch_max=1024, tcache_depth=0, waves=16, halt_grace_ns=1000000,
+                            chunk_mode=tango.CHUNK_THROUGHPUT)
+    stop = ctypes.c_int(0)
+    res = {}
+
+    def go():
+        try:
+            res["r"] = tile.run(mc_in, dc, 0, mc_out, 0, 0, stop=stop)
+        except Exception as e:   # noqa: BLE001
+            res["e"] = e
+
+    th = threading.Thread(target=go)
+    th.start()
+    try:
+        t0 = time.time()
+        while int(mc_out[0]["seq"]) != 0 and time.time() - t0 < 30:
+            time.sleep(0.0002)
+        stop.value = 1                              # frags are still in flight on a slow share
+        th.join(timeout=30)
+        assert not th.is_alive()
+    finally:
+        stop.value = 1
+        th.join(timeout=30)
+        tile.close()
+    assert "e" not in res, res.get("e")
+    diag, _ = res["r"]
+    assert diag["halt_drop_cnt"] == 0
+    assert diag["out_cnt"] + diag["sv_filt_cnt"] == diag["in_cnt"] > 64
+    assert all(int(mc_out[o]["seq"]) == o for o in range(int(diag["out_cnt"])))
+
+
+def test_tiles_per_device_capped_at_hw_queues():
+    """Each tile's run holds one hardware queue of the high-priority pool
+    for its whole run; a process gets GPU_MAX_HW_QUEUES (4) per priority, so
+    a fifth tile on one device is refused at creation instead of queueing
+    its kernel behind another tile's run."""
+    import os
+    from firedancer_amd import ed25519, tango
+    cap = int(os.environ.get("GPU_MAX_HW_QUEUES") or 4)
+    tiles = []
+    try:
+        for _ in range(cap):
+            tiles.append(tango.VerifyTile(0, batch_max=256, tcache_depth=0))
+        with pytest.raises(ed25519.EngineError):
+            tango.VerifyTile(0, batch_max=256, tcache_depth=0)
+        tiles.pop().close()
+        tiles.append(tango.VerifyTile(0, batch_max=256, tcache_depth=0))   # a freed queue is usable again
+    finally:
+        for t in tiles:
+            t.close()
 
 
 def test_engine_call_beside_a_tile_with_a_partial_share(golden, engine):
