@@ -159,9 +159,9 @@ inline ulong now_ns( void ) {
 #define LAT_SLOTS    (8UL)          /* ... of a latency chunk (8 lanes each) */
 
 /* Copy mode's helper protocol (below) */
-#define CP_BLK      (8UL)                    /* frags per claimed copy block */
+#define CP_NB       (2UL)                    /* copy blocks per pass: the two halves (one CAS each: finer blocks cost
+                                                more in cache-line round trips than they balance) */
 #define CP_NJ       (4UL)                    /* job arrays in the helper's ring */
-#define CP_NB       (STAGE_PASS / CP_BLK)    /* blocks per pass at most */
 #define CP_STEAL_NS (30000UL)                /* a helper block still unfinished this long after the stager ran out of
                                                 blocks is re-copied by the stager into fresh frames */
 #define COPY_SPLIT_MIN (32UL)                /* passes of fewer frags are copied on the stager alone */
@@ -210,7 +210,7 @@ copy_jobs( copy_job_t const * j, ulong lo, ulong hi ) {
 
 /* The copy helper (cfg.copy_cpu).  A pass posts its job list as a
    generation g into job array g % CP_NJ; the stager and the helper both
-   claim blocks of CP_BLK frags by CAS on `claim` (g << 16 | next block),
+   claim its two halves by CAS on `claim` (g << 16 | next block),
    and the helper marks each block it copied in done[g % CP_NJ][b] = g.
    The stager never waits on a helper that stopped running (a descheduled
    pinned thread held a pass for up to 9 ms, profiles/r05_bench_a_detail.json):
@@ -224,7 +224,7 @@ struct copier_t {
   alignas(64) std::atomic<ulong> claim;
   alignas(64) std::atomic<int>   quit;
   alignas(64) std::atomic<ulong> done[CP_NJ][CP_NB];
-  std::atomic<ulong>             nj[CP_NJ];
+  std::atomic<ulong>             nj[CP_NJ], bsz[CP_NJ];   /* a pass's frags and its block size (half, rounded up) */
   copy_job_t                     jobs[CP_NJ][STAGE_PASS];
 };
 
@@ -236,10 +236,10 @@ copier_loop( copier_t * cp, int cpu ) {
     ulong c = cp->claim.load( std::memory_order_acquire );
     ulong const g = c >> 16, b = c & 0xffffUL;
     if( g ) {
-      ulong const s = g % CP_NJ, nj = cp->nj[s].load( std::memory_order_relaxed );
-      if( b * CP_BLK < nj ) {
+      ulong const s = g % CP_NJ, nj = cp->nj[s].load( std::memory_order_relaxed ), bz = cp->bsz[s].load( std::memory_order_relaxed );
+      if( b < CP_NB && b * bz < nj ) {
         if( cp->claim.compare_exchange_weak( c, c + 1UL, std::memory_order_acq_rel ) ) {
-          copy_jobs( cp->jobs[s], b * CP_BLK, std::min( nj, (b + 1UL) * CP_BLK ) );
+          copy_jobs( cp->jobs[s], b * bz, std::min( nj, (b + 1UL) * bz ) );
           _mm_sfence();   /* the copies before the done mark */
           cp->done[s][b].store( g, std::memory_order_release );
         }
@@ -889,7 +889,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     cp = new (std::nothrow) copier_t();
     if( cp ) {
       cp->claim.store( 0UL ); cp->quit.store( 0 );
-      for( ulong s=0; s<CP_NJ; s++ ) { cp->nj[s].store( 0UL ); for( ulong b=0; b<CP_NB; b++ ) cp->done[s][b].store( 0UL ); }
+      for( ulong s=0; s<CP_NJ; s++ ) { cp->nj[s].store( 0UL ); cp->bsz[s].store( 1UL ); for( ulong b=0; b<CP_NB; b++ ) cp->done[s][b].store( 0UL ); }
       try { cth = std::thread( copier_loop, cp, t->cfg.copy_cpu ); } catch( ... ) { delete cp; cp = NULL; }
     }
   }
@@ -938,7 +938,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
      whose source an orphaned helper block may still be reading */
   auto copy_rel = [&]() -> ulong {
     ulong rel = in_seq;
-    for( orphan_t const & o : orphans ) rel = std::min( rel, cp->jobs[o.s][o.b * CP_BLK].seq );
+    for( orphan_t const & o : orphans ) rel = std::min( rel, cp->jobs[o.s][o.b * cp->bsz[o.s].load( std::memory_order_relaxed )].seq );
     return rel;
   };
 
@@ -1045,9 +1045,10 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     if( nj ) {
       if( jobs != ljobs.data() && nj >= COPY_SPLIT_MIN ) {
         /* post the pass to the helper; claim blocks beside it */
-        ulong const g = gnext, s = snext, nb = (nj + CP_BLK - 1UL) / CP_BLK;
+        ulong const g = gnext, s = snext, bz = (nj + 1UL) / 2UL, nb = CP_NB;
         cgen = g;
         cp->nj[s].store( nj, std::memory_order_relaxed );
+        cp->bsz[s].store( bz, std::memory_order_relaxed );
         cp->claim.store( g << 16, std::memory_order_release );
         ulong mine = 0UL;   /* bit b: the stager copied block b */
         for( ;; ) {
@@ -1055,7 +1056,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
           ulong const b = c & 0xffffUL;
           if( b >= nb ) break;
           if( cp->claim.compare_exchange_weak( c, c + 1UL, std::memory_order_acq_rel ) ) {
-            copy_jobs( jobs, b * CP_BLK, std::min( nj, (b + 1UL) * CP_BLK ) );
+            copy_jobs( jobs, b * bz, std::min( nj, (b + 1UL) * bz ) );
             mine |= 1UL << b;
           }
         }
@@ -1067,7 +1068,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
           while( cp->done[s][b].load( std::memory_order_acquire ) != g && now_ns() - tw < CP_STEAL_NS ) _mm_pause();
           if( cp->done[s][b].load( std::memory_order_acquire ) == g ) continue;
           orphan_t o; o.g = g; o.s = s; o.b = b;
-          ulong const lo = b * CP_BLK, hi = std::min( nj, lo + CP_BLK );
+          ulong const lo = b * bz, hi = std::min( nj, lo + bz );
           bool okb = true;
           std::vector<uint> fresh;
           for( ulong k = lo; k < hi && okb; k++ ) {
@@ -1148,18 +1149,23 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       while( cdone != t->desc_seq && t->desc_end[cdone & mask] <= pubd ) cdone++;
       ulong const waited = (ulong)(uint)((uint)t3 - t->ppend[handed & mask].t_stage);
       ulong const upto_sl = fd_verify_amd_tile_cut( &cc, staged_sl, handed_sl, t->desc_seq - cdone, thr, waited, full || done_in );
-      /* whole entries up to that slot count */
+      /* whole entries up to that slot count (PUB_SIG_MSG: one slot per entry) */
       ulong upto = handed;
       if( upto_sl == staged_sl ) upto = staged;
+      else if( !txn ) upto = handed + (upto_sl - handed_sl);
       else while( upto != staged && (uint)(t->ppend[upto & mask].sl_end - (uint)handed_sl) <= (uint)(upto_sl - handed_sl) ) upto++;
       if( upto != handed ) {
         ulong ds = t->desc_seq;
         uint const th = (uint)t3 & ~1u;
         for( ulong c = handed; c < upto; ) {
           ulong const avail = std::min( 64UL, upto - c );
-          for( ulong q = 0; q < avail; q++ ) pk_slots[q] = t->ppend[(c + q) & mask].slots;
-          ulong nsl = 0UL;
-          ulong const cnt = fd_verify_amd_tile_pack( pk_slots.data(), avail, thr, &nsl );
+          ulong nsl = 0UL, cnt;
+          if( txn ) {
+            for( ulong q = 0; q < avail; q++ ) pk_slots[q] = t->ppend[(c + q) & mask].slots;
+            cnt = fd_verify_amd_tile_pack( pk_slots.data(), avail, thr, &nsl );
+          } else {
+            cnt = nsl = std::min( avail, thr ? CHUNK_SLOTS : LAT_SLOTS );   /* the same rule, one slot per frag */
+          }
           bool const lat_chunk = !thr && nsl <= LAT_SLOTS;
           fd_amd_tile_desc_t * dd = t->desc + (ds & mask);
           dd->first = c;
