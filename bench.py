@@ -725,14 +725,21 @@ def stream_node(local, pub, sig, off, sz, blob, args, rank, world, dist):
     CPUs).  Rank 0 reports the node sum."""
     import torch
     from firedancer_amd import hip, tango
-    from firedancer_amd.shard import cpu_slice, max_over_ranks, peer_slot
+    from firedancer_amd.shard import max_over_ranks, node_plan, node_sum, peer_slot
     from firedancer_amd import ed25519
     ndev = max(1, hip.device_count())
     keys = [None] * world
-    dist.all_gather_object(keys, {"numa": ed25519.device_numa_node(local), "dev": local % ndev})
-    k, n = peer_slot([x["numa"] for x in keys], rank)
     saved = os.sched_getaffinity(0)
-    cpus = cpu_slice(saved, k, n) if n > 1 else sorted(saved)
+    dist.all_gather_object(keys, {"numa": ed25519.device_numa_node(local), "dev": local % ndev,
+                                  "cpus": sorted(saved), "quota": host_cores()[2]["cgroup_quota"]})
+    # every rank's CPU slice and host budget from one node plan (ranks on a NUMA node split its CPUs; the
+    # processes' shared cgroup quota, if any, caps the sum)
+    numa = [x["numa"] for x in keys]
+    node_cpus = {}
+    for x in keys:
+        node_cpus[x["numa"]] = sorted(set(node_cpus.get(x["numa"], [])) | set(x["cpus"]))
+    plans, plan_tot = node_plan(numa, node_cpus, 16384, zero_copy=True, cpu_quota=keys[0]["quota"])
+    cpus = plans[rank]["cpus"]
     if len(cpus) >= 5:
         os.sched_setaffinity(0, cpus)
     _, share = peer_slot([x["dev"] for x in keys], rank)
@@ -758,17 +765,21 @@ def stream_node(local, pub, sig, off, sz, blob, args, rank, world, dist):
                float(waves)]
     finally:
         os.sched_setaffinity(0, saved)
-    t = torch.zeros(world * len(res), dtype=torch.float64)
-    t[rank * len(res):(rank + 1) * len(res)] = torch.tensor(res, dtype=torch.float64)
+    cols = ["saturated_frags_per_s", "half_frags_per_s", "p50_us", "p99_us", "cpus", "waves"]
+    t = torch.zeros(world * len(cols), dtype=torch.float64)
+    if res:
+        t[rank * len(cols):(rank + 1) * len(cols)] = torch.tensor(res, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    per = t.view(world, len(res)).tolist()
+    agg = node_sum(t.view(world, len(cols)).tolist(), cols)
     return {"ranks": world, "batch_max": 16384, "staging": "zero_copy",
-            "saturated_frags_per_s_node": sum(r[0] for r in per),
+            "saturated_frags_per_s_node": agg["saturated_frags_per_s"],
             "saturated_run_span_s_max": span_sat,
-            "at_50%_frags_per_s_node": sum(r[1] for r in per),
-            "per_rank": [{"saturated_frags_per_s": r[0], "at_50%": {"frags_per_s": r[1], "p50_us": r[2], "p99_us": r[3]},
-                          "cpus": int(r[4]), "waves": int(r[5]), "numa_node": keys[i]["numa"], "device": keys[i]["dev"]}
-                         for i, r in enumerate(per)],
+            "at_50%_frags_per_s_node": agg["half_frags_per_s"],
+            "per_rank": [{"saturated_frags_per_s": r["saturated_frags_per_s"],
+                          "at_50%": {"frags_per_s": r["half_frags_per_s"], "p50_us": r["p50_us"], "p99_us": r["p99_us"]},
+                          "cpus": int(r["cpus"]), "waves": int(r["waves"]), "numa_node": keys[i]["numa"],
+                          "device": keys[i]["dev"]} for i, r in enumerate(agg["per_rank"])],
+            "host_budget": plan_tot,
             "note": "every rank's tile runs at once (barrier before each run); node value = sum of the ranks' rates"}
 
 

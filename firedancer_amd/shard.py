@@ -101,3 +101,87 @@ def cpu_slice(cpus, k, n):
         raise ValueError("bad slice %r of %r" % (k, n))
     per = len(cpus) // n
     return cpus[k * per:(k + 1) * per]
+
+
+# ---------------------------------------------------------------- node plan
+
+FRAME_SZ = 1408                        # FD_VERIFY_AMD_FRAME_SZ
+RING_ENTRY_BYTES = 16 + 16 + 24        # ring entry + chunk descriptor + 3 result words, per ring slot
+
+
+def tile_window(batch_max, window=0):
+    """The tile's default window (frags in flight), fd_verify_tile.cpp tile_window."""
+    if window:
+        return int(window)
+    if batch_max >= 1 << 12:
+        return 1 << 18
+    if batch_max >= 1 << 10:
+        return 1 << 17
+    return max(64 * batch_max, 1 << 15)
+
+
+def tile_budget(batch_max, cpus, zero_copy=True, window=0, out_frame_cnt=0):
+    """Host budget of ONE verify tile on the CPU slice `cpus` (sorted list):
+    which spinning threads it runs on which CPU, and the pinned host memory
+    it holds (fd_verify_amd_tile_new_cfg / _run).
+
+    Threads, in the order they get a CPU of their own: the stager (the
+    caller's thread, always), the publisher (cfg.publish_cpu; inline on the
+    stager when the slice has one CPU), and, in copy mode only, the copy
+    helper (cfg.copy_cpu; inline when the slice has fewer than 3 CPUs).
+    Pinned memory: the output dcache ((4096 + batch_max + window) frames of
+    1408 B), the ring / descriptors / results (a power of 2 >= the window,
+    56 B per slot), 4 KB of control words."""
+    cpus = sorted(cpus)
+    if not cpus:
+        raise ValueError("a tile needs at least one CPU")
+    w = tile_window(batch_max, window)
+    frames = int(out_frame_cnt) or 4096 + int(batch_max) + w
+    ring = 1
+    while ring < min(w, frames):
+        ring <<= 1
+    plan = {"stager_cpu": cpus[0],
+            "publish_cpu": cpus[1] if len(cpus) >= 2 else None,
+            "copy_cpu": cpus[2] if (not zero_copy and len(cpus) >= 3) else None}
+    plan["spinning_threads"] = 1 + (plan["publish_cpu"] is not None) + (plan["copy_cpu"] is not None)
+    plan["pinned_bytes"] = frames * FRAME_SZ + ring * RING_ENTRY_BYTES + 4096
+    plan["window"] = w
+    return plan
+
+
+def node_plan(numa_of_rank, node_cpus, batch_max, zero_copy=True, cpu_quota=None):
+    """The N-tile node (one tile per GPU, the reference's scaling unit,
+    fd_frank_init:67-80, fd_frank_main.c:118-143): each rank gets a disjoint
+    slice of its GPU's NUMA node's CPUs (ranks sharing a node split it,
+    peer_slot / cpu_slice), capped so that all ranks together fit the
+    process group's CPU quota (cgroup cpu.max, e.g. 16 on a one-GPU box's
+    share), and a tile_budget on that slice.  Returns one plan per rank plus
+    the node totals."""
+    world = len(numa_of_rank)
+    if cpu_quota:
+        per = max(1, int(cpu_quota) // world)
+    else:
+        per = None
+    plans = []
+    for r in range(world):
+        k, n = peer_slot(list(numa_of_rank), r)
+        sl = cpu_slice(node_cpus[numa_of_rank[r]], k, n)
+        if per is not None:
+            sl = sl[:per]
+        b = tile_budget(batch_max, sl, zero_copy=zero_copy)
+        b.update(rank=r, numa_node=numa_of_rank[r], cpus=sl)
+        plans.append(b)
+    tot = {"ranks": world, "spinning_threads": sum(p["spinning_threads"] for p in plans),
+           "pinned_bytes": sum(p["pinned_bytes"] for p in plans),
+           "cpus_used": len({c for p in plans for c in p["cpus"][:p["spinning_threads"]]})}
+    return plans, tot
+
+
+def node_sum(per_rank, cols):
+    """Rank 0's aggregation of the N-tile node rows (bench.py stream_node):
+    per_rank[r] = list of floats in `cols` order; the node value of a rate
+    column is the sum over ranks (every rank's tile ran at once, each on its
+    own GPU, no data exchanged), latency columns stay per rank."""
+    out = {c: sum(r[i] for r in per_rank) for i, c in enumerate(cols) if c.endswith("per_s")}
+    out["per_rank"] = [dict(zip(cols, r)) for r in per_rank]
+    return out

@@ -118,3 +118,80 @@ def test_peer_slot_and_cpu_slice():
     assert cpu_slice(range(10), 2, 3) == [6, 7, 8]
     with pytest.raises(ValueError):
         cpu_slice(range(10), 3, 3)
+
+
+def _node_worker(rank, world, port, q):
+    """One rank of an 8-tile node rehearsal on CPU: its config-4 shard, its
+    CPU slice and host budget from the node plan, and the node-sum
+    aggregation bench.py's stream_node performs (gloo, control plane only)."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from firedancer_amd.shard import node_plan, node_sum, shard_range
+    numa = [r // 4 for r in range(world)]                      # two NUMA nodes, four GPUs each
+    node_cpus = {0: list(range(0, 64)), 1: list(range(64, 128))}
+    plans, tot = node_plan(numa, node_cpus, 16384, zero_copy=True, cpu_quota=16)
+    mine = plans[rank]
+    lo, hi = shard_range(1 << 24, rank, world)
+    rate = 1e6 * (rank + 1)                                    # a stand-in for the rank's measured tile rate
+    cols = ["saturated_frags_per_s", "p50_us", "cpus"]
+    t = torch.zeros(world * len(cols), dtype=torch.float64)
+    t[rank * len(cols):(rank + 1) * len(cols)] = torch.tensor([rate, 1300.0 + rank, float(len(mine["cpus"]))],
+                                                              dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    agg = node_sum(t.view(world, len(cols)).tolist(), cols)
+    got = [None] * world
+    dist.all_gather_object(got, {"rank": rank, "lo": lo, "hi": hi, "cpus": mine["cpus"],
+                                 "threads": mine["spinning_threads"], "pinned": mine["pinned_bytes"],
+                                 "publish_cpu": mine["publish_cpu"], "copy_cpu": mine["copy_cpu"]})
+    if rank == 0:
+        q.put((got, agg, tot))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_eight_rank_node_plan_and_node_sum():
+    """gloo world_size 8 (CPU; the 8-GPU node is unmeasured on hardware): the
+    ranks' config-4 shards partition 2^24 signatures, each rank's tile gets a
+    disjoint CPU slice on its own NUMA node within a 16-CPU quota (2 CPUs:
+    stager + publisher, zero copy), eight tiles pin ~3.3 GB of host memory,
+    and rank 0's node sum is the sum of the ranks' rates."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 8
+    procs = [ctx.Process(target=_node_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, agg, tot = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got = sorted(got, key=lambda x: x["rank"])
+    assert got[0]["lo"] == 0 and got[-1]["hi"] == 1 << 24
+    assert all(a["hi"] == b["lo"] for a, b in zip(got, got[1:]))
+    flat = [c for g in got for c in g["cpus"]]
+    assert len(flat) == len(set(flat)) == 16                    # disjoint, and the quota holds
+    for g in got:
+        node = g["rank"] // 4
+        assert all(64 * node <= c < 64 * (node + 1) for c in g["cpus"])   # on the GPU's NUMA node
+        assert g["threads"] == 2 and g["publish_cpu"] == g["cpus"][1] and g["copy_cpu"] is None
+    assert tot["spinning_threads"] == 16 and tot["cpus_used"] == 16
+    assert 3.0e9 < tot["pinned_bytes"] < 3.6e9
+    assert agg["saturated_frags_per_s"] == sum(1e6 * (r + 1) for r in range(world))
+    assert [round(r["p50_us"]) for r in agg["per_rank"]] == [1300 + r for r in range(world)]
+
+
+def test_tile_budget_scarce_cpus():
+    """One CPU: the publisher runs inline on the stager; copy mode gets its
+    helper only from three CPUs."""
+    from firedancer_amd.shard import tile_budget
+    b = tile_budget(4096, [5])
+    assert b["spinning_threads"] == 1 and b["publish_cpu"] is None
+    b = tile_budget(4096, [5, 6, 7], zero_copy=False)
+    assert b["spinning_threads"] == 3 and b["copy_cpu"] == 7
+    b = tile_budget(1024, [5, 6], window=1 << 15)
+    assert b["window"] == 1 << 15 and b["pinned_bytes"] < 60e6
