@@ -88,7 +88,9 @@ def parse():
     ap.add_argument("--no-stream", action="store_true", help="skip the streaming-tile sweep (config 5)")
     ap.add_argument("--workload", choices=("sigs", "txn"), default="sigs",
                     help="sigs: configs[1] (default bench line); txn: configs[3] multi-signer transactions")
-    ap.add_argument("--stream-frags", type=int, default=1 << 22, help="frags per saturated streaming-tile run")
+    ap.add_argument("--stream-frags", type=int, default=1 << 23,
+                    help="frags per saturated streaming-tile run (2^23: ~150 ms at saturation, so the run's ramp "
+                         "and drain -- ~5 ms in all -- weigh ~3 %% of the whole-run rate)")
     ap.add_argument("--paced-seconds", type=float, default=0.5,
                     help="length of a paced streaming-tile run (latency over its steady state: after its first 20 ms)")
     ap.add_argument("--txn-full-check", action="store_true",
