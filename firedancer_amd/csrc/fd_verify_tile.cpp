@@ -1166,7 +1166,13 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     if( staged != handed ) {
       while( cdone != t->desc_seq && t->desc_end[cdone & mask] <= pubd ) cdone++;
       ulong const waited = (ulong)(uint)((uint)t3 - t->ppend[handed & mask].t_stage);
-      ulong const upto_sl = fd_verify_amd_tile_cut( &cc, staged_sl, handed_sl, t->desc_seq - cdone, thr, waited, full || done_in );
+      /* a full window (or no free frame) flushes only when nothing handed
+         over is still unpublished: otherwise the chunks in flight free room,
+         and flushing each pass's few freed frags cut the saturated stream
+         into part-filled chunks (47 frags per 64-lane chunk at 16384 zero
+         copy, profiles/r05_tile_cut_full_ab.txt) */
+      bool const flush = done_in || (full && handed == pubd);
+      ulong const upto_sl = fd_verify_amd_tile_cut( &cc, staged_sl, handed_sl, t->desc_seq - cdone, thr, waited, flush );
       /* whole entries up to that slot count (PUB_SIG_MSG: one slot per entry) */
       ulong upto = handed;
       if( upto_sl == staged_sl ) upto = staged;

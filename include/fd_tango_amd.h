@@ -337,8 +337,9 @@ fd_verify_amd_tile_set_verdict_log( fd_verify_amd_tile_t * tile, schar * log, ul
    Whole chunks go at once; a partial latency chunk once waited_ns (its
    oldest frag's wait) >= lat_fill_ns or while chunks_in_flight <
    lat_free_chunks; a partial throughput chunk once waited_ns >=
-   chunk_wait_ns; everything at batch_max staged, on flush (window or
-   frames ran out, end of input) or waited_ns >= batch_wait_ns != 0. */
+   chunk_wait_ns; everything at batch_max staged, on flush (end of input,
+   or the window / frames ran out while nothing handed over is still
+   unpublished) or waited_ns >= batch_wait_ns != 0. */
 ulong
 fd_verify_amd_tile_cut( fd_verify_amd_tile_cfg_t const * cfg, ulong staged, ulong handed, ulong chunks_in_flight,
                         int thr, ulong waited_ns, int flush );
