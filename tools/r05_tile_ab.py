@@ -5,7 +5,8 @@ published frag checked against the batch engine's verdicts and the SHA-512
 tags.  Reports whole-run and steady rates and the mean fill of throughput
 chunks (frags per 64-lane chunk).
 usage: python tools/r05_tile_ab.py OUT.jsonl LIB[,LIB...] [rounds] [frags] [bmax,...]
-       LIB "" = the product library."""
+       LIB "" = the product library; NAME=VALUE = the product library with that
+       environment variable set (e.g. FD_AMD_TILE_POOL=1)."""
 import hashlib
 import json
 import os
@@ -18,7 +19,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def child(lib, frags, bmaxes, out):
-    if lib:
+    if "=" in lib:      # NAME=VALUE: the product library with that environment variable set
+        k, v = lib.split("=", 1)
+        os.environ[k] = v
+    elif lib:
         os.environ["FD_AMD_LIB"] = os.path.join(ROOT, lib)
     sys.path.insert(0, ROOT)
     from firedancer_amd import ed25519, tango, workload
