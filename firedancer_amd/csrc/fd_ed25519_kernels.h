@@ -97,7 +97,7 @@ typedef struct {
   fd_amd_tile_mirror_t mw[FD_AMD_TILE_MIRRORS];     /* per XCD: descriptor head | heartbeat << 48 | err << 62 | stop << 63 */
   uint64_t             done;    uint64_t pad1[7];   /* chunks finished (one atomic add per chunk; the scout mirrors it) */
   uint64_t             stat[4];                     /* chunks in latency mode, in throughput mode; frags in each */
-  uint64_t             prof[8];                     /* diagnostics build (FD_AMD_DIAG, args.prof): summed ticks gather, decomp, DSM, results, wait, fence, prep */
+  uint64_t             prof[16];                    /* diagnostics build (FD_AMD_DIAG, args.prof): summed ticks gather, decomp, DSM, results, wait, fence, prep; k_tile_pool: its tallies */
 } fd_amd_tile_dctl_t;
 typedef struct {
   fd_amd_tile_hctl_t *       hctl;     /* device address of the mapped control words */

@@ -2046,6 +2046,50 @@ tile_txn_layout( u32 l, u32 k, u32 e_sz, u32 e_k, u8 const * __restrict__ mir, u
   return n;
 }
 
+/* Copy a chunk's k frags in: frame q (16-B word w of it) by lane 16 (q % 4)
+   + (w % 16) of round q / 4; four rounds (16 frames) have every load
+   issued before any store, so a 64-frag chunk waits four round trips to
+   the frames' memory (host memory over PCIe in zero-copy mode), not
+   sixteen (profiles/r05_tile_pool_dev.txt: 365 -> ~100 us per chunk under
+   load).  Frames are <= 1328 B = 83 words, chunk-aligned (every 16-B word
+   whole), and hold up to six words per lane per round.  Zero copy: every
+   word also goes out to the frag's output frame; PUB_SIG_MSG: pub and sig
+   to their planes. */
+__device__ __forceinline__ void
+tile_gather( fd_amd_tile_args_t const & A, u32 k, u32 l, u32 e_src, u32 e_out, u32 e_sz, u8 * __restrict__ mir,
+             u8 * __restrict__ pub, u8 * __restrict__ sig, bool txn ) {
+  u32 const g = l >> 4, j = l & 15u;
+  for( u32 q0 = 0; q0 < k; q0 += 16u ) {
+    uint4 v[4][6];
+    u32 nv[4];
+    _Pragma("unroll") for( int h=0; h<4; h++ ) {
+      u32 const q = q0 + 4u*(u32)h + g;
+      u32 const src = (u32)__shfl( (int)e_src, (int)(q & 63u) );
+      u32 const fs  = (u32)__shfl( (int)e_sz,  (int)(q & 63u) );
+      nv[h] = q < k ? (fs + 15u) >> 4 : 0u;
+      uint4 const * s = (uint4 const *)(A.src + ((size_t)src << 6));
+      _Pragma("unroll") for( int r=0; r<6; r++ ) {
+        u32 w = j + 16u*(u32)r;
+        v[h][r] = w < nv[h] ? s[w] : make_uint4( 0u, 0u, 0u, 0u );
+      }
+    }
+    _Pragma("unroll") for( int h=0; h<4; h++ ) {
+      u32 const q = q0 + 4u*(u32)h + g;
+      u32 const oc = (u32)__shfl( (int)e_out, (int)(q & 63u) );
+      uint4 * m = (uint4 *)(mir + (size_t)(q & 63u) * TILE_FRAME);
+      uint4 * o = A.out ? (uint4 *)(A.out + ((size_t)oc << 6)) : (uint4 *)0;
+      _Pragma("unroll") for( int r=0; r<6; r++ ) {
+        u32 w = j + 16u*(u32)r;
+        if( w < nv[h] ) { m[w] = v[h][r]; if( o ) o[w] = v[h][r]; }
+      }
+      if( q < k && !txn ) {
+        if( j < 2u )      ((uint4 *)(pub + 32u*q))[j]      = v[h][0];
+        else if( j < 6u ) ((uint4 *)(sig + 64u*q))[j - 2u] = v[h][0];
+      }
+    }
+  }
+}
+
 /* Verify ring entries [c0, c0 + k) (k <= 64) on this wave, claimed at
    s_memrealtime tc.  PUB_SIG_MSG: entry q is signature slot q.  TXN
    (A.txn): entry q is a wire transaction whose slots tile_txn_layout lays
@@ -2078,36 +2122,9 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __rest
     u64 w0 = ld_sys64( ep ), w1 = ld_sys64( ep + 1 );
     e_src = (u32)w0; e_out = (u32)(w0 >> 32); e_sz = (u32)w1; e_k = (u32)(w1 >> 32);
   }
-  /* 2. copy the frags in: four frags per round, 16 lanes each, up to six
-        16-B words per lane issued before any is stored (frames <= 1328 B =
-        83 words; frames are chunk-aligned, so every 16-B word is whole) */
-  {
-    u32 const g = l >> 4, j = l & 15u;
-    for( u32 q0 = 0; q0 < k; q0 += 4u ) {
-      u32 const q = q0 + g;
-      u32 const src = (u32)__shfl( (int)e_src, (int)(q & 63u) );
-      u32 const oc  = (u32)__shfl( (int)e_out, (int)(q & 63u) );
-      u32 const fs  = (u32)__shfl( (int)e_sz,  (int)(q & 63u) );
-      u32 const nv  = q < k ? (fs + 15u) >> 4 : 0u;
-      uint4 const * s = (uint4 const *)(A.src + ((size_t)src << 6));
-      uint4 v[6];
-      _Pragma("unroll") for( int r=0; r<6; r++ ) {
-        u32 w = j + 16u*(u32)r;
-        v[r] = w < nv ? s[w] : make_uint4( 0u, 0u, 0u, 0u );
-      }
-      uint4 * m = (uint4 *)(mir + (size_t)(q & 63u) * TILE_FRAME);
-      uint4 * o = A.out ? (uint4 *)(A.out + ((size_t)oc << 6)) : (uint4 *)0;
-      _Pragma("unroll") for( int r=0; r<6; r++ ) {
-        u32 w = j + 16u*(u32)r;
-        if( w < nv ) { m[w] = v[r]; if( o ) o[w] = v[r]; }
-      }
-      if( q < k && !txn ) {
-        if( j < 2u )      ((uint4 *)(pub + 32u*q))[j]      = v[0];
-        else if( j < 6u ) ((uint4 *)(sig + 64u*q))[j - 2u] = v[0];
-      }
-    }
-    if( l < k && !txn ) { off[l] = l * TILE_FRAME + 96u; sz[l] = e_sz - 96u; }
-  }
+  /* 2. copy the frags in (tile_gather) */
+  tile_gather( A, k, l, e_src, e_out, e_sz, mir, pub, sig, txn );
+  if( l < k && !txn ) { off[l] = l * TILE_FRAME + 96u; sz[l] = e_sz - 96u; }
   __syncthreads();
   /* TXN: parse and lay the chunk's signature slots out (n of them) */
   i8 * skp = (i8 *)(scr + S.skp);
@@ -2202,12 +2219,15 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __rest
 #define TP_CLAIM 16u        /* most queue positions a refill claims */
 #endif
 #ifndef TP_TARGET
-#define TP_TARGET 4096u     /* per XCD: ready items + 64 x fronts under way below which a wave takes a chunk */
+#define TP_TARGET 8192u     /* per XCD: ready items + 64 x fronts under way below which a wave takes a chunk */
 #endif
 static_assert( TP_P >= 64 && TP_P <= 128, "pool: each lane owns slots l and l + 64" );
 enum { OP_F = 5 };          /* pool class: op stream done, the compare is next */
 
 struct tp_lay_t { size_t bt, qctl, items, reg, ws, total; };
+/* a region's workspace: the N = 64 layout (the chunk mode's per-wave one),
+   one per region, so a front touches the same few pages as a chunk */
+constexpr size_t TP_RS = ws_al( ws_layout_const( 64 ).total );
 __host__ __device__ constexpr tp_lay_t tp_layout( void ) {
   tp_lay_t T = {};
   size_t o = 0;
@@ -2215,7 +2235,7 @@ __host__ __device__ constexpr tp_lay_t tp_layout( void ) {
   T.qctl  = o; o = ws_al( o + FD_AMD_TP_X * sizeof(fd_amd_tp_qctl_t) );
   T.items = o; o = ws_al( o + (size_t)FD_AMD_TP_X * TP_Q * 16UL );              /* 16-B ready items */
   T.reg   = o; o = ws_al( o + (size_t)TP_C * sizeof(fd_amd_tp_region_t) );
-  T.ws    = o; o = ws_al( o + ws_layout_const( 64UL * TP_C ).total );
+  T.ws    = o; o = ws_al( o + (size_t)TP_C * ws_al( ws_layout_const( 64 ).total ) );   /* region r: an N = 64 workspace */
   T.total = o;
   return T;
 }
@@ -2311,9 +2331,14 @@ tp_res_word( fd_amd_tile_args_t const & A, u64 j, i8 v ) {
    still has signatures in pools */
 __device__ __forceinline__ bool
 tp_front( fd_amd_tile_args_t const & A, u64 t, u64 c0, u32 k, u8 * __restrict__ scr, tile_scratch_t const & S,
-          u32 * __restrict__ lds, fd_amd_tp_qctl_t * __restrict__ Q, u8 * __restrict__ items, u64 tc ) {
+          u32 * __restrict__ lds, fd_amd_tp_qctl_t * __restrict__ Q, u8 * __restrict__ items, u64 tc, u64 * pt ) {
+  /* pt (A.prof, diagnostics build): ticks in gather [12], prep [13], decomp
+     [14], -A table and starts [15], header and early results [16], the
+     release [17], the items [18] */
+  u64 ts = A.prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
+# define TP_STAMP( k_ ) do { if( A.prof ) { u64 t_ = __builtin_amdgcn_s_memrealtime(); if( !threadIdx.x ) pt[k_] += t_ - ts; ts = t_; } } while(0)
   constexpr tp_lay_t    T = tp_layout();
-  constexpr ws_layout_t W = ws_layout_const( 64UL * TP_C );
+  constexpr ws_layout_t W = ws_layout_const( 64 );
   u32 const r = (u32)(t % TP_C);
   fd_amd_tp_region_t * R = (fd_amd_tp_region_t *)(A.pool + T.reg) + r;
   {
@@ -2328,7 +2353,7 @@ tp_front( fd_amd_tile_args_t const & A, u64 t, u64 c0, u32 k, u8 * __restrict__ 
   }
   u32 l = threadIdx.x;
   asm volatile( "" : "+v"(l) );
-  u8 * ws = A.pool + T.ws;
+  u8 * ws = A.pool + T.ws + (size_t)r * TP_RS;
   u8 * mir = scr + S.mir; u8 * pub = scr + S.pub; u8 * sig = scr + S.sig;
   u32 * off = (u32 *)(scr + S.off); u32 * sz = (u32 *)(scr + S.sz);
   i8 * err = R->err;
@@ -2341,60 +2366,38 @@ tp_front( fd_amd_tile_args_t const & A, u64 t, u64 c0, u32 k, u8 * __restrict__ 
     u64 w0 = ld_sys64( ep ), w1 = ld_sys64( ep + 1 );
     e_src = (u32)w0; e_out = (u32)(w0 >> 32); e_sz = (u32)w1; e_k = (u32)(w1 >> 32);
   }
-  {
-    u32 const g = l >> 4, j = l & 15u;
-    for( u32 q0 = 0; q0 < k; q0 += 4u ) {
-      u32 const q = q0 + g;
-      u32 const src = (u32)__shfl( (int)e_src, (int)(q & 63u) );
-      u32 const oc  = (u32)__shfl( (int)e_out, (int)(q & 63u) );
-      u32 const fs  = (u32)__shfl( (int)e_sz,  (int)(q & 63u) );
-      u32 const nv  = q < k ? (fs + 15u) >> 4 : 0u;
-      uint4 const * s = (uint4 const *)(A.src + ((size_t)src << 6));
-      uint4 v[6];
-      _Pragma("unroll") for( int rr=0; rr<6; rr++ ) {
-        u32 w = j + 16u*(u32)rr;
-        v[rr] = w < nv ? s[w] : make_uint4( 0u, 0u, 0u, 0u );
-      }
-      uint4 * m = (uint4 *)(mir + (size_t)(q & 63u) * TILE_FRAME);
-      uint4 * o = A.out ? (uint4 *)(A.out + ((size_t)oc << 6)) : (uint4 *)0;
-      _Pragma("unroll") for( int rr=0; rr<6; rr++ ) {
-        u32 w = j + 16u*(u32)rr;
-        if( w < nv ) { m[w] = v[rr]; if( o ) o[w] = v[rr]; }
-      }
-      if( q < k && !txn ) {
-        if( j < 2u )      ((uint4 *)(pub + 32u*q))[j]      = v[0];
-        else if( j < 6u ) ((uint4 *)(sig + 64u*q))[j - 2u] = v[0];
-      }
-    }
-    if( l < k && !txn ) { off[l] = l * TILE_FRAME + 96u; sz[l] = e_sz - 96u; }
-  }
+  tile_gather( A, k, l, e_src, e_out, e_sz, mir, pub, sig, txn );
+  if( l < k && !txn ) { off[l] = l * TILE_FRAME + 96u; sz[l] = e_sz - 96u; }
   __syncthreads();
   i8 * skp = (i8 *)(scr + S.skp);
   u32 * tx = (u32 *)(scr + S.tx);
   u32 const n = txn ? tile_txn_layout( l, k, e_sz, e_k, mir, pub, sig, off, sz, skp, tx, lds ) : k;
   if( txn ) __syncthreads();
+  TP_STAMP( 12 );
 
   /* 2. k_prep's and k_decomp's bodies into the region's workspace rows */
   u32 const wb = r * 64u;
-  prep_body( l, n, pub, sig, off, sz, mir, err, ws, W, txn ? (i8 const *)skp : (i8 const *)0, wb );
+  prep_body( l, n, pub, sig, off, sz, mir, err, ws, W, txn ? (i8 const *)skp : (i8 const *)0 );
   __syncthreads();
-  decomp_body( l, n, pub, sig, err, ws, W, true, wb );
-  if( n > 32u ) decomp_body( l + 64u, n, pub, sig, err, ws, W, true, wb );
+  TP_STAMP( 13 );
+  decomp_body( l, n, pub, sig, err, ws, W, true );
+  if( n > 32u ) decomp_body( l + 64u, n, pub, sig, err, ws, W, true );
   __syncthreads();
+  TP_STAMP( 14 );
 
   /* 3. the -A table and the op-stream start (k_ai) */
-  u32 const wi = wb + l;
+  u32 const wi = wb + l;                                /* the signature's index in the pool buffer */
   bool act = l < n && err[l] == 1;
-  if( act && (ws[W.ds + 2u*wi] | ws[W.ds + 2u*wi + 1u]) ) { err[l] = (i8)-2; act = false; }
-  tp_ai_table( act, ws, W, wi );
+  if( act && (ws[W.ds + 2u*l] | ws[W.ds + 2u*l + 1u]) ) { err[l] = (i8)-2; act = false; }
+  tp_ai_table( act, ws, W, l );
   u32 i1 = 0u, i2 = 0u, i3 = 0u;
   if( act ) {
-    int const p = ((int const *)(ws + W.top))[wi];
+    int const p = ((int const *)(ws + W.top))[l];
     u32 heads = 0xffffffffu, pz = 0u, op = (u32)OP_F;   /* no digit at all: R' is the identity */
     if( p >= 0 ) {
-      u32 const ne = ((u32 const *)(ws + W.evn))[wi];
+      u32 const ne = ((u32 const *)(ws + W.evn))[l];
       u32 const na = ne & 0xffu, nb = (ne >> 8) & 0xffu;
-      u16 const * ev = (u16 const *)(ws + W.dig) + (size_t)wi*128u;
+      u16 const * ev = (u16 const *)(ws + W.dig) + (size_t)l*128u;
       u32 const hA = na ? (u32)ev[na - 1u] : 0xffffu, hB = nb ? (u32)ev[64u + nb - 1u] : 0xffffu;
       heads = hA | (hB << 16); pz = ((u32)p & 0xffffu) | (na << 16) | (nb << 24); op = (u32)OP_D;
     }
@@ -2402,6 +2405,7 @@ tp_front( fd_amd_tile_args_t const & A, u64 t, u64 c0, u32 k, u8 * __restrict__ 
   }
   u64 const m = __builtin_amdgcn_ballot_w64( act );
   u32 const ni = (u32)__builtin_popcountll( m );
+  TP_STAMP( 15 );
 
   /* 4. the region's header; entries with nothing in a pool get their
         result now (tags here, words after the release) */
@@ -2410,7 +2414,7 @@ tp_front( fd_amd_tile_args_t const & A, u64 t, u64 c0, u32 k, u8 * __restrict__ 
   if( l < k ) {
     if( !txn ) {
       now = !((m >> l) & 1UL);
-      if( now ) { v = err[l]; tag = ((u64 const *)(ws + W.tag))[wi]; }
+      if( now ) { v = err[l]; tag = ((u64 const *)(ws + W.tag))[l]; }
     } else {
       u32 const w = tx[l], b = w & 0xffu, kk = (w >> 8) & 0xffu;
       R->tx[l] = w;
@@ -2421,7 +2425,7 @@ tp_front( fd_amd_tile_args_t const & A, u64 t, u64 c0, u32 k, u8 * __restrict__ 
       if( now ) {
         if( !(w >> 31) ) v = (i8)TXN_ERR_PARSE;
         else for( u32 i=0u; i<kk; i++ ) { i8 const e = err[b + i]; if( e ) { v = e; break; } }
-        if( kk ) tag = ((u64 const *)(ws + W.tag))[wb + b];
+        if( kk ) tag = ((u64 const *)(ws + W.tag))[b];
       }
     }
     if( now ) tp_res_tag( A, c0 + l, tag, (u32)tc );
@@ -2429,8 +2433,10 @@ tp_front( fd_amd_tile_args_t const & A, u64 t, u64 c0, u32 k, u8 * __restrict__ 
   if( txn && l < n ) R->own[l] = (u8)lds[l];              /* tile_txn_layout's slot -> entry */
   if( l == 0u ) st_ag32( &R->live, ni );
   asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
+  TP_STAMP( 16 );
   __builtin_amdgcn_fence( __ATOMIC_RELEASE, "" );         /* system: the region's lines, and the zero-copy frames */
   asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
+  TP_STAMP( 17 );
   if( now ) tp_res_word( A, c0 + l, v );
 
   /* 5. the ready items */
@@ -2440,6 +2446,8 @@ tp_front( fd_amd_tile_args_t const & A, u64 t, u64 c0, u32 k, u8 * __restrict__ 
     pos = rfl64( pos ) + lane_rank( m );
     if( act ) *(uint4 *)(items + (pos % TP_Q) * 16UL) = make_uint4( (u32)(pos + 1UL), i1, i2, i3 | (tp_lap( pos ) << 30) );
   }
+  TP_STAMP( 18 );
+# undef TP_STAMP
   return true;
 }
 
@@ -2459,7 +2467,7 @@ struct tp_lds_t {
 __device__ __forceinline__ void
 tp_fin_step( fd_amd_tile_args_t const & A, tp_buf_t const & B, tp_lds_t const & P, u64 & mF0, u64 & mF1 ) {
   constexpr tp_lay_t    T = tp_layout();
-  constexpr ws_layout_t W = ws_layout_const( 64UL * TP_C );
+  constexpr ws_layout_t W = ws_layout_const( 64 );
   u32 const l = threadIdx.x;
   u32 const nF0 = (u32)__builtin_popcountll( mF0 );
   u32 const rk0 = lane_rank( mF0 ), rk1 = nF0 + lane_rank( mF1 );
@@ -2478,10 +2486,11 @@ tp_fin_step( fd_amd_tile_args_t const & A, tp_buf_t const & B, tp_lds_t const & 
   fe uZ, uY, uX;
   fe_mul_fold2w( uZ, t.Z, t.T, uY, t.Z, t.Y );
   uX = fe_mul_fold1( t.X, t.T );
+  u32 const wsr = (u32)(T.ws + (size_t)(wi >> 6) * TP_RS);   /* the signature's region workspace */
   fe RX, RY;
   _Pragma("unroll") for( int k=0; k<10; k++ ) {
-    RX.v[k] = (i32)B.ld4( (u32)(T.ws + W.R + 4UL*((size_t)k*W.N + wi)) );
-    RY.v[k] = (i32)B.ld4( (u32)(T.ws + W.R + 4UL*((size_t)(10+k)*W.N + wi)) );
+    RX.v[k] = (i32)B.ld4( wsr + (u32)(W.R + 4UL*((size_t)k*64u + (wi & 63u))) );
+    RY.v[k] = (i32)B.ld4( wsr + (u32)(W.R + 4UL*((size_t)(10+k)*64u + (wi & 63u))) );
   }
   fe xZ, yZ;
   fe_mul_fold2w( xZ, uZ, RX, yZ, uZ, RY );
@@ -2499,7 +2508,7 @@ tp_fin_step( fd_amd_tile_args_t const & A, tp_buf_t const & B, tp_lds_t const & 
   if( !A.txn ) {
     if( live ) {
       jq = c0 + sl; vq = v; last = true;
-      tp_res_tag( A, jq, B.ld8( (u32)(T.ws + W.tag + 8UL*wi) ), tcr );
+      tp_res_tag( A, jq, B.ld8( wsr + (u32)(W.tag + 8UL*sl) ), tcr );
     }
   } else if( live ) {
     /* this slot's verdict, then the entry's count; the last one reduces */
@@ -2516,7 +2525,7 @@ tp_fin_step( fd_amd_tile_args_t const & A, tp_buf_t const & B, tp_lds_t const & 
         i8 const e = (i8)(B.ld4( rb + (u32)offsetof( fd_amd_tp_region_t, err ) + (si & ~3u) ) >> (8u*(si & 3u)));
         if( e ) { vq = e; break; }
       }
-      tp_res_tag( A, jq, kk ? B.ld8( (u32)(T.ws + W.tag + 8UL*(r*64u + b)) ) : 0UL, tcr );
+      tp_res_tag( A, jq, kk ? B.ld8( wsr + (u32)(W.tag + 8UL*b) ) : 0UL, tcr );
     }
   }
   asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
@@ -2537,7 +2546,7 @@ __device__ __forceinline__ void
 tp_run( fd_amd_tile_args_t const & A, u8 * __restrict__ scr, tile_scratch_t const & S, ws_layout_t L64,
         u64 const * mw, u32 xcc, tp_lds_t const & P, u64 (* __restrict__ evl)[33], u64 * s_tally, bool prof ) {
   constexpr tp_lay_t    T = tp_layout();
-  constexpr ws_layout_t W = ws_layout_const( 64UL * TP_C );
+  constexpr ws_layout_t W = ws_layout_const( 64 );
   fd_amd_tile_dctl_t * D = A.dctl;
   fd_amd_tp_qctl_t * Q = (fd_amd_tp_qctl_t *)(A.pool + T.qctl) + xcc;
   u8 * items = A.pool + T.items + (size_t)xcc * TP_Q * 16UL;
@@ -2618,7 +2627,7 @@ tp_run( fd_amd_tile_args_t const & A, u8 * __restrict__ scr, tile_scratch_t cons
         if( e8 ) tile_chunk( A, c, take, true, scr, L64, S, bi, evl, s_tally, tc );
         else {
           if( l == 0u ) __hip_atomic_fetch_add( &Q->fronts, 1UL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-          ok = tp_front( A, tk, c, take, scr, S, (u32 *)&evl[0][0], Q, items, tc );
+          ok = tp_front( A, tk, c, take, scr, S, (u32 *)&evl[0][0], Q, items, tc, s_tally );
           if( l == 0u ) __hip_atomic_fetch_sub( &Q->fronts, 1UL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
           if( prof && !ok && l == 0u ) s_tally[7] += 1UL;
         }
@@ -2775,7 +2784,8 @@ tp_run( fd_amd_tile_args_t const & A, u8 * __restrict__ scr, tile_scratch_t cons
     u32 ja = (m.z >> 16) & 0xffu, jb = m.z >> 24;
     u32 const pidx = (op == OP_AA && ja >= 2u) ? ja - 2u : (op == OP_AB && jb >= 2u) ? 64u + jb - 2u : 0u;
     bool const pop = (op == OP_AA && ja >= 2u) || (op == OP_AB && jb >= 2u);
-    u32 const nh = B.ld4( pop ? (u32)(T.ws + W.dig + 256UL*si + 4UL*(pidx >> 1)) : (u32)T.bt );
+    u32 const wsr = (u32)(T.ws + (size_t)(si >> 6) * TP_RS), sl = si & 63u;   /* the slot's region workspace */
+    u32 const nh = B.ld4( pop ? wsr + (u32)(W.dig + 256UL*sl + 4UL*(pidx >> 1)) : (u32)T.bt );
     p1p1 t;
     pool_load_ts( t, &P.t[0][s], TP_P );
 
@@ -2784,7 +2794,7 @@ tp_run( fd_amd_tile_args_t const & A, u8 * __restrict__ scr, tile_scratch_t cons
       int dg = (op == OP_AA) ? (int)(i8)(hA >> 8) : (int)(i8)(hB >> 8);
       bool neg = isadd && dg < 0;
       int e = isadd ? ((dg < 0 ? -dg : dg) >> 1) & 7 : 0;
-      u32 const qb = (op == OP_AA) ? (u32)(T.ws + W.Ai + 4UL*((size_t)si*384u + (u32)e*48u)) : (u32)(T.bt + 4UL*(u32)e*48u);
+      u32 const qb = (op == OP_AA) ? wsr + (u32)(W.Ai + 4UL*((size_t)sl*384u + (u32)e*48u)) : (u32)(T.bt + 4UL*(u32)e*48u);
       int const rowM = neg ? 2 : 1, rowP = neg ? 1 : 2;
       fe q[4];
 #     define Q_ROW( R_, C_ ) do {                                                     \
@@ -2975,7 +2985,7 @@ k_tile_pool( fd_amd_tile_args_t A ) {
   constexpr tile_scratch_t S = tile_scratch_layout();
   constexpr u32 O_M = TP_P*10u*16u, O_LIST = O_M + TP_P*16u, O_EVL = O_LIST + 64u*4u, O_PS = O_EVL + 8u*33u*8u, O_END = O_PS + 12u*8u;
   __shared__ __attribute__((aligned(16))) u64 s_raw[O_END / 8u];
-  __shared__ u64 s_tally[12];
+  __shared__ u64 s_tally[20];
   fd_amd_tile_dctl_t * D = A.dctl;
   u32 const l = threadIdx.x;
   if( blockIdx.x == 0u ) {
@@ -2985,7 +2995,7 @@ k_tile_pool( fd_amd_tile_args_t A ) {
   u32 const xcc = __builtin_amdgcn_s_getreg( 20 | (0 << 6) | (3 << 11) ) % FD_AMD_TILE_MIRRORS;
   u64 const * mw = &D->mw[xcc].w;
   u8 * scr = A.scratch + (size_t)blockIdx.x * S.total;
-  if( l < 12u ) s_tally[l] = 0UL;
+  if( l < 20u ) s_tally[l] = 0UL;
   tp_lds_t P;
   P.t = (int4 (*)[TP_P])s_raw;
   P.m = (uint4 *)(s_raw + O_M/8u);
@@ -2999,7 +3009,10 @@ k_tile_pool( fd_amd_tile_args_t A ) {
   tp_run( A, scr, S, L, mw, xcc, P, (u64 (*)[33])(s_raw + O_EVL/8u), s_tally, prof );
   if( l == 0u ) {
     _Pragma("unroll") for( int q=0; q<4; q++ ) atomicAdd( (unsigned long long *)&D->stat[q], (unsigned long long)s_tally[8 + q] );
-    if( prof ) { _Pragma("unroll") for( int q=0; q<8; q++ ) atomicAdd( (unsigned long long *)&D->prof[q], (unsigned long long)s_tally[q] ); }
+    if( prof ) {
+      _Pragma("unroll") for( int q=0; q<8; q++ ) atomicAdd( (unsigned long long *)&D->prof[q], (unsigned long long)s_tally[q] );
+      _Pragma("unroll") for( int q=0; q<8; q++ ) atomicAdd( (unsigned long long *)&D->prof[8 + q], (unsigned long long)s_tally[12 + q] );
+    }
   }
 }
 

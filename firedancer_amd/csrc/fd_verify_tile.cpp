@@ -541,8 +541,7 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
       hipMalloc( (void **)&t->dctl, sizeof(fd_amd_tile_dctl_t) ) != hipSuccess ||
       hipMalloc( (void **)&t->scratch, waves * fd_amd_tile_scratch_stride() ) != hipSuccess ||
       ( t->pool_on && ( hipMalloc( (void **)&t->pool, fd_amd_tp_pool_size() ) != hipSuccess ||
-                        fd_amd_tp_pool_init( t->pool, t->pst ) != 0 ||
-                        hipStreamSynchronize( t->pst ) != hipSuccess ) ) ) {
+                        fd_amd_tp_pool_init( t->pool, t->pst ) != 0 ) ) ) {   /* stream order: before the first run's kernel */
     (void)hipGetLastError();
     tile_persist_free( t );
     return FD_ED25519_AMD_ERR_DEVICE;
@@ -1284,10 +1283,12 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
                        hipStreamSynchronize( t->pst ) != hipSuccess ) ) rc = FD_ED25519_AMD_ERR_DEVICE;
 #ifdef FD_AMD_DIAG
   if( A.prof && !t->pending ) {   /* diagnostics build: the kernel's per-wave tallies, summed */
-    ulong pf[8] = { 0 };
-    if( hipMemcpy( pf, t->dctl->prof, sizeof pf, hipMemcpyDeviceToHost ) == hipSuccess )
-      fprintf( stderr, "tile_prof %s %lu %lu %lu %lu %lu %lu %lu %lu\n", t->pool ? "pool" : "chunk",
-               pf[0], pf[1], pf[2], pf[3], pf[4], pf[5], pf[6], pf[7] );
+    ulong pf[16] = { 0 };
+    if( hipMemcpy( pf, t->dctl->prof, sizeof pf, hipMemcpyDeviceToHost ) == hipSuccess ) {
+      fprintf( stderr, "tile_prof %s", t->pool ? "pool" : "chunk" );
+      for( int q=0; q<16; q++ ) fprintf( stderr, " %lu", pf[q] );
+      fprintf( stderr, "\n" );
+    }
   }
 #endif
   if( __atomic_load_n( &H->kerr, __ATOMIC_ACQUIRE ) ) {
