@@ -97,7 +97,7 @@ typedef struct {
   fd_amd_tile_mirror_t mw[FD_AMD_TILE_MIRRORS];     /* per XCD: descriptor head | heartbeat << 48 | err << 62 | stop << 63 */
   uint64_t             done;    uint64_t pad1[7];   /* chunks finished (one atomic add per chunk; the scout mirrors it) */
   uint64_t             stat[4];                     /* chunks in latency mode, in throughput mode; frags in each */
-  uint64_t             prof[16];                    /* diagnostics build (FD_AMD_DIAG, args.prof): summed ticks gather, decomp, DSM, results, wait, fence, prep; k_tile_pool: its tallies */
+  uint64_t             prof[8];                     /* diagnostics build (FD_AMD_DIAG, args.prof): summed ticks gather, decomp, DSM, results, wait, fence, prep */
 } fd_amd_tile_dctl_t;
 typedef struct {
   fd_amd_tile_hctl_t *       hctl;     /* device address of the mapped control words */
@@ -115,49 +115,7 @@ typedef struct {
   uint64_t                   watchdog; /* s_memrealtime ticks (100 MHz) without a host heartbeat before the kernel gives up */
   uint32_t                   prof;     /* diagnostics build only: sum per-phase time stamps into dctl->prof */
   uint32_t                   txn;      /* TXN framing: entries are wire transactions, results per transaction */
-  uint8_t *                  pool;     /* pooled throughput mode (NULL = off): the fd_amd_tp_* buffer below */
 } fd_amd_tile_args_t;
-
-/* Pooled throughput mode of k_tile_persist.  A throughput chunk is split
-   in two: its FRONT (gather, SHA-512, decompression, the -A table) runs on
-   the wave that took the chunk and lays the chunk's signatures out in one
-   of FD_AMD_TP_C REGIONS of a large workspace; the signatures then enter a
-   ready queue of the wave's XCD, and every wave of that XCD keeps a POOL of
-   FD_AMD_TP_P signatures in LDS that it refills one signature at a time from
-   the queue and steps like k_dsmp (pure doubling steps with squares when 64
-   pool slots want a doubling, else k_dsm's uniform step).  A finished
-   signature's limb compare and result words come from the pool's wave.
-   Hand-offs stay inside one XCD (one L2): the front's plain stores reach
-   the L2, a release makes the region's lines clean, and every load of
-   handed-off bytes bypasses the CU's L1 (sc1). */
-#define FD_AMD_TP_P  (96u)                  /* pool slots per wave */
-#define FD_AMD_TP_C  (8192u)                /* regions (throughput chunks whose signatures are in flight) */
-#define FD_AMD_TP_Q  (64u * FD_AMD_TP_C)    /* ready-queue entries per XCD */
-#define FD_AMD_TP_X  (8u)                   /* XCDs (queues) */
-/* per XCD: items [head, res) are published or being written; fronts: chunks
-   being laid out on this XCD (each will add <= 64 items) */
-typedef struct { uint64_t res; uint64_t pad0[7]; uint64_t head; uint64_t pad1[7]; uint64_t fronts; uint64_t pad2[7]; } fd_amd_tp_qctl_t;
-/* a region: one throughput chunk's signatures (slot s at workspace index
-   64 r + s) and what their results need */
-typedef struct {
-  uint64_t c0;          /* first ring index */
-  uint32_t k, n;        /* ring entries, signature slots */
-  uint32_t tc;          /* low 32 bits of the claim tick (res_time) */
-  uint32_t live;        /* signatures still in pools (agent atomics); 0 = the region is free */
-  uint32_t pad[2];
-  uint32_t tx[64];      /* TXN: entry q: first slot | slots << 8 | parsed << 31 */
-  uint32_t ecnt[64];    /* TXN: entry q: its signatures still in pools (agent atomics) */
-  uint8_t  own[64];     /* TXN: slot -> entry */
-  int8_t   err[64];     /* slot verdicts */
-} fd_amd_tp_region_t;
-/* the pool buffer (device memory): the base-point table, then the words to
-   zero before every launch (queue control, queue items, regions), then the
-   workspace */
-size_t fd_amd_tp_pool_size( void );
-size_t fd_amd_tp_zero_offset( void );
-size_t fd_amd_tp_zero_size( void );
-/* writes the base-point table into a new pool buffer (once) */
-int fd_amd_tp_pool_init( void * d_pool, hipStream_t stream );
 size_t fd_amd_tile_scratch_stride( void );
 /* waves: grid size (wave 0 is the scout that mirrors the host words) */
 int fd_amd_launch_tile_persist( fd_amd_tile_args_t const * a, uint32_t waves, hipStream_t stream );   /* 0, -1 (waves), or a hipError_t */

@@ -129,15 +129,12 @@ __device__ __forceinline__ void
 prep_body( u32 i, u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
            u32 const * __restrict__ msg_off, u32 const * __restrict__ msg_sz,
            u8 const * __restrict__ blob, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L,
-           i8 const * __restrict__ skip, u32 wbase = 0u ) {
-  /* i indexes the inputs and err, wi = i + wbase the workspace planes (the
-     streaming tile's pooled mode lays chunks out in one large workspace) */
+           i8 const * __restrict__ skip ) {
   if( i >= n ) return;
-  u32 const wi = i + wbase;
   if( skip && skip[i] ) {   /* slot of a transaction that failed to parse (fd_txn_kernels.hip) */
-    ((int *)(ws + L.top))[wi] = -1;
-    ((u32 *)(ws + L.evn))[wi] = 0u;
-    ((u64 *)(ws + L.tag))[wi] = 0UL;
+    ((int *)(ws + L.top))[i] = -1;
+    ((u32 *)(ws + L.evn))[i] = 0u;
+    ((u64 *)(ws + L.tag))[i] = 0UL;
     err[i] = (i8)skip[i];
     return;
   }
@@ -167,7 +164,7 @@ prep_body( u32 i, u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ si
     }
   }
 
-  u64 * evw = (u64 *)(ws + L.dig) + (size_t)wi*32u;  /* this signature's event row: 16 words h, 16 words s */
+  u64 * evw = (u64 *)(ws + L.dig) + (size_t)i*32u;   /* this signature's event row: 16 words h, 16 words s */
   u32 nh = 0u, ns = 0u;
   int top = -1;
   u64 tag = 0UL;
@@ -224,9 +221,9 @@ prep_body( u32 i, u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ si
     } );
     if( ns & 3u ) evw[16u + (ns >> 2)] = buf;
   }
-  ((u32 *)(ws + L.evn))[wi] = nh | (ns << 8);
-  ((int *)(ws + L.top))[wi] = top;
-  ((u64 *)(ws + L.tag))[wi] = tag;
+  ((u32 *)(ws + L.evn))[i] = nh | (ns << 8);
+  ((int *)(ws + L.top))[i] = top;
+  ((u64 *)(ws + L.tag))[i] = tag;
   err[i] = (i8)code;
 }
 
@@ -248,11 +245,10 @@ k_prep( u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
    decided are skipped. */
 __device__ __forceinline__ void
 decomp_body( u32 t, u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ sig,
-             i8 const * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, bool gate, u32 wbase = 0u ) {
+             i8 const * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, bool gate ) {
   u32 i = t >> 1; u32 which = t & 1u;
   if( i >= n ) return;
   if( gate && err[i] != 1 ) return;
-  u32 const wi = i + wbase;   /* workspace index (prep_body) */
   u8 * ds = ws + L.ds;
   /* the point as 8 LE dwords in two 16-B loads (sig / pub records are 64- /
      32-byte aligned, as k_prep reads them; on the latency path these are
@@ -277,7 +273,7 @@ decomp_body( u32 t, u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ 
   fe chk = fe_sub( vxx, u );
   if( fe_isnonzero( chk ) ) {
     chk = fe_add( vxx, u );
-    if( fe_isnonzero( chk ) ) { ds[2u*wi + which] = 1u; return; }
+    if( fe_isnonzero( chk ) ) { ds[2u*i + which] = 1u; return; }
     x = fe_mul( x, SQRTM1 );
   }
   if( fe_isnegative( x ) != (int)(w[7] >> 31) ) x = fe_neg( x );
@@ -288,18 +284,18 @@ decomp_body( u32 t, u32 n, u8 const * __restrict__ pub, u8 const * __restrict__ 
     i32 * A = (i32 *)(ws + L.A);
     fe nx = fe_neg( x ), nt = fe_neg( T );     /* A := -A (user.c:406-407) */
     _Pragma("unroll") for( int k=0; k<10; k++ ) {
-      A[(size_t)(k   )*N + wi] = nx.v[k];
-      A[(size_t)(10+k)*N + wi] = Y.v[k];
-      A[(size_t)(20+k)*N + wi] = nt.v[k];
+      A[(size_t)(k   )*N + i] = nx.v[k];
+      A[(size_t)(10+k)*N + i] = Y.v[k];
+      A[(size_t)(20+k)*N + i] = nt.v[k];
     }
   } else {
     i32 * R = (i32 *)(ws + L.R);
     _Pragma("unroll") for( int k=0; k<10; k++ ) {
-      R[(size_t)(k   )*N + wi] = x.v[k];
-      R[(size_t)(10+k)*N + wi] = Y.v[k];
+      R[(size_t)(k   )*N + i] = x.v[k];
+      R[(size_t)(10+k)*N + i] = Y.v[k];
     }
   }
-  ds[2u*wi + which] = 0u;
+  ds[2u*i + which] = 0u;
 }
 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FD_DECOMP_WAVES)))
@@ -428,14 +424,6 @@ __device__ __forceinline__ i32 vsel( u64 m, i32 t, i32 f ) {
   i32 r;
   asm( "v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m) );
   return r;
-}
-
-/* the same where the mask is wave-uniform but the compiler may hold it in
-   VGPRs (a loop with many live uniform values): read it back to SGPRs */
-__device__ __forceinline__ i32 vsel_u( u64 m, i32 t, i32 f ) {
-  u64 const s = ((u64)(u32)__builtin_amdgcn_readfirstlane( (int)(u32)(m >> 32) ) << 32) |
-                (u32)__builtin_amdgcn_readfirstlane( (int)(u32)m );
-  return vsel( s, t, f );
 }
 
 enum { PH_DBL = 0, PH_ADDA = 1, PH_ADDB = 2, PH_FIN = 3, PH_DONE = 4 };
@@ -2050,11 +2038,11 @@ tile_txn_layout( u32 l, u32 k, u32 e_sz, u32 e_k, u8 const * __restrict__ mir, u
    + (w % 16) of round q / 4; four rounds (16 frames) have every load
    issued before any store, so a 64-frag chunk waits four round trips to
    the frames' memory (host memory over PCIe in zero-copy mode), not
-   sixteen (profiles/r05_tile_pool_dev.txt: 365 -> ~100 us per chunk under
-   load).  Frames are <= 1328 B = 83 words, chunk-aligned (every 16-B word
-   whole), and hold up to six words per lane per round.  Zero copy: every
-   word also goes out to the frag's output frame; PUB_SIG_MSG: pub and sig
-   to their planes. */
+   sixteen (gather 92 -> 62 us per chunk at saturation, paced service p50
+   1.30 -> 1.25 ms: profiles/r05_tile_pool_experiment.txt).  Frames are
+   <= 1328 B = 83 words, chunk-aligned (every 16-B word whole): up to six
+   words per lane per round.  Zero copy: every word also goes out to the
+   frag's output frame; PUB_SIG_MSG: pub and sig to their planes. */
 __device__ __forceinline__ void
 tile_gather( fd_amd_tile_args_t const & A, u32 k, u32 l, u32 e_src, u32 e_out, u32 e_sz, u8 * __restrict__ mir,
              u8 * __restrict__ pub, u8 * __restrict__ sig, bool txn ) {
@@ -2171,726 +2159,6 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __rest
 # undef TILE_STAMP
 }
 
-/* ------------------------------------------------------------------ */
-/* k_tile_persist, POOLED throughput mode (args.pool, fd_ed25519_kernels.h).
- *
- * The per-lane body of a throughput chunk (k_dsm's uniform 8-mul step)
- * runs every op of 64 signatures side by side, so a lane that doubles
- * while its neighbours add still computes general products.  The batch
- * engine's k_dsmp instead keeps a POOL of signatures per wave and steps 64
- * that want the same op class, which needs a stream of signatures that
- * refills the pool one at a time -- here the XCD's ready queue:
- *
- *   front   the wave that took throughput chunk t lays its signatures out
- *           in region r = t % TP_C of the pool buffer's workspace
- *           (workspace index 64 r + slot): the frags gathered as in
- *           tile_chunk, k_prep's and k_decomp's bodies, the -A table and
- *           each signature's op-stream start; then one release (the
- *           region's lines clean in the XCD's L2, the zero-copy frames out
- *           to the host) and one 16-B ready item per signature into the
- *           queue of its XCD.  Signatures the front decides (s check,
- *           undecodable points, TXN parse failures) never enter a pool;
- *           an entry with nothing left in a pool gets its result here.
- *   pool    every wave of the XCD refills free pool slots from the queue
- *           (one atomic add per refill) and steps 64 slots of one class:
- *           a pure doubling step when 64 want one, else k_dsm's step
- *           taking every ADD first; a signature whose op stream ended
- *           waits in class F, and a compare step (the limb compare of
- *           fd_ed25519_user.c:417-425, as k_fin) finishes up to 64 of
- *           them and stores their result words.  TXN: the last signature
- *           of an entry (an agent-scope counter per entry) reduces it.
- *
- * Hand-offs never leave the XCD (the queue of HW_REG_XCC_ID): plain stores
- * reach the XCD's L2 and every load of handed-off bytes is an sc1 load
- * that bypasses the reading CU's L1 (MI355X_MICROARCH.md, visibility);
- * counters are agent-scope atomics.  A region is reused only when its
- * live counter is 0.  Same field ops per signature as k_dsm: same limbs. */
-
-#define TP_P FD_AMD_TP_P
-#define TP_C FD_AMD_TP_C
-#define TP_Q FD_AMD_TP_Q
-#ifndef TP_FIN_MIN
-#define TP_FIN_MIN 8u       /* finished signatures that make a compare step */
-#endif
-#ifndef TP_REFILL
-#define TP_REFILL 8u        /* free slots that make a refill */
-#endif
-#ifndef TP_CLAIM
-#define TP_CLAIM 16u        /* most queue positions a refill claims */
-#endif
-#ifndef TP_TARGET
-#define TP_TARGET 8192u     /* per XCD: ready items + 64 x fronts under way below which a wave takes a chunk */
-#endif
-static_assert( TP_P >= 64 && TP_P <= 128, "pool: each lane owns slots l and l + 64" );
-enum { OP_F = 5 };          /* pool class: op stream done, the compare is next */
-
-struct tp_lay_t { size_t bt, qctl, items, reg, ws, total; };
-/* a region's workspace: the N = 64 layout (the chunk mode's per-wave one),
-   one per region, so a front touches the same few pages as a chunk */
-constexpr size_t TP_RS = ws_al( ws_layout_const( 64 ).total );
-__host__ __device__ constexpr tp_lay_t tp_layout( void ) {
-  tp_lay_t T = {};
-  size_t o = 0;
-  T.bt    = o; o = ws_al( o + 8UL*48UL*4UL );                                   /* base-point table, bi12 rows */
-  T.qctl  = o; o = ws_al( o + FD_AMD_TP_X * sizeof(fd_amd_tp_qctl_t) );
-  T.items = o; o = ws_al( o + (size_t)FD_AMD_TP_X * TP_Q * 16UL );              /* 16-B ready items */
-  T.reg   = o; o = ws_al( o + (size_t)TP_C * sizeof(fd_amd_tp_region_t) );
-  T.ws    = o; o = ws_al( o + (size_t)TP_C * ws_al( ws_layout_const( 64 ).total ) );   /* region r: an N = 64 workspace */
-  T.total = o;
-  return T;
-}
-static_assert( tp_layout().total < (1UL << 31), "pool buffer: 31-bit buffer offsets" );
-size_t fd_amd_tp_pool_size( void )   { return tp_layout().total; }
-size_t fd_amd_tp_zero_offset( void ) { return tp_layout().qctl; }
-size_t fd_amd_tp_zero_size( void )   { return tp_layout().ws - tp_layout().qctl; }
-
-__global__ void __launch_bounds__(64)
-k_tp_init( u8 * pool ) { bi12_fill( (i32 (*)[48])(pool + tp_layout().bt) ); }
-
-int
-fd_amd_tp_pool_init( void * d_pool, hipStream_t stream ) {
-  hipLaunchKernelGGL( k_tp_init, dim3(1), dim3(64), 0, stream, (u8 *)d_pool );
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-/* sc1 (L1-bypassing) loads of the pool buffer: every load of bytes another
-   wave wrote */
-struct tp_buf_t {
-  __amdgpu_buffer_rsrc_t r;
-  __device__ __forceinline__ uint4 ld16( u32 off ) const {
-    auto v = __builtin_amdgcn_raw_buffer_load_b128( r, (int)off, 0, 16 );
-    return make_uint4( v[0], v[1], v[2], v[3] );
-  }
-  __device__ __forceinline__ u64 ld8( u32 off ) const {
-    auto v = __builtin_amdgcn_raw_buffer_load_b64( r, (int)off, 0, 16 );
-    return ((u64)v[1] << 32) | v[0];
-  }
-  __device__ __forceinline__ u32 ld4( u32 off ) const { return __builtin_amdgcn_raw_buffer_load_b32( r, (int)off, 0, 16 ); }
-};
-
-__device__ __forceinline__ u32 ld_ag32( u32 const * p ) { return __hip_atomic_load( (u32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
-__device__ __forceinline__ void st_ag32( u32 * p, u32 v ) { __hip_atomic_store( p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
-
-/* the ready item of queue position pos, one 16-B store: { low 32 bits of
-   pos + 1, workspace index | class << 24, heads, p | ja << 16 | jb << 24 |
-   lap << 30 } (k_dsmp's slot record; lap: the queue lap mod 4, a second
-   tag in the other 8-B half) */
-__device__ __forceinline__ u32 tp_lap( u64 pos ) { return (u32)((pos / TP_Q + 1UL) & 3UL); }
-
-/* -A's odd multiples (the Ai table, k_dsm's first phase) of workspace index
-   wi, one lane per signature, stored straight from the lane */
-__device__ __forceinline__ void
-tp_ai_table( bool act, u8 * __restrict__ ws, ws_layout_t L, u32 wi ) {
-  size_t const N = L.N;
-  i32 * Ail = (i32 *)(ws + L.Ai) + (size_t)wi*384u;
-  p3 A;
-  i32 const * Aw = (i32 const *)(ws + L.A);
-  _Pragma("unroll") for( int k=0; k<10; k++ ) {
-    A.X.v[k] = act ? Aw[(size_t)(k   )*N + wi] : 0;
-    A.Y.v[k] = act ? Aw[(size_t)(10+k)*N + wi] : (k==0);
-    A.T.v[k] = act ? Aw[(size_t)(20+k)*N + wi] : 0;
-    A.Z.v[k] = (k==0);
-  }
-  fe cZ, cYmX, cYpX, cT2d;
-  ge_to_cached( cZ, cYmX, cYpX, cT2d, A );
-# define AI_ROW( e, r, f ) do {                                                   \
-    int4 * d_ = (int4 *)(Ail + (e)*48 + (r)*12);                                  \
-    d_[0] = make_int4( f.v[0], f.v[1], f.v[2], f.v[3] );                          \
-    d_[1] = make_int4( f.v[4], f.v[5], f.v[6], f.v[7] );                          \
-    d_[2] = make_int4( f.v[8], f.v[9], 0, 0 );                                    \
-  } while(0)
-# define AI_STORE( e ) do { AI_ROW( e, 0, cZ ); AI_ROW( e, 1, cYmX ); AI_ROW( e, 2, cYpX ); AI_ROW( e, 3, cT2d ); } while(0)
-  if( act ) AI_STORE( 0 );
-  p1p1 t = ge_dbl( A.X, A.Y, A.Z );
-  p3 A2 = ge_p1p1_to_p3( t );
-  for( int e=0; e<7; e++ ) {
-    p1p1 s2 = ge_add<false>( A2, cZ, cYmX, cYpX, cT2d, false );
-    p3 u = ge_p1p1_to_p3( s2 );
-    ge_to_cached( cZ, cYmX, cYpX, cT2d, u );
-    if( act ) AI_STORE( e+1 );
-  }
-# undef AI_STORE
-# undef AI_ROW
-}
-
-/* result words of ring index j: tag, trace time, then (after the caller's
-   wait) the word */
-__device__ __forceinline__ void
-tp_res_tag( fd_amd_tile_args_t const & A, u64 j, u64 tag, u32 tc ) {
-  u64 const x = j & A.mask;
-  st_sys64( A.res_tag + x, tag );
-  if( A.res_time ) st_sys64( A.res_time + x, (u64)tc | ((u64)(u32)__builtin_amdgcn_s_memrealtime() << 32) );
-}
-__device__ __forceinline__ void
-tp_res_word( fd_amd_tile_args_t const & A, u64 j, i8 v ) {
-  st_sys64( A.res_word + (j & A.mask), ((j + 1UL) << 8) | (u64)(u8)v );
-}
-
-/* the front of throughput chunk t (ring entries [c0, c0 + k)) into region
-   t % TP_C; false, with nothing done, while that region's previous chunk
-   still has signatures in pools */
-__device__ __forceinline__ bool
-tp_front( fd_amd_tile_args_t const & A, u64 t, u64 c0, u32 k, u8 * __restrict__ scr, tile_scratch_t const & S,
-          u32 * __restrict__ lds, fd_amd_tp_qctl_t * __restrict__ Q, u8 * __restrict__ items, u64 tc, u64 * pt ) {
-  /* pt (A.prof, diagnostics build): ticks in gather [12], prep [13], decomp
-     [14], -A table and starts [15], header and early results [16], the
-     release [17], the items [18] */
-  u64 ts = A.prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
-# define TP_STAMP( k_ ) do { if( A.prof ) { u64 t_ = __builtin_amdgcn_s_memrealtime(); if( !threadIdx.x ) pt[k_] += t_ - ts; ts = t_; } } while(0)
-  constexpr tp_lay_t    T = tp_layout();
-  constexpr ws_layout_t W = ws_layout_const( 64 );
-  u32 const r = (u32)(t % TP_C);
-  fd_amd_tp_region_t * R = (fd_amd_tp_region_t *)(A.pool + T.reg) + r;
-  {
-    u32 live = 0u;
-    if( threadIdx.x == 0u ) live = ld_ag32( &R->live );
-    if( __builtin_amdgcn_readfirstlane( (int)live ) ) return false;
-  }
-  {
-    __attribute__((address_space(1))) u8 * g = (__attribute__((address_space(1))) u8 *)scr;
-    asm volatile( "" : "+s"(g) );
-    scr = (u8 *)g;
-  }
-  u32 l = threadIdx.x;
-  asm volatile( "" : "+v"(l) );
-  u8 * ws = A.pool + T.ws + (size_t)r * TP_RS;
-  u8 * mir = scr + S.mir; u8 * pub = scr + S.pub; u8 * sig = scr + S.sig;
-  u32 * off = (u32 *)(scr + S.off); u32 * sz = (u32 *)(scr + S.sz);
-  i8 * err = R->err;
-  bool const txn = A.txn != 0u;
-
-  /* 1. ring entries and the frags, as tile_chunk */
-  u32 e_src = 0u, e_out = 0u, e_sz = 96u, e_k = 0u;
-  if( l < k ) {
-    u64 const * ep = (u64 const *)(A.ent + ((c0 + l) & A.mask));
-    u64 w0 = ld_sys64( ep ), w1 = ld_sys64( ep + 1 );
-    e_src = (u32)w0; e_out = (u32)(w0 >> 32); e_sz = (u32)w1; e_k = (u32)(w1 >> 32);
-  }
-  tile_gather( A, k, l, e_src, e_out, e_sz, mir, pub, sig, txn );
-  if( l < k && !txn ) { off[l] = l * TILE_FRAME + 96u; sz[l] = e_sz - 96u; }
-  __syncthreads();
-  i8 * skp = (i8 *)(scr + S.skp);
-  u32 * tx = (u32 *)(scr + S.tx);
-  u32 const n = txn ? tile_txn_layout( l, k, e_sz, e_k, mir, pub, sig, off, sz, skp, tx, lds ) : k;
-  if( txn ) __syncthreads();
-  TP_STAMP( 12 );
-
-  /* 2. k_prep's and k_decomp's bodies into the region's workspace rows */
-  u32 const wb = r * 64u;
-  prep_body( l, n, pub, sig, off, sz, mir, err, ws, W, txn ? (i8 const *)skp : (i8 const *)0 );
-  __syncthreads();
-  TP_STAMP( 13 );
-  decomp_body( l, n, pub, sig, err, ws, W, true );
-  if( n > 32u ) decomp_body( l + 64u, n, pub, sig, err, ws, W, true );
-  __syncthreads();
-  TP_STAMP( 14 );
-
-  /* 3. the -A table and the op-stream start (k_ai) */
-  u32 const wi = wb + l;                                /* the signature's index in the pool buffer */
-  bool act = l < n && err[l] == 1;
-  if( act && (ws[W.ds + 2u*l] | ws[W.ds + 2u*l + 1u]) ) { err[l] = (i8)-2; act = false; }
-  tp_ai_table( act, ws, W, l );
-  u32 i1 = 0u, i2 = 0u, i3 = 0u;
-  if( act ) {
-    int const p = ((int const *)(ws + W.top))[l];
-    u32 heads = 0xffffffffu, pz = 0u, op = (u32)OP_F;   /* no digit at all: R' is the identity */
-    if( p >= 0 ) {
-      u32 const ne = ((u32 const *)(ws + W.evn))[l];
-      u32 const na = ne & 0xffu, nb = (ne >> 8) & 0xffu;
-      u16 const * ev = (u16 const *)(ws + W.dig) + (size_t)l*128u;
-      u32 const hA = na ? (u32)ev[na - 1u] : 0xffffu, hB = nb ? (u32)ev[64u + nb - 1u] : 0xffffu;
-      heads = hA | (hB << 16); pz = ((u32)p & 0xffffu) | (na << 16) | (nb << 24); op = (u32)OP_D;
-    }
-    i1 = wi | (op << 24); i2 = heads; i3 = pz;
-  }
-  u64 const m = __builtin_amdgcn_ballot_w64( act );
-  u32 const ni = (u32)__builtin_popcountll( m );
-  TP_STAMP( 15 );
-
-  /* 4. the region's header; entries with nothing in a pool get their
-        result now (tags here, words after the release) */
-  if( l == 0u ) { R->c0 = c0; R->k = k; R->n = n; R->tc = (u32)tc; }
-  bool now = false; i8 v = 0; u64 tag = 0UL;
-  if( l < k ) {
-    if( !txn ) {
-      now = !((m >> l) & 1UL);
-      if( now ) { v = err[l]; tag = ((u64 const *)(ws + W.tag))[l]; }
-    } else {
-      u32 const w = tx[l], b = w & 0xffu, kk = (w >> 8) & 0xffu;
-      R->tx[l] = w;
-      u64 const km = kk >= 64u ? ~0UL : ((1UL << kk) - 1UL);
-      u32 const cnt = (u32)__builtin_popcountll( (m >> b) & km );
-      st_ag32( &R->ecnt[l], cnt );
-      now = cnt == 0u;
-      if( now ) {
-        if( !(w >> 31) ) v = (i8)TXN_ERR_PARSE;
-        else for( u32 i=0u; i<kk; i++ ) { i8 const e = err[b + i]; if( e ) { v = e; break; } }
-        if( kk ) tag = ((u64 const *)(ws + W.tag))[b];
-      }
-    }
-    if( now ) tp_res_tag( A, c0 + l, tag, (u32)tc );
-  }
-  if( txn && l < n ) R->own[l] = (u8)lds[l];              /* tile_txn_layout's slot -> entry */
-  if( l == 0u ) st_ag32( &R->live, ni );
-  asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
-  TP_STAMP( 16 );
-  __builtin_amdgcn_fence( __ATOMIC_RELEASE, "" );         /* system: the region's lines, and the zero-copy frames */
-  asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
-  TP_STAMP( 17 );
-  if( now ) tp_res_word( A, c0 + l, v );
-
-  /* 5. the ready items */
-  if( ni ) {
-    u64 pos = 0UL;
-    if( l == 0u ) pos = __hip_atomic_fetch_add( &Q->res, (u64)ni, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-    pos = rfl64( pos ) + lane_rank( m );
-    if( act ) *(uint4 *)(items + (pos % TP_Q) * 16UL) = make_uint4( (u32)(pos + 1UL), i1, i2, i3 | (tp_lap( pos ) << 30) );
-  }
-  TP_STAMP( 18 );
-# undef TP_STAMP
-  return true;
-}
-
-__device__ __forceinline__ u64 rotr64( u64 x, u32 r ) { return r ? (x >> r) | (x << (64u - r)) : x; }
-__device__ __forceinline__ u64 rotl64( u64 x, u32 r ) { return r ? (x << r) | (x >> (64u - r)) : x; }
-
-/* the pool's LDS: p1p1 state, slot records, the step's rank list */
-struct tp_lds_t {
-  int4  (* t)[TP_P];   /* [10][TP_P]: 16-B column r of slot s */
-  uint4 * m;           /* [TP_P]: { workspace index, heads, p | ja << 16 | jb << 24, class }; class W: { queue position, -, - } */
-  u32   * list;        /* [64] */
-  u64   * ps;          /* [12]: the loop's state while a chunk's bodies run */
-};
-
-/* The compare step: up to 64 slots of class F -> p1p1 -> p2, the limb
-   compare against R (k_fin), the result words; the slots become free. */
-__device__ __forceinline__ void
-tp_fin_step( fd_amd_tile_args_t const & A, tp_buf_t const & B, tp_lds_t const & P, u64 & mF0, u64 & mF1 ) {
-  constexpr tp_lay_t    T = tp_layout();
-  constexpr ws_layout_t W = ws_layout_const( 64 );
-  u32 const l = threadIdx.x;
-  u32 const nF0 = (u32)__builtin_popcountll( mF0 );
-  u32 const rk0 = lane_rank( mF0 ), rk1 = nF0 + lane_rank( mF1 );
-  u64 const S0 = mF0 & __builtin_amdgcn_ballot_w64( rk0 < 64u ), S1 = mF1 & __builtin_amdgcn_ballot_w64( rk1 < 64u );
-  u32 const nsel = (u32)(__builtin_popcountll( S0 ) + __builtin_popcountll( S1 ));
-  if( (S0 >> l) & 1UL ) P.list[rk0] = l;
-  if( (S1 >> l) & 1UL ) P.list[rk1] = l + 64u;
-  mF0 &= ~S0; mF1 &= ~S1;
-  __builtin_amdgcn_wave_barrier();
-  bool const live = l < nsel;
-  u32 const s = live ? P.list[l] : 0u;
-  uint4 const mm = P.m[s];
-  u32 const wi = mm.x & 0xffffffu;
-  p1p1 t;
-  pool_load_ts( t, &P.t[0][s], TP_P );
-  fe uZ, uY, uX;
-  fe_mul_fold2w( uZ, t.Z, t.T, uY, t.Z, t.Y );
-  uX = fe_mul_fold1( t.X, t.T );
-  u32 const wsr = (u32)(T.ws + (size_t)(wi >> 6) * TP_RS);   /* the signature's region workspace */
-  fe RX, RY;
-  _Pragma("unroll") for( int k=0; k<10; k++ ) {
-    RX.v[k] = (i32)B.ld4( wsr + (u32)(W.R + 4UL*((size_t)k*64u + (wi & 63u))) );
-    RY.v[k] = (i32)B.ld4( wsr + (u32)(W.R + 4UL*((size_t)(10+k)*64u + (wi & 63u))) );
-  }
-  fe xZ, yZ;
-  fe_mul_fold2w( xZ, uZ, RX, yZ, uZ, RY );
-  bool eq = true;
-  _Pragma("unroll") for( int k=0; k<8; k++ ) eq = eq && (xZ.v[k] == uX.v[k]) && (yZ.v[k] == uY.v[k]);
-  i8 const v = (i8)(eq ? 0 : -3);
-
-  /* results */
-  u32 const r = wi >> 6, sl = wi & 63u;
-  fd_amd_tp_region_t * R = (fd_amd_tp_region_t *)(A.pool + T.reg) + r;
-  u32 const rb = (u32)(T.reg + (size_t)r * sizeof(fd_amd_tp_region_t));
-  u64 const c0 = B.ld8( rb + (u32)offsetof( fd_amd_tp_region_t, c0 ) );
-  u32 const tcr = B.ld4( rb + (u32)offsetof( fd_amd_tp_region_t, tc ) );
-  bool last = false; u64 jq = 0UL; i8 vq = 0;
-  if( !A.txn ) {
-    if( live ) {
-      jq = c0 + sl; vq = v; last = true;
-      tp_res_tag( A, jq, B.ld8( wsr + (u32)(W.tag + 8UL*sl) ), tcr );
-    }
-  } else if( live ) {
-    /* this slot's verdict, then the entry's count; the last one reduces */
-    __hip_atomic_store( (u8 *)&R->err[sl], (u8)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-    asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
-    u32 const q = (B.ld4( rb + (u32)offsetof( fd_amd_tp_region_t, own ) + (sl & ~3u) ) >> (8u*(sl & 3u))) & 0xffu;
-    u32 const old = __hip_atomic_fetch_sub( &R->ecnt[q], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-    if( old == 1u ) {
-      last = true; jq = c0 + q;
-      u32 const w = B.ld4( rb + (u32)offsetof( fd_amd_tp_region_t, tx ) + 4u*q ), b = w & 0xffu, kk = (w >> 8) & 0xffu;
-      if( !(w >> 31) ) vq = (i8)TXN_ERR_PARSE;
-      else for( u32 i=0u; i<kk; i++ ) {
-        u32 const si = b + i;
-        i8 const e = (i8)(B.ld4( rb + (u32)offsetof( fd_amd_tp_region_t, err ) + (si & ~3u) ) >> (8u*(si & 3u)));
-        if( e ) { vq = e; break; }
-      }
-      tp_res_tag( A, jq, kk ? B.ld8( wsr + (u32)(W.tag + 8UL*b) ) : 0UL, tcr );
-    }
-  }
-  asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
-  if( last ) tp_res_word( A, jq, vq );
-  asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
-  if( live ) (void)__hip_atomic_fetch_sub( &R->live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-}
-
-/* The pooled mode's persistent loop (k_tile_persist with args.pool): per
-   iteration the control words, a chunk when the wave holds a ticket whose
-   descriptor is out (latency chunks whole, as tile_chunk; throughput
-   chunks as a front), a refill from the XCD's queue, then a compare step
-   or a pool step.  Nothing in it waits on another wave; it sleeps only
-   with nothing to do, and every wave leaves at the stop or error bit of
-   its mirror word (or when that word stood still for the watchdog). */
-enum { OP_W = 6 };          /* pool class: a claimed queue position whose item is not written yet */
-__device__ __forceinline__ void
-tp_run( fd_amd_tile_args_t const & A, u8 * __restrict__ scr, tile_scratch_t const & S, ws_layout_t L64,
-        u64 const * mw, u32 xcc, tp_lds_t const & P, u64 (* __restrict__ evl)[33], u64 * s_tally, bool prof ) {
-  constexpr tp_lay_t    T = tp_layout();
-  constexpr ws_layout_t W = ws_layout_const( 64 );
-  fd_amd_tile_dctl_t * D = A.dctl;
-  fd_amd_tp_qctl_t * Q = (fd_amd_tp_qctl_t *)(A.pool + T.qctl) + xcc;
-  u8 * items = A.pool + T.items + (size_t)xcc * TP_Q * 16UL;
-  u32 const iofs = (u32)(T.items + (size_t)xcc * TP_Q * 16UL);
-  tp_buf_t B; B.r = __builtin_amdgcn_make_buffer_rsrc( A.pool, (short)0, (int)T.total, 0x00020000 );
-  i32 (* bi)[48] = (i32 (*)[48])(A.pool + T.bt);
-  u64 const valid1 = (TP_P >= 128u) ? ~0UL : ((1UL << (TP_P - 64u)) - 1UL);
-  u64 mD0 = 0, mD1 = 0, mA0 = 0, mA1 = 0, mF0 = 0, mF1 = 0, mW0 = 0, mW1 = 0;
-  bool hold = false;                  /* a ticket is held: descriptor tk */
-  u64 tk = 0UL;
-  bool have = false;                  /* control words loaded during the last step */
-  u64 cw = 0UL, cr = 0UL, ch = 0UL, cf = 0UL;
-  u64 wlast = ~0UL, tw = __builtin_amdgcn_s_memrealtime();
-  u32 nap = 1u;
-  u32 rotc = 0u;                      /* selection rotation (bits 0-5) and word order (bit 6) */
-  u32 lvl = 0u;                       /* issue priority */
-  for( ;; ) {
-    /* the lane index, opaque per iteration: otherwise every per-lane
-       address of the bodies is hoisted out of the loop and kept live across
-       the chunk bodies, which then spill */
-    u32 l = threadIdx.x;
-    asm volatile( "" : "+v"(l) );
-    if( !have && l == 0u ) {
-      cw = ld_dev64( mw );
-      cr = __hip_atomic_load( &Q->res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-      ch = __hip_atomic_load( &Q->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-      cf = __hip_atomic_load( &Q->fronts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-    }
-    have = false;
-    u64 const w = rfl64( cw ), qres = rfl64( cr ), qhead = rfl64( ch ), qfr = rfl64( cf );
-    cw = cr = ch = cf = 0UL;   /* dead until the step reloads them (not live across a front) */
-    if( w & (TILE_MW_ERR | TILE_MW_STOP) ) break;
-    /* the class masks are wave-uniform; said so once per iteration (the
-       parked copies come back through LDS) */
-    mD0 = rfl64( mD0 ); mD1 = rfl64( mD1 ); mA0 = rfl64( mA0 ); mA1 = rfl64( mA1 );
-    mF0 = rfl64( mF0 ); mF1 = rfl64( mF1 ); mW0 = rfl64( mW0 ); mW1 = rfl64( mW1 );
-    {
-      u64 const now = __builtin_amdgcn_s_memrealtime();
-      if( w != wlast ) { wlast = w; tw = now; }
-      else if( now - tw > A.watchdog ) break;      /* no scout (or host) for that long: give up */
-    }
-    u32 const nD = (u32)(__builtin_popcountll( mD0 ) + __builtin_popcountll( mD1 ));
-    u32 const nA = (u32)(__builtin_popcountll( mA0 ) + __builtin_popcountll( mA1 ));
-    u32 const nF = (u32)(__builtin_popcountll( mF0 ) + __builtin_popcountll( mF1 ));
-    u32 const nW = (u32)(__builtin_popcountll( mW0 ) + __builtin_popcountll( mW1 ));
-    u64 const backlog = qres > qhead ? qres - qhead : 0UL;
-
-    /* 1. a chunk: take a ticket while the XCD's ready items and fronts
-          under way are short of TP_TARGET (always, when the pool is empty) */
-    if( !hold && (nD + nA + nF + nW == 0u || backlog + 64UL * qfr < (u64)TP_TARGET) ) {
-      u64 t = 0UL;
-      if( l == 0u ) t = atomicAdd( (unsigned long long *)&D->ticket, 1ULL );
-      tk = rfl64( t ); hold = true;
-    }
-    bool did = false;
-    if( hold && TILE_MW_HEAD( w ) > tk ) {
-      u64 tc = __builtin_amdgcn_s_memrealtime();
-      u64 c = 0, cm = 0;
-      if( l == 0u ) {
-        u64 const * dp = (u64 const *)(A.desc + (tk & A.mask));
-        c = ld_sys64( dp ); cm = ld_sys64( dp + 1 );
-      }
-      c = rfl64( c ); cm = rfl64( cm );
-      u32 const take = (u32)cm & 0x7fffffffu;
-      bool const e8 = ((u32)cm >> 31) != 0u;
-      __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "" );    /* the host's frames: drop this CU's stale lines */
-      asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
-      bool ok = true;
-      if( take && take <= 64u ) {
-        /* the pool's state waits in LDS while the chunk bodies run (kept in
-           registers across them, it made those bodies spill) */
-        volatile u64 * ps = P.ps;
-        if( l == 0u ) {
-          ps[0] = mD0; ps[1] = mD1; ps[2] = mA0; ps[3] = mA1; ps[4] = mF0; ps[5] = mF1; ps[6] = mW0; ps[7] = mW1;
-          ps[8] = tk; ps[9] = wlast; ps[10] = tw;
-        }
-        u64 const tf0 = prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
-        if( e8 ) tile_chunk( A, c, take, true, scr, L64, S, bi, evl, s_tally, tc );
-        else {
-          if( l == 0u ) __hip_atomic_fetch_add( &Q->fronts, 1UL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-          ok = tp_front( A, tk, c, take, scr, S, (u32 *)&evl[0][0], Q, items, tc, s_tally );
-          if( l == 0u ) __hip_atomic_fetch_sub( &Q->fronts, 1UL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-          if( prof && !ok && l == 0u ) s_tally[7] += 1UL;
-        }
-        if( prof && l == 0u ) s_tally[6] += __builtin_amdgcn_s_memrealtime() - tf0;
-        __builtin_amdgcn_wave_barrier();
-        mD0 = rfl64( ps[0] ); mD1 = rfl64( ps[1] ); mA0 = rfl64( ps[2] ); mA1 = rfl64( ps[3] );
-        mF0 = rfl64( ps[4] ); mF1 = rfl64( ps[5] ); mW0 = rfl64( ps[6] ); mW1 = rfl64( ps[7] );
-        tk = rfl64( ps[8] ); wlast = rfl64( ps[9] ); tw = rfl64( ps[10] );
-      }
-      if( ok ) {
-        hold = false; did = true;
-        if( l == 0u ) {
-          s_tally[e8 ? 8 : 9] += 1UL; s_tally[e8 ? 10 : 11] += take;
-          atomicAdd( (unsigned long long *)&D->done, 1ULL );   /* progress, mirrored to the host by the scout */
-        }
-      }
-    }
-
-    /* 2. refill: claim queue positions for free slots (class W), then turn
-          every W slot whose item is written into a D / F slot */
-    u64 const f0 = ~(mD0 | mA0 | mF0 | mW0), f1 = ~(mD1 | mA1 | mF1 | mW1) & valid1;
-    u32 const nfree = (u32)(__builtin_popcountll( f0 ) + __builtin_popcountll( f1 ));
-    u32 const nbusy = nD + nA + nF;
-    if( nfree && backlog && (nfree >= TP_REFILL || nbusy < 64u) ) {
-      /* at most TP_CLAIM per refill: a wave that claimed everything in
-         sight would hoard the XCD's next items while its neighbours idle */
-      u32 const cm = nfree < TP_CLAIM ? nfree : TP_CLAIM;
-      u32 const c = (u32)(backlog < (u64)cm ? backlog : (u64)cm);
-      u64 base = 0UL;
-      if( l == 0u ) base = __hip_atomic_fetch_add( &Q->head, (u64)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-      base = rfl64( base );
-      u32 const pf0 = (u32)__builtin_popcountll( f0 );
-      u32 const k0 = lane_rank( f0 ), k1 = pf0 + lane_rank( f1 );
-      bool const c0 = ((f0 >> l) & 1UL) && k0 < c, c1 = ((f1 >> l) & 1UL) && k1 < c;
-      if( c0 ) { u64 const pos = base + k0; P.m[l] = make_uint4( (u32)pos, (u32)(pos >> 32), 0u, (u32)OP_W ); }
-      if( c1 ) { u64 const pos = base + k1; P.m[l + 64u] = make_uint4( (u32)pos, (u32)(pos >> 32), 0u, (u32)OP_W ); }
-      mW0 |= __builtin_amdgcn_ballot_w64( c0 );
-      mW1 |= __builtin_amdgcn_ballot_w64( c1 );
-    }
-    if( mW0 | mW1 ) {
-      bool const w0 = (mW0 >> l) & 1UL, w1 = (mW1 >> l) & 1UL;
-      uint4 const s0 = P.m[l], s1 = P.m[l + 64u < TP_P ? l + 64u : l];
-      u64 const p0 = ((u64)s0.y << 32) | s0.x, p1 = ((u64)s1.y << 32) | s1.x;
-      uint4 const it0 = B.ld16( iofs + (u32)((p0 % TP_Q) * 16UL) ), it1 = B.ld16( iofs + (u32)((p1 % TP_Q) * 16UL) );
-      bool const r0 = w0 && it0.x == (u32)(p0 + 1UL) && (it0.w >> 30) == tp_lap( p0 );
-      bool const r1 = w1 && it1.x == (u32)(p1 + 1UL) && (it1.w >> 30) == tp_lap( p1 );
-      p1p1 id;   /* new signatures enter with the identity (p1p1 whose p2 is (0,1,1)) */
-      id.X = fe_zero(); id.Y = fe_one(); id.Z = fe_one(); id.T = fe_one();
-      u32 const op0 = it0.y >> 24, op1 = it1.y >> 24;
-      u32 const te = (u32)(__builtin_amdgcn_s_memrealtime() >> 5) << 3;   /* entry time, 0.32 us units, in bits 3.. of the class word */
-      if( r0 ) { P.m[l] = make_uint4( it0.y & 0xffffffu, it0.z, it0.w & 0x3fffffffu, op0 | te ); pool_store_ts( &P.t[0][l], TP_P, id ); }
-      if( r1 ) { P.m[l + 64u] = make_uint4( it1.y & 0xffffffu, it1.z, it1.w & 0x3fffffffu, op1 | te ); pool_store_ts( &P.t[0][l + 64u], TP_P, id ); }
-      u64 const g0 = __builtin_amdgcn_ballot_w64( r0 ), g1 = __builtin_amdgcn_ballot_w64( r1 );
-      u64 const d0 = __builtin_amdgcn_ballot_w64( r0 && op0 == (u32)OP_D ), d1 = __builtin_amdgcn_ballot_w64( r1 && op1 == (u32)OP_D );
-      mW0 &= ~g0; mW1 &= ~g1;
-      mD0 |= d0; mD1 |= d1;
-      mF0 |= g0 & ~d0; mF1 |= g1 & ~d1;
-    }
-
-    u32 const kD = (u32)(__builtin_popcountll( mD0 ) + __builtin_popcountll( mD1 ));
-    u32 const kA = (u32)(__builtin_popcountll( mA0 ) + __builtin_popcountll( mA1 ));
-    u32 const kF = (u32)(__builtin_popcountll( mF0 ) + __builtin_popcountll( mF1 ));
-    if( kD + kA + kF == 0u ) {
-      if( !did ) {
-        /* nothing to step: sleep, longer the longer nothing came */
-        if( lvl ) { lvl = 0u; __builtin_amdgcn_s_setprio( 0 ); }
-        u64 const ts0 = prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
-        for( u32 z = 0; z < nap; z++ ) __builtin_amdgcn_s_sleep( 4 );
-        if( prof && l == 0u ) s_tally[5] += __builtin_amdgcn_s_memrealtime() - ts0;
-        nap = nap < 32u ? nap + 1u : 32u;
-      }
-      continue;
-    }
-    nap = 1u;
-
-    /* 3. the compare step, when enough finished signatures wait (or the
-          pool has nothing else to fill a step) */
-    if( kF >= TP_FIN_MIN || (kF && kD + kA < 64u) ) {
-      if( prof && l == 0u ) s_tally[3] += 1UL;
-      tp_fin_step( A, B, P, mF0, mF1 );
-      continue;
-    }
-
-    /* 4. a pool step (k_dsmp's): a pure doubling step on 64 D slots, or a
-          mixed step taking every A slot first and filling with D slots;
-          the next iteration's control words load meanwhile */
-    if( l == 0u ) {
-      cw = ld_dev64( mw );
-      cr = __hip_atomic_load( &Q->res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-      ch = __hip_atomic_load( &Q->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-      cf = __hip_atomic_load( &Q->fronts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-    }
-    have = true;
-    /* issue priority by the age of the pool's oldest signature (every 4th
-       step): two waves share a SIMD, and at equal priority the arbiter
-       prefers the older WAVE, so the other one's pool would crawl and, the
-       tile publishing in order, hold everything behind it (the chunk mode's
-       chunk-age priority, tile_age_prio) */
-    if( !(rotc & 3u) ) {
-      u32 const now5 = (u32)(__builtin_amdgcn_s_memrealtime() >> 5);
-      u64 const occ0 = mD0 | mA0 | mF0, occ1 = mD1 | mA1 | mF1;
-      u32 const w0 = P.m[l].w, w1 = P.m[l + 64u < TP_P ? l + 64u : l].w;
-      u32 const a0 = ((occ0 >> l) & 1UL) ? ((now5 - (w0 >> 3)) & 0x1fffffffu) : 0u;
-      u32 const a1 = ((occ1 >> l) & 1UL) ? ((now5 - (w1 >> 3)) & 0x1fffffffu) : 0u;
-      u32 const ag = a0 > a1 ? a0 : a1;   /* 0.32 us units: 2500 = 0.8 ms */
-      u32 const want = __builtin_amdgcn_ballot_w64( ag >= 7500u ) ? 3u : __builtin_amdgcn_ballot_w64( ag >= 5000u ) ? 2u
-                     : __builtin_amdgcn_ballot_w64( ag >= 2500u ) ? 1u : 0u;
-      if( want != lvl ) {
-        lvl = want;
-        if( want == 1u )      __builtin_amdgcn_s_setprio( 1 );
-        else if( want == 2u ) __builtin_amdgcn_s_setprio( 2 );
-        else if( want == 3u ) __builtin_amdgcn_s_setprio( 3 );
-        else                  __builtin_amdgcn_s_setprio( 0 );
-      }
-    }
-    u32 const kM = (kD + kA) < 64u ? (kD + kA) : 64u, kDs = kD < 64u ? kD : 64u;
-    bool const mixed = kDs < kM;
-    u32 const nsel = mixed ? kM : kDs;
-    u64 const sA0 = mixed ? mA0 : 0UL, sA1 = mixed ? mA1 : 0UL;
-    u32 const aoff = mixed ? kA : 0u;
-    /* selection order [ADD slots, DBL slots] (ADDs only in a mixed step),
-       each class in a rotating slot order: both words rotated by rot, and
-       the word that goes first alternating step by step, so a DBL slot
-       waits at most a few steps however full the pool is (in plain slot
-       order the high slots starved: tail latency).  Owner lane l ranks the
-       slots at rotated position l of the first (F) and second (G) word. */
-    u32 const rot = rotc & 63u;
-    bool const sw = (rotc >> 6) & 1u;
-    u64 const fA = rotr64( sw ? sA1 : sA0, rot ), gA = rotr64( sw ? sA0 : sA1, rot );
-    u64 const fD = rotr64( sw ? mD1 : mD0, rot ), gD = rotr64( sw ? mD0 : mD1, rot );
-    u32 const paF = (u32)__builtin_popcountll( fA ), pdF = (u32)__builtin_popcountll( fD );
-    u32 const rkF = (u32)vsel_u( fA, (i32)lane_rank( fA ), (i32)(aoff + lane_rank( fD )) );
-    u32 const rkG = (u32)vsel_u( gA, (i32)(paF + lane_rank( gA )), (i32)(aoff + pdF + lane_rank( gD )) );
-    u64 const SF = (fA | fD) & __builtin_amdgcn_ballot_w64( rkF < 64u );
-    u64 const SG = (gA | gD) & __builtin_amdgcn_ballot_w64( rkG < 64u );
-    u64 const S0 = rotl64( sw ? SG : SF, rot ), S1 = rotl64( sw ? SF : SG, rot );
-    mA0 &= ~S0; mA1 &= ~S1; mD0 &= ~S0; mD1 &= ~S1;
-    bool const live = l < nsel;
-    u64 const tst = prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
-    if( prof && l == 0u ) { s_tally[mixed ? 1 : 0] += 1UL; s_tally[2] += nsel; }
-    {
-      u32 const pos = (l + rot) & 63u;
-      if( __builtin_amdgcn_inverse_ballot_w64( SF ) ) P.list[rkF] = pos + (sw ? 64u : 0u);
-      if( __builtin_amdgcn_inverse_ballot_w64( SG ) ) P.list[rkG] = pos + (sw ? 0u : 64u);
-    }
-    rotc = (rotc + 64u + 29u) & 127u;
-    __builtin_amdgcn_wave_barrier();
-    u32 const s = live ? P.list[l] : 0u;
-    uint4 const m = P.m[s];
-    u32 const op = live ? (m.w & 7u) : (u32)OP_D;
-    u32 const si = live ? m.x : 0u;
-    u32 hA = m.y & 0xffffu, hB = m.y >> 16;
-    int p = (int)(short)(m.z & 0xffffu);
-    u32 ja = (m.z >> 16) & 0xffu, jb = m.z >> 24;
-    u32 const pidx = (op == OP_AA && ja >= 2u) ? ja - 2u : (op == OP_AB && jb >= 2u) ? 64u + jb - 2u : 0u;
-    bool const pop = (op == OP_AA && ja >= 2u) || (op == OP_AB && jb >= 2u);
-    u32 const wsr = (u32)(T.ws + (size_t)(si >> 6) * TP_RS), sl = si & 63u;   /* the slot's region workspace */
-    u32 const nh = B.ld4( pop ? wsr + (u32)(W.dig + 256UL*sl + 4UL*(pidx >> 1)) : (u32)T.bt );
-    p1p1 t;
-    pool_load_ts( t, &P.t[0][s], TP_P );
-
-    if( mixed ) {
-      bool isadd = op == OP_AA || op == OP_AB;
-      int dg = (op == OP_AA) ? (int)(i8)(hA >> 8) : (int)(i8)(hB >> 8);
-      bool neg = isadd && dg < 0;
-      int e = isadd ? ((dg < 0 ? -dg : dg) >> 1) & 7 : 0;
-      u32 const qb = (op == OP_AA) ? wsr + (u32)(W.Ai + 4UL*((size_t)sl*384u + (u32)e*48u)) : (u32)(T.bt + 4UL*(u32)e*48u);
-      int const rowM = neg ? 2 : 1, rowP = neg ? 1 : 2;
-      fe q[4];
-#     define Q_ROW( R_, C_ ) do {                                                     \
-        u32 const o_ = qb + 48u*(u32)(C_);                                           \
-        uint4 x0 = B.ld16( o_ ), x1 = B.ld16( o_ + 16u ), x2 = B.ld16( o_ + 32u );   \
-        q[R_].v[0] = (i32)x0.x; q[R_].v[1] = (i32)x0.y; q[R_].v[2] = (i32)x0.z; q[R_].v[3] = (i32)x0.w;  \
-        q[R_].v[4] = (i32)x1.x; q[R_].v[5] = (i32)x1.y; q[R_].v[6] = (i32)x1.z; q[R_].v[7] = (i32)x1.w;  \
-        q[R_].v[8] = (i32)x2.x; q[R_].v[9] = (i32)x2.y;                              \
-      } while(0)
-      Q_ROW( 0, 0 ); Q_ROW( 1, rowM ); Q_ROW( 2, rowP ); Q_ROW( 3, 3 );
-#     undef Q_ROW
-      p3 u = ge_p1p1_to_p3_fold( t );
-      _Pragma("unroll") for( int rr=0; rr<4; rr++ )
-        asm volatile( "" : "+v"(q[rr].v[0]), "+v"(q[rr].v[1]), "+v"(q[rr].v[2]), "+v"(q[rr].v[3]), "+v"(q[rr].v[4]),
-                           "+v"(q[rr].v[5]), "+v"(q[rr].v[6]), "+v"(q[rr].v[7]), "+v"(q[rr].v[8]), "+v"(q[rr].v[9])
-                         : "v"(u.X.v[9]), "v"(u.T.v[9]) );
-      u64 mD = __builtin_amdgcn_ballot_w64( !isadd ), mN = __builtin_amdgcn_ballot_w64( neg );
-      fe m0, m1, m2, m3;
-      {
-        fe a0, b0, a1, b1, a2, b2, a3, b3;
-        _Pragma("unroll") for( int k=0; k<10; k++ ) {
-          i32 xy = u.X.v[k] + u.Y.v[k];
-          a0.v[k] = xy;                                     b0.v[k] = vsel( mD, xy, q[2].v[k] );
-          a1.v[k] = vsel( mD, u.Y.v[k], u.Y.v[k] - u.X.v[k] ); b1.v[k] = vsel( mD, u.Y.v[k], q[1].v[k] );
-          a2.v[k] = u.Z.v[k];                              b2.v[k] = vsel( mD, u.Z.v[k] + u.Z.v[k], q[0].v[k] );
-          a3.v[k] = vsel( mD, u.X.v[k], u.T.v[k] );        b3.v[k] = vsel( mD, u.X.v[k], q[3].v[k] );
-        }
-        fe_mul_fold2w<true, true>( m0, a0, b0, m1, a1, b1 );
-        fe_mul_fold2w<false, true>( m2, a2, b2, m3, a3, b3 );
-      }
-      {
-        u64 mS = mD | mN;
-        i32 Dv = vsel( mD, -1, 0 ), Sv = vsel( mS, -1, 0 ), Sn = vsel( mS, 1, 0 );
-        i32 cXe = Dv & (1<<25), cXo = Dv & (1<<24);
-        i32 cZe = vsel( mD, 0, vsel( mN, (1<<25), -(1<<25) ) ), cZo = vsel( mD, 0, vsel( mN, (1<<24), -(1<<24) ) );
-        i32 const nb2e = (i32)fd_opaque( -(2L<<25) ), nb2o = (i32)fd_opaque( -(2L<<24) );
-        i32 const sT = vsel( mD, 0, 2 );
-        _Pragma("unroll") for( int k=0; k<10; k++ ) {
-          i32 cX = (k & 1) ? cXo : cXe, cZ = (k & 1) ? cZo : cZe;
-          i32 A0 = m0.v[k], A1 = m1.v[k], A2 = m2.v[k], A3 = m3.v[k];
-          i32 sA3 = fd_xad( A3, Sv, Sn );
-          i32 z2 = A2 + A2;
-          i32 Z = fd_add3( vsel( mD, A1, z2 ), sA3, cZ );
-          t.X.v[k] = fd_add3( A0 - A1, sA3 & Dv, cX );
-          t.Y.v[k] = fd_add3s( A1, vsel( mD, A3, A0 ), (k & 1) ? nb2o : nb2e );
-          t.Z.v[k] = Z;
-          t.T.v[k] = (i32)((u32)A2 << (u32)sT) - Z;
-        }
-      }
-    } else {
-      fe uZ, uY, uX;
-      fe_mul_fold2w( uZ, t.Z, t.T, uY, t.Z, t.Y );
-      uX = fe_mul_fold1( t.X, t.T );
-      fe xy = fe_add( uX, uY );
-      fe a, b, c, d;
-      fe_sq_fold2w<false, false>( a, xy, b, uY );
-      fe_sq_fold2w<false, true>( c, uX, d, uZ );
-      _Pragma("unroll") for( int k=0; k<10; k++ ) {
-        i32 z = b.v[k] - c.v[k];
-        t.X.v[k] = a.v[k] - b.v[k] - c.v[k];
-        t.Y.v[k] = b.v[k] + c.v[k];
-        t.Z.v[k] = z;
-        t.T.v[k] = d.v[k] - z;
-      }
-    }
-
-    /* advance the op stream (k_dsmp); a finished stream waits in class F */
-    bool const isAA = op == OP_AA, isAB = op == OP_AB, isDb = op == OP_D;
-    {
-      u32 ev = __builtin_amdgcn_ubfe( nh, (pidx & 1u) << 4, 16u );
-      ja -= (u32)isAA; jb -= (u32)isAB;
-      hA = isAA ? (ja ? ev : 0xffffu) : hA;
-      hB = isAB ? (jb ? ev : 0xffffu) : hB;
-    }
-    bool const toAA = isDb && hA != 0xffffu && (hA & 0xffu) == (u32)p;
-    bool const toAB = !toAA && (isDb || isAA) && hB != 0xffffu && (hB & 0xffu) == (u32)p;
-    p -= (int)!(toAA || toAB);
-    u32 const nop = !live ? (u32)OP_EMPTY : toAA ? (u32)OP_AA : toAB ? (u32)OP_AB : (p < 0) ? (u32)OP_F : (u32)OP_D;
-    if( live ) {
-      pool_store_ts( &P.t[0][s], TP_P, t );
-      P.m[s] = make_uint4( si, hA | (hB << 16), ((u32)p & 0xffffu) | (ja << 16) | (jb << 24), nop | (m.w & ~7u) );
-    }
-    /* the new classes, at the owner lanes (rotated), back to slot order */
-    u32 const vF = (u32)__builtin_amdgcn_ds_bpermute( (int)((rkF & 63u) << 2), (int)nop );
-    u32 const vG = (u32)__builtin_amdgcn_ds_bpermute( (int)((rkG & 63u) << 2), (int)nop );
-    u64 const dF = __builtin_amdgcn_ballot_w64( vF == OP_D ), dG = __builtin_amdgcn_ballot_w64( vG == OP_D );
-    u64 const aF = __builtin_amdgcn_ballot_w64( vF == OP_AA || vF == OP_AB ), aG = __builtin_amdgcn_ballot_w64( vG == OP_AA || vG == OP_AB );
-    u64 const d0 = rotl64( sw ? dG : dF, rot ), d1 = rotl64( sw ? dF : dG, rot );
-    u64 const a0 = rotl64( sw ? aG : aF, rot ), a1 = rotl64( sw ? aF : aG, rot );
-    mD0 |= S0 & d0; mA0 |= S0 & a0; mF0 |= S0 & ~d0 & ~a0;
-    mD1 |= S1 & d1; mA1 |= S1 & a1; mF1 |= S1 & ~d1 & ~a1;
-    if( prof && l == 0u ) s_tally[4] += __builtin_amdgcn_s_memrealtime() - tst;
-  }
-  (void)prof;
-}
-
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 k_tile_persist( fd_amd_tile_args_t A ) {
   constexpr ws_layout_t    L = ws_layout_const( 64 );   /* every plane offset an immediate */
@@ -2975,47 +2243,6 @@ k_tile_persist( fd_amd_tile_args_t A ) {
   }
 }
 
-/* The pooled throughput mode as its own kernel (same launch contract as
-   k_tile_persist: wave 0 the scout, the rest take tickets): its pool loop
-   keeps more state across its steps than the chunk loop, and the two in
-   one function spilled. */
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
-k_tile_pool( fd_amd_tile_args_t A ) {
-  constexpr ws_layout_t    L = ws_layout_const( 64 );
-  constexpr tile_scratch_t S = tile_scratch_layout();
-  constexpr u32 O_M = TP_P*10u*16u, O_LIST = O_M + TP_P*16u, O_EVL = O_LIST + 64u*4u, O_PS = O_EVL + 8u*33u*8u, O_END = O_PS + 12u*8u;
-  __shared__ __attribute__((aligned(16))) u64 s_raw[O_END / 8u];
-  __shared__ u64 s_tally[20];
-  fd_amd_tile_dctl_t * D = A.dctl;
-  u32 const l = threadIdx.x;
-  if( blockIdx.x == 0u ) {
-    if( l == 0u ) tile_scout( D, A.hctl, A.watchdog );
-    return;
-  }
-  u32 const xcc = __builtin_amdgcn_s_getreg( 20 | (0 << 6) | (3 << 11) ) % FD_AMD_TILE_MIRRORS;
-  u64 const * mw = &D->mw[xcc].w;
-  u8 * scr = A.scratch + (size_t)blockIdx.x * S.total;
-  if( l < 20u ) s_tally[l] = 0UL;
-  tp_lds_t P;
-  P.t = (int4 (*)[TP_P])s_raw;
-  P.m = (uint4 *)(s_raw + O_M/8u);
-  P.list = (u32 *)(s_raw + O_LIST/8u);
-  P.ps = s_raw + O_PS/8u;
-  __syncthreads();
-  bool const prof = A.prof != 0u;
-  /* prof (diagnostics build): s_tally [0] doubling steps, [1] mixed steps,
-     [2] their lanes, [3] compare steps, [4] ticks in pool steps, [5]
-     ticks asleep, [6] ticks in chunk bodies, [7] fronts put off (region busy) */
-  tp_run( A, scr, S, L, mw, xcc, P, (u64 (*)[33])(s_raw + O_EVL/8u), s_tally, prof );
-  if( l == 0u ) {
-    _Pragma("unroll") for( int q=0; q<4; q++ ) atomicAdd( (unsigned long long *)&D->stat[q], (unsigned long long)s_tally[8 + q] );
-    if( prof ) {
-      _Pragma("unroll") for( int q=0; q<8; q++ ) atomicAdd( (unsigned long long *)&D->prof[q], (unsigned long long)s_tally[q] );
-      _Pragma("unroll") for( int q=0; q<8; q++ ) atomicAdd( (unsigned long long *)&D->prof[8 + q], (unsigned long long)s_tally[12 + q] );
-    }
-  }
-}
-
 #ifdef FD_AMD_DIAG
 /* Diagnostics build only.  Measurement aid: k_tile_persist's chunk pipeline without the host
    hand-off (no tickets, no polling, nothing in mapped memory): wave w runs
@@ -3069,8 +2296,7 @@ int
 fd_amd_launch_tile_persist( fd_amd_tile_args_t const * a, uint32_t waves, hipStream_t stream ) {
   if( waves < 2u ) return -1;
   (void)hipGetLastError();   /* the check below is the launch's own: every earlier call checked its return code */
-  if( a->pool ) hipLaunchKernelGGL( k_tile_pool, dim3(waves), dim3(64), 0, stream, *a );
-  else          hipLaunchKernelGGL( k_tile_persist, dim3(waves), dim3(64), 0, stream, *a );
+  hipLaunchKernelGGL( k_tile_persist, dim3(waves), dim3(64), 0, stream, *a );
   hipError_t const e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;   /* the HIP error, for the caller's message */
 }

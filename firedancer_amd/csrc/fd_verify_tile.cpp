@@ -313,8 +313,6 @@ struct fd_verify_amd_tile {
   fd_amd_tile_dctl_t * dctl;
   fd_amd_tile_dctl_t   d0;          /* its seed (host copy, alive while the copy is queued) */
   uint8_t *            scratch;
-  uint8_t *            pool;       /* pooled throughput mode (k_tile_pool): its buffer, NULL = chunk mode */
-  bool                 pool_on;    /* use it (FD_AMD_TILE_POOL=1 while it is an A/B) */
   ulong                R;          /* ring size (power of 2) */
   ulong                window;     /* frags in flight at most (handed to the GPU, not yet published) */
   uint32_t             waves;      /* grid of a run (the share), fixed at the first run */
@@ -472,9 +470,8 @@ tile_persist_free( fd_verify_amd_tile_t * t ) {
   if( t->res )     (void)hipHostFree( t->res );
   if( t->dctl )    (void)hipFree( t->dctl );
   if( t->scratch ) (void)hipFree( t->scratch );
-  if( t->pool )    (void)hipFree( t->pool );
   t->pst = NULL; t->pdone = NULL; t->hctl = NULL; t->ring = NULL; t->desc = NULL; t->res = NULL;
-  t->dctl = NULL; t->scratch = NULL; t->pool = NULL;
+  t->dctl = NULL; t->scratch = NULL;
   t->persist_ok = false;
 }
 
@@ -539,9 +536,7 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
       hipHostMalloc( (void **)&t->res, 3UL * R * sizeof(uint64_t), hf ) != hipSuccess ||
       hipHostGetDevicePointer( &t->res_dev, t->res, 0 ) != hipSuccess ||
       hipMalloc( (void **)&t->dctl, sizeof(fd_amd_tile_dctl_t) ) != hipSuccess ||
-      hipMalloc( (void **)&t->scratch, waves * fd_amd_tile_scratch_stride() ) != hipSuccess ||
-      ( t->pool_on && ( hipMalloc( (void **)&t->pool, fd_amd_tp_pool_size() ) != hipSuccess ||
-                        fd_amd_tp_pool_init( t->pool, t->pst ) != 0 ) ) ) {   /* stream order: before the first run's kernel */
+      hipMalloc( (void **)&t->scratch, waves * fd_amd_tile_scratch_stride() ) != hipSuccess ) {
     (void)hipGetLastError();
     tile_persist_free( t );
     return FD_ED25519_AMD_ERR_DEVICE;
@@ -578,7 +573,6 @@ fd_verify_amd_tile_new_cfg( fd_verify_amd_tile_cfg_t const * cfg ) {
   if( c.out_frame_cnt > (0xFFFFFFFFUL / FRAME_CHUNKS) ) return NULL;   /* chunk indices are 32-bit */
   fd_verify_amd_tile_t * t = new fd_verify_amd_tile_t();
   t->cfg = c; t->device = c.device; t->batch_max = c.batch_max;
-  { char const * e = getenv( "FD_AMD_TILE_POOL" ); t->pool_on = e && *e == '1'; }
   t->framing = c.framing; t->cus = cus;
   t->tc.init( c.tcache_depth );
   bool ok = hipHostMalloc( (void **)&t->out_base, c.out_frame_cnt * FD_VERIFY_AMD_FRAME_SZ, hipHostMallocMapped ) == hipSuccess &&
@@ -840,9 +834,6 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   for( int x=0; x<FD_AMD_TILE_MIRRORS; x++ ) t->d0.mw[x].w = dbase;
   if( hipMemcpyAsync( t->dctl, &t->d0, sizeof t->d0, hipMemcpyHostToDevice, t->pst ) != hipSuccess )
     return FD_ED25519_AMD_ERR_DEVICE;
-  /* pooled mode: its queues and regions start empty every run */
-  if( t->pool && hipMemsetAsync( t->pool + fd_amd_tp_zero_offset(), 0, fd_amd_tp_zero_size(), t->pst ) != hipSuccess )
-    return FD_ED25519_AMD_ERR_DEVICE;
   fd_amd_tile_args_t A;
   memset( &A, 0, sizeof A );
   A.hctl = (fd_amd_tile_hctl_t *)t->hctl_dev;
@@ -856,7 +847,6 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   A.out  = zc_dev ? t->out_dev : NULL;
   A.dctl = t->dctl;
   A.scratch = t->scratch;
-  A.pool = t->pool;
   A.watchdog = 500000000UL;   /* 5 s of s_memrealtime (100 MHz) without a heartbeat */
   A.txn = txn ? 1u : 0u;
 #ifdef FD_AMD_DIAG
@@ -1281,16 +1271,6 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   ulong st[4] = { 0, 0, 0, 0 };
   if( !t->pending && ( hipMemcpyAsync( st, t->dctl->stat, sizeof st, hipMemcpyDeviceToHost, t->pst ) != hipSuccess ||
                        hipStreamSynchronize( t->pst ) != hipSuccess ) ) rc = FD_ED25519_AMD_ERR_DEVICE;
-#ifdef FD_AMD_DIAG
-  if( A.prof && !t->pending ) {   /* diagnostics build: the kernel's per-wave tallies, summed */
-    ulong pf[16] = { 0 };
-    if( hipMemcpy( pf, t->dctl->prof, sizeof pf, hipMemcpyDeviceToHost ) == hipSuccess ) {
-      fprintf( stderr, "tile_prof %s", t->pool ? "pool" : "chunk" );
-      for( int q=0; q<16; q++ ) fprintf( stderr, " %lu", pf[q] );
-      fprintf( stderr, "\n" );
-    }
-  }
-#endif
   if( __atomic_load_n( &H->kerr, __ATOMIC_ACQUIRE ) ) {
     fprintf( stderr, "fd_verify_amd_tile_run: the tile kernel's watchdog fired (no host heartbeat for 5 s)\n" );
     rc = FD_ED25519_AMD_ERR_DEVICE;
