@@ -9,10 +9,11 @@ k_decomp -> the double-scalar multiply: k_ai + k_dsmp + k_fin at this size)
 over one batch of n synthetic signatures (2^20 single-signer signatures,
 200-byte Solana-txn-sized messages, fresh random keypairs), with the inputs
 already resident in HBM when the timed region starts.  Consecutive steps
-alternate between --streams (default 3) stream/workspace sets: three
-batches in flight (measured +2 % over two: a batch's multiply starts in the
-previous one's drain and the fronts queue behind fewer multiplies;
-profiles/r02_k_dsmp_pool_ab.txt).  For N > 1 (launched by torch.distributed.run) every rank verifies
+alternate between --streams (default 4) stream/workspace sets: four
+batches in flight, one per HIP hardware queue (three measured +2 % over two:
+a batch's multiply starts in the previous one's drain and the fronts queue
+behind fewer multiplies, profiles/r02_k_dsmp_pool_ab.txt; four +1.0 % over
+three and six -0.5 %, interleaved on one box, profiles/r05_ab_streams.txt).  For N > 1 (launched by torch.distributed.run) every rank verifies
 its own batch of n signatures on its own GPU -- signatures are independent,
 so there is no data-path collective (weak scaling); gloo is used only for
 the start/stop barriers and the max-over-ranks of the time.
@@ -42,7 +43,7 @@ import numpy as np
 
 # HIP's hardware-queue count is left as the process finds it (the box
 # default is 4, HIP's own): the streaming tile runs one persistent kernel on
-# one stream, and the resident batches use --streams (3) streams.  The value
+# one stream, and the resident batches use --streams (4) streams.  The value
 # in effect is reported in the JSON line (config.hip_hw_queues).
 HW_QUEUES = os.environ.get("GPU_MAX_HW_QUEUES", "default (4)")
 
@@ -75,7 +76,7 @@ def parse():
     ap.add_argument("--msg-sz", type=int, default=200)
     ap.add_argument("--dsm-kernel", choices=("default", "k_dsm", "k_dsmp"), default="default",
                     help="throughput double-scalar-mult kernel (A/B; default: the library's size rule)")
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--streams", type=int, default=4,
                     help="batches in flight (consecutive steps alternate streams / workspaces)")
     ap.add_argument("--total-sigs", type=int, default=1 << 24,
                     help="txn workload: signatures over all ranks (strong scaling)")

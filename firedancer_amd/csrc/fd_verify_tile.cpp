@@ -1335,6 +1335,68 @@ fd_verify_amd_tile_run( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcac
 /* ------------------------------------------------------------------ */
 /* streaming benchmark and end-to-end check: producer -> tile -> consumer */
 
+/* The `want` quietest CPUs of `allowed` (CPU 0 excluded: it takes most
+   of the machine's interrupts): per-CPU busy time from /proc/stat over
+   ~30 ms, then one CPU per physical core while there are enough.  The
+   bench box is one cgroup on a shared machine, so the spinning threads
+   would otherwise land on CPUs other tenants keep busy, and a thread
+   preempted for 1-2 ms shows up as a latency tail (profiles/
+   r05_bench_*: producer_late_max 1.7 ms in one paced run).  Falls back to
+   the highest-numbered CPUs when /proc/stat is unreadable.  Returns the
+   number of CPUs written to out. */
+static int
+tile_quiet_cpus( cpu_set_t const * allowed, int want, int * out ) {
+  auto snap = []( std::vector<unsigned long long> & busy, std::vector<unsigned long long> & tot ) -> bool {
+    FILE * f = fopen( "/proc/stat", "r" );
+    if( !f ) return false;
+    char line[512];
+    while( fgets( line, sizeof line, f ) ) {
+      int c; unsigned long long v[8] = { 0 };
+      if( strncmp( line, "cpu", 3 ) || line[3] < '0' || line[3] > '9' ) continue;
+      if( sscanf( line + 3, "%d %llu %llu %llu %llu %llu %llu %llu %llu", &c, v, v+1, v+2, v+3, v+4, v+5, v+6, v+7 ) < 5 ) continue;
+      if( c < 0 || c >= CPU_SETSIZE ) continue;
+      if( (size_t)c >= busy.size() ) { busy.resize( (size_t)c + 1, 0ULL ); tot.resize( (size_t)c + 1, 0ULL ); }
+      unsigned long long t = 0; for( int k=0; k<8; k++ ) t += v[k];
+      tot[c] = t; busy[c] = t - v[3] - v[4];   /* all but idle and iowait */
+    }
+    fclose( f );
+    return true;
+  };
+  std::vector<unsigned long long> b0, t0, b1, t1;
+  bool ok = snap( b0, t0 );
+  if( ok ) { struct timespec ts = { 0, 30000000L }; nanosleep( &ts, NULL ); ok = snap( b1, t1 ); }
+  std::vector<std::pair<double, int>> cand;
+  for( int c=CPU_SETSIZE-1; c>0; c-- ) {
+    if( !CPU_ISSET( c, allowed ) ) continue;
+    double load = 0.0;
+    if( ok && (size_t)c < b1.size() && (size_t)c < b0.size() && t1[c] > t0[c] )
+      load = (double)(b1[c] - b0[c]) / (double)(t1[c] - t0[c]);
+    cand.emplace_back( load, c );
+  }
+  std::stable_sort( cand.begin(), cand.end(), []( std::pair<double, int> const & a, std::pair<double, int> const & b ) {
+    return a.first < b.first; } );   /* stable: ties keep the highest-numbered first */
+  auto core = []( int c ) -> int {   /* the first CPU listed as c's SMT sibling (its core), or c */
+    char pth[128]; snprintf( pth, sizeof pth, "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", c );
+    FILE * f = fopen( pth, "r" ); int k = c;
+    if( f ) { if( fscanf( f, "%d", &k ) != 1 ) k = c; fclose( f ); }
+    return k;
+  };
+  int n = 0;
+  std::vector<int> cores;
+  for( int pass=0; pass<2 && n<want; pass++ ) {   /* pass 0: one CPU per core; pass 1: fill with siblings */
+    for( auto const & x : cand ) {
+      if( n >= want ) break;
+      int const c = x.second, k = core( c );
+      bool used = false;
+      for( int q=0; q<n; q++ ) if( out[q] == c ) used = true;
+      if( used ) continue;
+      if( !pass && std::find( cores.begin(), cores.end(), k ) != cores.end() ) continue;
+      out[n++] = c; cores.push_back( k );
+    }
+  }
+  return n;
+}
+
 /* Move every other thread of this process off the given CPUs (those
    whose mask would not become empty); returns the threads moved and their
    old masks. */
@@ -1410,16 +1472,16 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   /* the four spinning threads (producer, tile, its publisher, consumer)
      each get a CPU of their own from the process's allowed set, so the
      scheduler does not stack them (the saturated rate otherwise varies run
-     to run): the highest-numbered allowed CPUs, away from CPU 0, which
-     takes most of the machine's interrupts (tile passes of 1-5 ms and p99
-     spikes were seen with the tile thread on CPU 0) */
+     to run): the quietest allowed CPUs, one per core, away from CPU 0,
+     which takes most of the machine's interrupts (tile passes of 1-5 ms
+     and p99 spikes were seen with the tile thread on CPU 0) */
   cpu_set_t allowed, saved; CPU_ZERO( &allowed ); CPU_ZERO( &saved );
   int cpus[5] = { -1, -1, -1, -1, -1 }, ncpu = 0;
   bool pin = !sched_getaffinity( 0, sizeof allowed, &allowed ) && CPU_COUNT( &allowed ) >= 5;
   if( pin ) {
     saved = allowed;
     int const want = CPU_COUNT( &allowed ) >= 6 ? 5 : 4;   /* the fifth: copy mode's helper */
-    for( int c=CPU_SETSIZE-1; c>0 && ncpu<want; c-- ) if( CPU_ISSET( c, &allowed ) ) cpus[ncpu++] = c;
+    ncpu = tile_quiet_cpus( &allowed, want, cpus );
     pin = ncpu >= 4;
   }
   auto pin_to = [&]( int k ) {
