@@ -246,11 +246,9 @@ def dsm_in_pipeline(st, ms_per_step, stage_ms, n):
 
 def pmc_summary_path():
     """The newest round's committed PMC summary (profiles/rNN_pmc_latest.json)."""
-    for r in ("r03", "r02", "r01"):
-        path = os.path.join(ROOT, "profiles", r + "_pmc_latest.json")
-        if os.path.exists(path):
-            return path
-    return None
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_latest.json")))
+    return paths[-1] if paths else None
 
 
 def pmc_traffic(kernel, n):

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-5 measurement set on one GPU box (each step time-limited, chained): the default bench line
 # (headline, stream_tile rows, TXN row, CPU baseline), rocprof kernel stats and PMC passes of the
-# headline kernels, the config-4 transaction bench.
+# headline kernels (summarised for the bench's traffic field), the config-4 transaction bench, a
+# 3-batch kernel trace.
 # usage: tools/r05_final_measure.sh <tag>
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -13,6 +14,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
   --streams 1 --no-cpu --no-latency --no-stream --no-host-fed > $O/prof.log 2>&1 || { echo "rocprof failed"; tail -20 $O/prof.log; exit 1; }
 echo "rocprof ok"
 bash tools/prof_pmc.sh $O/pmc > $O/pmc.log 2>&1 || { echo "pmc failed"; tail -20 $O/pmc.log; exit 1; }
+python3 tools/pmc_summary.py $O/pmc 1048576 > $O/pmc_summary.json || { echo "pmc summary failed"; exit 1; }
 echo "pmc ok"
 timeout -k 10 300 python3 bench.py --workload txn --steps 5 --warmup 1 --detail $O/txn_detail.json > $O/txn.json 2> $O/txn.err || { echo "txn bench failed"; tail -20 $O/txn.err; exit 1; }
 echo "txn ok"
