@@ -1444,7 +1444,10 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
     depth_min = std::max( depth_min, tile_window( &wc ) + 4096UL );
   }
   ulong depth = 1UL; while( depth < depth_min ) depth <<= 1;
-  ulong out_depth = 1UL; while( out_depth < 2UL*batch_max + 1024UL ) out_depth <<= 1;
+  /* output depth: the reference's verify -> dedup link (receive_buffer_size
+     16384, fdctl/config/default.toml:241, frank.rs:88), or two batches when
+     larger: room for a consumer descheduled for a few hundred us */
+  ulong out_depth = 1UL; while( out_depth < std::max( 2UL*batch_max + 1024UL, 16384UL ) ) out_depth <<= 1;
   ulong const frame = FD_VERIFY_AMD_FRAME_SZ, frame_c = FRAME_CHUNKS;
   /* Data region: either every pool frame once (what a NIC would have
      DMA'd; the producer publishes metadata only, so the bench measures the
@@ -1481,8 +1484,13 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   if( pin ) {
     saved = allowed;
     int const want = CPU_COUNT( &allowed ) >= 6 ? 5 : 4;   /* the fifth: copy mode's helper */
-    ncpu = tile_quiet_cpus( &allowed, want, cpus );
+    char const * pk = getenv( "FD_AMD_BENCH_CPU_PICK" );      /* A/B: "top" = the round-4 rule */
+    if( pk && !strcmp( pk, "top" ) ) { for( int c=CPU_SETSIZE-1; c>0 && ncpu<want; c-- ) if( CPU_ISSET( c, &allowed ) ) cpus[ncpu++] = c; }
+    else ncpu = tile_quiet_cpus( &allowed, want, cpus );
     pin = ncpu >= 4;
+    static int said = 0;
+    if( !said ) { said = 1; fprintf( stderr, "fd_verify_amd_bench_stream: spinning threads on CPUs %d %d %d %d %d\n",
+                                     cpus[0], cpus[1], cpus[2], cpus[3], cpus[4] ); }
   }
   auto pin_to = [&]( int k ) {
     if( !pin ) return;
@@ -1499,6 +1507,9 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   fd_verify_amd_tile_cfg_default( &cfg );
   cfg.device = device; cfg.batch_max = batch_max; cfg.batch_wait_ns = batch_wait_ns; cfg.tcache_depth = 0UL;
   cfg.waves = waves;
+  /* output frames: the frags in flight, a pass, and a consumer that lags by
+     up to the output depth (a frame is reused once out_fseq passed it) */
+  cfg.out_frame_cnt = tile_window( &cfg ) + out_depth + batch_max + 4096UL;
   cfg.framing = txn ? FD_VERIFY_AMD_FRAMING_TXN : FD_VERIFY_AMD_FRAMING_PUB_SIG_MSG;
   cfg.chunk_mode = (flags & FD_VERIFY_AMD_BENCH_CHUNK_LAT) ? FD_VERIFY_AMD_CHUNK_LATENCY
                  : (flags & FD_VERIFY_AMD_BENCH_CHUNK_THR) ? FD_VERIFY_AMD_CHUNK_THROUGHPUT : FD_VERIFY_AMD_CHUNK_AUTO;
