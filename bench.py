@@ -109,6 +109,17 @@ def parse():
 
 # ---------------------------------------------------------------- host facts
 
+def cgroup_throttle():
+    """(nr_throttled, throttled_usec) of this process's cgroup (v2 cpu.stat),
+    or None: a paced tile run that the CPU quota throttled shows its stalls
+    here, not in the tile."""
+    try:
+        st = dict(ln.split() for ln in open("/sys/fs/cgroup/cpu.stat") if ln.strip())
+        return int(st.get("nr_throttled", 0)), int(st.get("throttled_usec", 0))
+    except (OSError, ValueError):
+        return None
+
+
 def host_cores():
     """Cores this process may use: the affinity set, capped by a cgroup CPU
     quota and by the host share the pool grants a one-GPU box
@@ -555,8 +566,12 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
 
     def paced(bmax, zc, rate):
         nf = int(max(50000, rate * args.paced_seconds))
+        th0 = cgroup_throttle()
         r = tango.bench_stream(local, bmax, 0, *pool, nf, rate=rate, zero_copy=zc)
+        th1 = cgroup_throttle()
         return {"offered_frags_per_s": rate, "frags_per_s": r["frags_per_s"], "frags": nf,
+                "cgroup_throttled": None if th0 is None or th1 is None else
+                {"periods": th1[0] - th0[0], "us": th1[1] - th0[1]},
                 "p50_us": r["p50_ns"] / 1e3, "p99_us": r["p99_ns"] / 1e3,
                 "p99_over_p50": r["p99_ns"] / max(r["p50_ns"], 1.0),
                 "all_frags": {"p50_us": r["all_p50_ns"] / 1e3, "p99_us": r["all_p99_ns"] / 1e3,
