@@ -1439,8 +1439,10 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
      bound the stream instead of the tile); the rewriting modes keep 8
      batches (their dcache is sized past the depth) */
   ulong depth_min = 8UL*batch_max + 1024UL;
+  ulong window = 0UL;                                          /* A/B: the tile's window (0 = tile_window's rule) */
+  { char const * w = getenv( "FD_AMD_BENCH_WINDOW" ); if( w && *w ) window = strtoul( w, NULL, 0 ); }
   if( !writes ) {
-    fd_verify_amd_tile_cfg_t wc; fd_verify_amd_tile_cfg_default( &wc ); wc.batch_max = batch_max;
+    fd_verify_amd_tile_cfg_t wc; fd_verify_amd_tile_cfg_default( &wc ); wc.batch_max = batch_max; wc.window = window;
     depth_min = std::max( depth_min, tile_window( &wc ) + 4096UL );
   }
   ulong depth = 1UL; while( depth < depth_min ) depth <<= 1;
@@ -1506,7 +1508,7 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   fd_verify_amd_tile_cfg_t cfg;
   fd_verify_amd_tile_cfg_default( &cfg );
   cfg.device = device; cfg.batch_max = batch_max; cfg.batch_wait_ns = batch_wait_ns; cfg.tcache_depth = 0UL;
-  cfg.waves = waves;
+  cfg.waves = waves; cfg.window = window;
   /* output frames: the frags in flight, a pass, and a consumer that lags by
      up to the output depth (a frame is reused once out_fseq passed it) */
   cfg.out_frame_cnt = tile_window( &cfg ) + out_depth + batch_max + 4096UL;
