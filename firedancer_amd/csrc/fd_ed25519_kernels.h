@@ -91,17 +91,13 @@ typedef struct {
 } fd_amd_tile_hctl_t;
 /* device control block (zeroed by the host before each launch) */
 #define FD_AMD_TILE_MIRRORS (8)
-#define FD_AMD_TILE_SIMD_KEYS (8192)   /* XCC 3 | SE 3 | SH 1 | CU 4 | SIMD 2 bits */
-typedef struct { uint64_t w; uint64_t tk; uint64_t pad[6]; } fd_amd_tile_mirror_t;
+typedef struct { uint64_t w; uint64_t pad[7]; } fd_amd_tile_mirror_t;
 typedef struct {
   uint64_t             ticket;  uint64_t pad0[7];   /* next chunk ticket (one atomic add per chunk) */
-  fd_amd_tile_mirror_t mw[FD_AMD_TILE_MIRRORS];     /* per XCD: w = descriptor head | heartbeat << 48 | err << 62 | stop << 63,
-                                                       tk = the ticket counter as the scout last read it */
+  fd_amd_tile_mirror_t mw[FD_AMD_TILE_MIRRORS];     /* per XCD: descriptor head | heartbeat << 48 | err << 62 | stop << 63 */
   uint64_t             done;    uint64_t pad1[7];   /* chunks finished (one atomic add per chunk; the scout mirrors it) */
-  uint64_t             stat[6];                     /* chunks in latency mode, in throughput mode; frags in each;
-                                                       chunks taken by second waves of a SIMD; second waves */
+  uint64_t             stat[4];                     /* chunks in latency mode, in throughput mode; frags in each */
   uint64_t             prof[8];                     /* diagnostics build (FD_AMD_DIAG, args.prof): summed ticks gather, decomp, DSM, results, wait, fence, prep */
-  uint32_t             simd[FD_AMD_TILE_SIMD_KEYS]; /* waves that arrived on each SIMD (args.roles) */
 } fd_amd_tile_dctl_t;
 typedef struct {
   fd_amd_tile_hctl_t *       hctl;     /* device address of the mapped control words */
@@ -119,8 +115,6 @@ typedef struct {
   uint64_t                   watchdog; /* s_memrealtime ticks (100 MHz) without a host heartbeat before the kernel gives up */
   uint32_t                   prof;     /* diagnostics build only: sum per-phase time stamps into dctl->prof */
   uint32_t                   txn;      /* TXN framing: entries are wire transactions, results per transaction */
-  uint32_t                   roles;    /* 1: a SIMD's second wave claims only descriptors no wave waits for */
-  uint32_t                   pad;
 } fd_amd_tile_args_t;
 size_t fd_amd_tile_scratch_stride( void );
 /* waves: grid size (wave 0 is the scout that mirrors the host words) */

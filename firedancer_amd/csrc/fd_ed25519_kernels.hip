@@ -1934,7 +1934,7 @@ __device__ __forceinline__ void
 #endif
 tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog ) {
   __builtin_amdgcn_s_setprio( 3 );   /* beside the workers' aged chunks on its SIMD */
-  u64 word = ld_dev64( &D->mw[0].w ), tkw = ~0UL, lastb = ~0UL, beat = 0UL;
+  u64 word = ld_dev64( &D->mw[0].w ), lastb = ~0UL, beat = 0UL;
   u64 tb = __builtin_amdgcn_s_memrealtime(), tpub = tb, tclk = tb;
   st_sys64( &H->gclock, tb );
   for( ;; ) {
@@ -1953,10 +1953,9 @@ tile_scout( fd_amd_tile_dctl_t * D, fd_amd_tile_hctl_t * H, u64 watchdog ) {
        waiting waves' own watchdog quiet) */
     if( now - tpub > 1000UL && now - tb < 1000UL ) { beat++; tpub = now; }
     u64 w = (h & ((1UL << 48) - 1UL)) | ((beat & 0x3fffUL) << 48) | (dead ? TILE_MW_ERR : 0UL) | (st ? TILE_MW_STOP : 0UL);
-    u64 const tk = ld_dev64( &D->ticket );   /* for second waves: head > tk = descriptors no wave waits for */
-    if( w != word || tk != tkw ) {
-      word = w; tkw = tk;
-      _Pragma("unroll") for( int x=0; x<FD_AMD_TILE_MIRRORS; x++ ) { st_dev64( &D->mw[x].w, w ); st_dev64( &D->mw[x].tk, tk ); }
+    if( w != word ) {
+      word = w;
+      _Pragma("unroll") for( int x=0; x<FD_AMD_TILE_MIRRORS; x++ ) st_dev64( &D->mw[x].w, w );
     }
     if( st || dead ) break;
     __builtin_amdgcn_s_sleep( 2 );
@@ -2178,26 +2177,11 @@ k_tile_persist( fd_amd_tile_args_t A ) {
   u32 const xcc = __builtin_amdgcn_s_getreg( 20 | (0 << 6) | (3 << 11) ) % FD_AMD_TILE_MIRRORS;
   u64 const * mw = &D->mw[xcc].w;
   u8 * scr = A.scratch + (size_t)blockIdx.x * S.total;
-  /* The wave's role.  The tile's waves fill two slots per SIMD, and two
-     chunks on one SIMD each run at about half speed.  With A.roles the first
-     wave to arrive on a SIMD takes a ticket whenever it is idle; the second
-     claims only descriptors that no wave is waiting for (a backlog), so below
-     saturation chunks land on SIMDs of their own, and at saturation both
-     slots stay busy as before. */
-  bool second = false;
-  if( A.roles ) {
-    u32 const hw  = __builtin_amdgcn_s_getreg( 4 | (0 << 6) | (31 << 11) );   /* HW_REG_HW_ID */
-    u32 const key = (xcc & 7u) << 10 | ((hw >> 13) & 7u) << 7 | ((hw >> 12) & 1u) << 6 | ((hw >> 8) & 15u) << 2 | ((hw >> 4) & 3u);
-    u32 r = 0u;
-    if( l == 0u ) r = atomicAdd( &D->simd[key], 1u );
-    second = __builtin_amdgcn_readfirstlane( (int)r ) != 0;
-  }
   /* per-wave tallies in LDS, not registers (the DSM bodies want every VGPR):
      [0..7] diagnostics build (A.prof) gather, front, DSM, results, wait,
-     fence, -, -; [8..11] latency chunks, throughput chunks, their frags;
-     [12] chunks taken as a second wave */
-  __shared__ u64 s_tally[13];
-  if( l < 13u ) s_tally[l] = 0UL;
+     fence, -, -; [8..11] latency chunks, throughput chunks, their frags */
+  __shared__ u64 s_tally[12];
+  if( l < 12u ) s_tally[l] = 0UL;
   u64 * const pt = s_tally;
   /* A run-time flag (the host sets it only in the diagnostics build), not a
      compile-time constant: with the profiling branches folded away the
@@ -2212,42 +2196,13 @@ k_tile_persist( fd_amd_tile_args_t A ) {
 #endif
   for( ;; ) {
     u64 t = 0;
-    u64 t0 = __builtin_amdgcn_s_memrealtime(), tw = t0, last = ~0UL;
-    bool go = false;
-    if( second ) {
-      /* a backlog in the mirror (head > tk) -> claim exactly ticket tk, or
-         the value the failed CAS returned if that is below the head too: a
-         second wave never holds a ticket for a descriptor not yet published */
-      for( ;; ) {
-        u64 w = 0UL, tk = 0UL;
-        if( l == 0u ) { w = ld_dev64( mw ); tk = ld_dev64( mw + 1 ); }
-        w = rfl64( w ); tk = rfl64( tk );
-        if( w & TILE_MW_ERR ) break;
-        u64 const h = TILE_MW_HEAD( w );
-        if( h > tk ) {
-          u64 got = ~0UL;
-          if( l == 0u ) {
-            unsigned long long * const tp = (unsigned long long *)&D->ticket;
-            u64 const o = atomicCAS( tp, tk, tk + 1UL );
-            if( o == tk ) got = tk;
-            else if( o < h && atomicCAS( tp, o, o + 1UL ) == o ) got = o;
-          }
-          got = rfl64( got );
-          if( got != ~0UL ) { t = got; go = true; break; }
-        }
-        if( w & TILE_MW_STOP ) break;                  /* the primaries drain what is left */
-        u64 const now = __builtin_amdgcn_s_memrealtime();
-        if( w != last ) { last = w; tw = now; }
-        else if( now - tw > A.watchdog ) break;
-        for( u32 z = 0; z < 32u; z++ ) __builtin_amdgcn_s_sleep( 4 );
-      }
-    } else {
-      if( l == 0u ) t = atomicAdd( (unsigned long long *)&D->ticket, 1ULL );
-      t = rfl64( t );
-    }
+    if( l == 0u ) t = atomicAdd( (unsigned long long *)&D->ticket, 1ULL );
+    t = rfl64( t );
     /* wait for descriptor t: poll the mirror, backing off with the
        distance to the head (the next in line polls every ~0.2 us) */
-    for( ; !second; ) {
+    u64 t0 = __builtin_amdgcn_s_memrealtime(), tw = t0, last = ~0UL;
+    bool go = false;
+    for( ;; ) {
       u64 const w = rfl64( l == 0u ? ld_dev64( mw ) : 0UL );
       if( TILE_MW_HEAD( w ) > t ) { go = true; break; }
       if( w & (TILE_MW_ERR | TILE_MW_STOP) ) break;
@@ -2278,13 +2233,12 @@ k_tile_persist( fd_amd_tile_args_t A ) {
     if( prof && !l ) pt[5] += __builtin_amdgcn_s_memrealtime() - tf;
     if( take && take <= 64u ) tile_chunk( A, c, take, e8, scr, L, S, bi, evl, pt, tc );
     if( !l ) {
-      s_tally[e8 ? 8 : 9] += 1UL; s_tally[e8 ? 10 : 11] += take; s_tally[12] += second ? 1UL : 0UL;
+      s_tally[e8 ? 8 : 9] += 1UL; s_tally[e8 ? 10 : 11] += take;
       atomicAdd( (unsigned long long *)&D->done, 1ULL );   /* progress, mirrored to the host by the scout */
     }
   }
   if( l == 0u ) {
-    _Pragma("unroll") for( int q=0; q<5; q++ ) atomicAdd( (unsigned long long *)&D->stat[q], (unsigned long long)s_tally[8 + q] );
-    if( second ) atomicAdd( (unsigned long long *)&D->stat[5], 1ULL );
+    _Pragma("unroll") for( int q=0; q<4; q++ ) atomicAdd( (unsigned long long *)&D->stat[q], (unsigned long long)s_tally[8 + q] );
     if( prof ) { _Pragma("unroll") for( int q=0; q<8; q++ ) atomicAdd( (unsigned long long *)&D->prof[q], (unsigned long long)pt[q] ); }
   }
 }

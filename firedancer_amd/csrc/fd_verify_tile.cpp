@@ -329,7 +329,6 @@ struct fd_verify_amd_tile {
      stopped at the window, the output frames, batch_max staged, or the
      STAGE_PASS bound; copy blocks the stager re-copied (helper stalls) */
   ulong                n_pass, n_hand, n_stop_window, n_stop_frames, n_stop_bmax, n_stop_pass, n_steal;
-  ulong                n_second_chunks, n_second_waves;   /* the last run: chunks second waves took, second waves */
   volatile int         started;    /* the current run's kernel wrote its first clock word */
 };
 
@@ -850,7 +849,6 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   A.scratch = t->scratch;
   A.watchdog = 500000000UL;   /* 5 s of s_memrealtime (100 MHz) without a heartbeat */
   A.txn = txn ? 1u : 0u;
-  { char const * e = getenv( "FD_AMD_TILE_ROLES" ); A.roles = (e && *e == '1') ? 1u : 0u; }   /* A/B only (profiles/r05_tile_roles_ab.txt) */
 #ifdef FD_AMD_DIAG
   { char const * e = getenv( "FD_AMD_TILE_PROF" ); A.prof = e && *e && *e != '0'; }   /* diagnostics build only */
 #endif
@@ -1270,7 +1268,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
                gc_host ? 1e-6 * (double)(t0 - gc_host) : -1.0, (ulong)__atomic_load_n( &H->gdone, __ATOMIC_ACQUIRE ),
                t->desc_seq - dbase, __atomic_load_n( &H->kerr, __ATOMIC_ACQUIRE ) );
   }
-  ulong st[6] = { 0, 0, 0, 0, 0, 0 };
+  ulong st[4] = { 0, 0, 0, 0 };
   if( !t->pending && ( hipMemcpyAsync( st, t->dctl->stat, sizeof st, hipMemcpyDeviceToHost, t->pst ) != hipSuccess ||
                        hipStreamSynchronize( t->pst ) != hipSuccess ) ) rc = FD_ED25519_AMD_ERR_DEVICE;
   if( __atomic_load_n( &H->kerr, __ATOMIC_ACQUIRE ) ) {
@@ -1295,7 +1293,6 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   t->pass_max_ns = pass_max;
   t->n_pass = n_pass; t->n_hand = n_hand; t->n_stop_window = n_stop_window; t->n_stop_frames = n_stop_frames;
   t->n_stop_bmax = n_stop_bmax; t->n_stop_pass = n_stop_pass; t->n_steal = n_steal;
-  t->n_second_chunks = st[4]; t->n_second_waves = st[5];
   __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
   if( in_fseq ) __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE );
   t->out_seq_end = r.out_seq;
@@ -1643,14 +1640,12 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   ulong const pass_max = tile->pass_max_ns;
   ulong const stg[6] = { tile->n_pass, tile->n_hand, tile->n_stop_window, tile->n_stop_frames, tile->n_stop_bmax, tile->n_stop_pass };
   ulong const n_steal = tile->n_steal;
-  ulong const n_sec_w = tile->n_second_waves, n_sec_c = tile->n_second_chunks;
   fd_verify_amd_tile_delete( tile );
   free( dcache );
   if( rc ) return rc;
   ulong n = std::min( (ulong)diag.out_cnt, frag_cnt );
-  for( int k=0; k<44; k++ ) out[k] = 0.0;
+  for( int k=0; k<42; k++ ) out[k] = 0.0;
   out[41] = (double)n_steal;
-  out[42] = (double)n_sec_w; out[43] = (double)n_sec_c;
   if( t90 > t10 && t10 && s90 > s10 ) out[40] = (double)(s90 - s10) / ((double)(t90 - t10) * 1e-9);
   /* decomposition (before lat is sorted: the samples are per published frag) */
   /* paced runs: percentiles over the steady state (n_st samples); the

@@ -173,7 +173,7 @@ def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, bl
     """fd_verify_amd_bench_stream: producer (rate frags/s, 0 = saturate) -> tile -> consumer; returns
     dict(frags_per_s, p50_ns, p99_ns, p999_ns, mean_batch, published, sv_filt, ovrn, mismatches, checked).
     With expect_err/expect_tag (per pool entry) the consumer checks every published frag."""
-    out = (ctypes.c_double * 44)()
+    out = (ctypes.c_double * 42)()
     p = [np.ascontiguousarray(a) for a in (pub, sig, msg_off, msg_sz, blob)]
     ee = np.ascontiguousarray(expect_err, np.int8) if expect_err is not None else None
     et = np.ascontiguousarray(expect_tag, np.uint64) if expect_tag is not None else None
@@ -194,6 +194,5 @@ def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, bl
             "tile_pass_max_ns", "consumer_gap_max_ns", "cut_p50_ns", "cut_p99_ns", "queue_p50_ns", "queue_p99_ns",
             "service_p50_ns", "service_p99_ns", "publish_p50_ns", "publish_p99_ns", "input_p50_ns", "input_p99_ns",
             "service_lat_chunk_p50_ns", "service_thr_chunk_p50_ns", "mode_switches", "traced", "_reserved", "passes",
-            "hand_offs", "stop_window", "stop_frames", "stop_batch_max", "stop_pass_bound", "all_p50_ns", "all_p99_ns", "steady_frags_per_s", "copy_steals",
-            "second_waves", "second_chunks")
+            "hand_offs", "stop_window", "stop_frames", "stop_batch_max", "stop_pass_bound", "all_p50_ns", "all_p99_ns", "steady_frags_per_s", "copy_steals")
     return dict(zip(keys, list(out)))

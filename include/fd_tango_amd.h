@@ -413,10 +413,8 @@ fd_verify_amd_tile_pack( uint const * slots, ulong cnt, int thr, ulong * nsl );
    frag.  out[40] (check mode) = the steady-state rate: input frags between
    10 % and 90 % of the run over the time the consumer took from one to the
    other (out[0] includes the run's ramp and drain); out[41] = copy blocks
-   the tile's stager re-copied because its helper had stalled; out[42] /
-   out[43] = the kernel's second waves of a SIMD and the chunks they took
-   (a second wave claims only descriptors no wave waits for).  out holds
-   44 doubles.
+   the tile's stager re-copied because its helper had stalled.  out holds
+   42 doubles.
    Threads: producer, tile, the tile's publisher and consumer each pinned
    to a CPU of their own when the process may use 5 or more (else unpinned,
    publisher inline); copy mode adds the tile's copy helper on a fifth CPU

@@ -4,6 +4,7 @@ takes tickets as it goes idle).  Each round runs both settings in their own
 process: a saturated run (every frag checked), then paced runs at 50 % and
 80 % of that run's rate, zero copy; JSON lines with the rate, p50 / p99,
 the service / queue / publish-wait tails and the second waves' share.
+Runs against commit 8857e83 (the roles code was removed after it; profiles/r05_tile_roles_ab.txt).
 usage: python tools/r05_roles_ab.py OUT.jsonl [rounds] [bmax,...] [paced_seconds]"""
 import hashlib
 import json
