@@ -6,7 +6,7 @@ tags.  Reports whole-run and steady rates and the mean fill of throughput
 chunks (frags per 64-lane chunk).
 usage: python tools/r05_tile_ab.py OUT.jsonl LIB[,LIB...] [rounds] [frags] [bmax,...]
        LIB "" = the product library; NAME=VALUE = the product library with that
-       environment variable set (e.g. FD_AMD_TILE_POOL=1)."""
+       environment variable set (e.g. FD_AMD_BENCH_WINDOW=524288)."""
 import hashlib
 import json
 import os
