@@ -10,7 +10,8 @@ over one batch of n synthetic signatures (2^20 single-signer signatures,
 200-byte Solana-txn-sized messages, fresh random keypairs), with the inputs
 already resident in HBM when the timed region starts.  Consecutive steps
 alternate between --streams (default 4) stream/workspace sets: four
-batches in flight, one per HIP hardware queue (three measured +2 % over two:
+batches in flight (the runtime maps them onto two of its hardware queues;
+GPU_MAX_HW_QUEUES=8 did not help, profiles/r05_ab_hwq.txt; three measured +2 % over two:
 a batch's multiply starts in the previous one's drain and the fronts queue
 behind fewer multiplies, profiles/r02_k_dsmp_pool_ab.txt; four +1.0 % over
 three and six -0.5 %, interleaved on one box, profiles/r05_ab_streams.txt).  For N > 1 (launched by torch.distributed.run) every rank verifies
