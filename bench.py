@@ -757,7 +757,11 @@ def stream_node(local, pub, sig, off, sz, blob, args, rank, world, dist):
         node_cpus[x["numa"]] = sorted(set(node_cpus.get(x["numa"], [])) | set(x["cpus"]))
     plans, plan_tot = node_plan(numa, node_cpus, 16384, zero_copy=True, cpu_quota=keys[0]["quota"])
     cpus = plans[rank]["cpus"]
-    if len(cpus) >= 5:
+    # the rank's threads stay inside its slice: with 5 or more CPUs the tile
+    # bench pins its spinning threads there; below that (8 ranks in a 16-CPU
+    # quota get 2 each) they share the slice unpinned, publishing inline,
+    # rather than every rank picking the same quiet CPUs of the whole machine
+    if cpus:
         os.sched_setaffinity(0, cpus)
     _, share = peer_slot([x["dev"] for x in keys], rank)
     waves = 0
