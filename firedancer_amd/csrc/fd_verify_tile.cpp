@@ -1446,10 +1446,13 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
     depth_min = std::max( depth_min, tile_window( &wc ) + 4096UL );
   }
   ulong depth = 1UL; while( depth < depth_min ) depth <<= 1;
-  /* output depth: the reference's verify -> dedup link (receive_buffer_size
-     16384, fdctl/config/default.toml:241, frank.rs:88), or two batches when
-     larger: room for a consumer descheduled for a few hundred us */
-  ulong out_depth = 1UL; while( out_depth < std::max( 2UL*batch_max + 1024UL, 16384UL ) ) out_depth <<= 1;
+  /* output depth: 2^17 frags, ~2.5 ms of the saturated rate, so that a
+     consumer descheduled for that long does not backpressure the tile (a
+     2.5 ms consumer gap behind the reference's 16384-deep verify -> dedup
+     link, receive_buffer_size, fdctl/config/default.toml:241, frank.rs:88,
+     filled it and then the tile's window: profiles/r05_bench_final_f2_detail.json,
+     4096 zero copy at 80 %); two batches when larger */
+  ulong out_depth = 1UL; while( out_depth < std::max( 2UL*batch_max + 1024UL, 1UL << 17 ) ) out_depth <<= 1;
   ulong const frame = FD_VERIFY_AMD_FRAME_SZ, frame_c = FRAME_CHUNKS;
   /* Data region: either every pool frame once (what a NIC would have
      DMA'd; the producer publishes metadata only, so the bench measures the
