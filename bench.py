@@ -582,7 +582,9 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
                 "stalls_us": {"producer_late_max": r["producer_late_max_ns"] / 1e3,
                               "tile_pass_max": r["tile_pass_max_ns"] / 1e3,
                               "consumer_gap_max": r["consumer_gap_max_ns"] / 1e3},
-                "copy_steals": int(r["copy_steals"])}
+                "copy_steals": int(r["copy_steals"]),
+                "loop": {k: int(r[k]) for k in ("passes", "hand_offs", "stop_window", "stop_frames", "stop_batch_max",
+                                                "stop_pass_bound")}}
 
     rows = []
     bmaxes = (256, 1024, 4096, 16384) if world == 1 else (16384,)
