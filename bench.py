@@ -90,9 +90,10 @@ def parse():
     ap.add_argument("--no-stream", action="store_true", help="skip the streaming-tile sweep (config 5)")
     ap.add_argument("--workload", choices=("sigs", "txn"), default="sigs",
                     help="sigs: configs[1] (default bench line); txn: configs[3] multi-signer transactions")
-    ap.add_argument("--stream-frags", type=int, default=1 << 23,
-                    help="frags per saturated streaming-tile run (2^23: ~150 ms at saturation, so the run's ramp "
-                         "and drain -- ~5 ms in all -- weigh ~3 %% of the whole-run rate)")
+    ap.add_argument("--stream-frags", type=int, default=1 << 25,
+                    help="frags per saturated streaming-tile run (2^25: ~0.6 s at saturation, so the run's ramp "
+                         "and drain -- ~5 ms in all -- weigh under 1 %% of the whole-run rate, as for a tile that "
+                         "runs continuously; 2^23 gave whole-run rates ~4 %% under the steady ones)")
     ap.add_argument("--paced-seconds", type=float, default=0.5,
                     help="length of a paced streaming-tile run (latency over its steady state: after its first 20 ms)")
     ap.add_argument("--txn-full-check", action="store_true",
@@ -691,7 +692,7 @@ def txn_stream_row(local, args):
     tag = np.array([_txn_first_tag(payload[int(o):int(o) + int(z)]) for o, z in zip(toff, tsz)], np.uint64)
     zpub, zsig = np.zeros((toff.size, 32), np.uint8), np.zeros((toff.size, 64), np.uint8)
     pool = (zpub, zsig, toff, tsz, payload)
-    nf = args.stream_frags // 4
+    nf = min(args.stream_frags // 4, 1 << 21)   # transactions per saturated TXN run
     sigs_per_txn = float(ed25519.txn_slots(payload, toff, tsz)[1]) / toff.size
 
     def paced(bmax, rate):
@@ -773,7 +774,7 @@ def stream_node(local, pub, sig, off, sz, blob, args, rank, world, dist):
     m = min(pub.shape[0], 1 << 16)
     p_off = (off[:m] - off[0]).astype(np.uint32)
     pool = (pub[:m], sig[:m], p_off, sz[:m], blob[off[0]:off[0] + int(p_off[-1]) + int(sz[m - 1])].copy())
-    nf = 4 * args.stream_frags
+    nf = args.stream_frags
     res = []
     try:
         dist.barrier()
