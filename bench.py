@@ -305,6 +305,24 @@ def _pick(d, keys):
     return {k: _r(d[k]) for k in keys if d is not None and k in d}
 
 
+# a paced run whose harness threads stalled: the producer (the NIC's stand-in) ran late or the consumer (the
+# dedup tile's stand-in) stopped polling for this long (a tile's own threads' stalls are not excused)
+HARNESS_STALL_US = {"producer_late_max": 1000.0, "consumer_gap_max": 2000.0}
+
+
+def harness_stalled(run):
+    st = run.get("stalls_us", {})
+    return any(st.get(k, 0.0) > v for k, v in HARNESS_STALL_US.items())
+
+
+def worst_of(rs):
+    """The worst run's p99 / p50 over all runs, and over the runs whose harness threads did not stall
+    (None when every run stalled); both are reported, the first is the row check."""
+    worst = max(rs, key=lambda x: x["p99_over_p50"])
+    clean = [x for x in rs if not harness_stalled(x)]
+    return worst, (max(x["p99_over_p50"] for x in clean) if clean else None), len(rs) - len(clean)
+
+
 def tile_summary(st):
     """One entry per streaming-tile row: saturated whole-run / steady rate,
     roofline frac, median p50 and the WORST run's p99 / p50 at each load."""
@@ -324,9 +342,14 @@ def tile_summary(st):
                 e["p50_us_" + load] = _r(a["p50_us"])
                 e["worst_p99_us_" + load] = _r(a["worst_p99_us"])
                 e["worst_x_" + load] = _r(a["worst_p99_over_p50"], 3)
+                if a.get("harness_stalled_runs"):
+                    e["stalled_runs_" + load] = a["harness_stalled_runs"]
+                    e["worst_x_unstalled_" + load] = _r(a["worst_p99_over_p50_unstalled"], 3)
             rows.append(e)
     s = {"all_checks_pass": st["all_checks_pass"],
          "every_row_worst_p99_within_2_5x_p50": st["every_row_p99_within_2_5x_p50"],
+         "every_row_worst_p99_within_2_5x_p50_runs_without_harness_stalls":
+             st["every_row_p99_within_2_5x_p50_unstalled"],
          "every_row_p50_nondecreasing_with_load": st["every_row_p50_nondecreasing_with_load"],
          "min_p50_ratio_80_over_50": _r(min(r["at_80%"]["p50_us"] / max(r["at_50%"]["p50_us"], 1e-3)
                                             for row in st["rows"] for k, r in row.items() if k in ("copy", "zero_copy")), 4),
@@ -346,9 +369,15 @@ def tile_summary(st):
                 e["p50_us_" + ld] = _r(a["p50_us"])
                 e["worst_p99_us_" + ld] = _r(a["worst_p99_us"])
                 e["worst_x_" + ld] = _r(a["worst_p99_over_p50"], 3)
+                if a.get("harness_stalled_runs"):
+                    e["stalled_runs_" + ld] = a["harness_stalled_runs"]
+                    e["worst_x_unstalled_" + ld] = _r(a["worst_p99_over_p50_unstalled"], 3)
             s["txn_framing"].append(e)
         s["every_row_worst_p99_within_2_5x_p50"] = s["every_row_worst_p99_within_2_5x_p50"] and \
             all(r["p99_within_2_5x_p50"] for r in tx["rows"])
+        s["every_row_worst_p99_within_2_5x_p50_runs_without_harness_stalls"] = \
+            s["every_row_worst_p99_within_2_5x_p50_runs_without_harness_stalls"] and \
+            all(r["p99_within_2_5x_p50_unstalled"] for r in tx["rows"])
         s["all_checks_pass"] = s["all_checks_pass"] and all(r["check_mismatches"] == 0 for r in tx["rows"])
     return s
 
@@ -392,10 +421,17 @@ def compact_line(out, detail):
             line[k + "_verifies_per_s"] = _r(out[k]["verifies_per_s"])
     if "verdicts" in out:
         line["verdicts"] = {k: v for k, v in out["verdicts"].items() if not isinstance(v, dict)}
+    # the summaries never cost the line: a summary that fails says so (the detail file has the record)
     if "stream_tile" in out:
-        line["stream_tile"] = tile_summary(out["stream_tile"])
+        try:
+            line["stream_tile"] = tile_summary(out["stream_tile"])
+        except (KeyError, TypeError, ValueError, ZeroDivisionError) as e:
+            line["stream_tile"] = {"summary_error": repr(e)[:200]}
     if out.get("stream_tile_node"):
-        line["stream_tile_node"] = node_summary(out["stream_tile_node"])
+        try:
+            line["stream_tile_node"] = node_summary(out["stream_tile_node"])
+        except (KeyError, TypeError, ValueError, ZeroDivisionError) as e:
+            line["stream_tile_node"] = {"summary_error": repr(e)[:200]}
     line["detail"] = detail
     s = json.dumps(line, separators=(",", ":"))
     if len(s) > LINE_MAX:   # never let the line outgrow the driver's parser: drop the bulkiest parts first
@@ -626,16 +662,19 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
                 # p50 is the median of the three runs' p50; the tail is the WORST run's p99 / p50 (a
                 # single bad run must fail the row: VERDICT r04 weak 2, 9); every run is kept whole
                 med = sorted(rs, key=lambda x: x["p50_us"])[1]
-                worst = max(rs, key=lambda x: x["p99_over_p50"])
+                worst, worst_clean, nstall = worst_of(rs)
                 r = {"p50_us": med["p50_us"], "frags_per_s": med["frags_per_s"],
                      "offered_frags_per_s": med["offered_frags_per_s"],
                      "worst_p99_us": worst["p99_us"], "worst_p99_over_p50": worst["p99_over_p50"],
-                     "worst_run": rs.index(worst), "runs": rs}
+                     "worst_run": rs.index(worst), "harness_stalled_runs": nstall,
+                     "worst_p99_over_p50_unstalled": worst_clean, "runs": rs}
                 rr["at_%d%%" % int(load * 100)] = r
             lo, hi = rr["at_50%"], rr["at_80%"]
             # medians of three runs, no slack
             rr["p50_nondecreasing_with_load"] = hi["p50_us"] >= lo["p50_us"]
             rr["p99_within_2_5x_p50"] = max(lo["worst_p99_over_p50"], hi["worst_p99_over_p50"]) <= 2.5
+            rr["p99_within_2_5x_p50_unstalled"] = all(x["worst_p99_over_p50_unstalled"] is None or
+                                                      x["worst_p99_over_p50_unstalled"] <= 2.5 for x in (lo, hi))
             row[key] = rr
         rows.append(row)
     fixed = {}
@@ -656,6 +695,8 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
            "frags_per_run": args.stream_frags,
            "all_checks_pass": all(r["check_mismatches"] == 0 for r in allr),
            "every_row_p99_within_2_5x_p50": all(r["p99_within_2_5x_p50"] for r in allr),
+           "every_row_p99_within_2_5x_p50_unstalled": all(r["p99_within_2_5x_p50_unstalled"] for r in allr),
+           "harness_stall_rule_us": HARNESS_STALL_US,
            "every_row_p50_nondecreasing_with_load": all(r["p50_nondecreasing_with_load"] for r in allr),
            "rows": rows}
     if fixed:
@@ -702,7 +743,8 @@ def txn_stream_row(local, args):
                 "p99_us": r["p99_ns"] / 1e3, "p99_over_p50": r["p99_ns"] / max(r["p50_ns"], 1.0),
                 "decomposition": _lat_parts(r),
                 "stalls_us": {"producer_late_max": r["producer_late_max_ns"] / 1e3,
-                              "tile_pass_max": r["tile_pass_max_ns"] / 1e3}}
+                              "tile_pass_max": r["tile_pass_max_ns"] / 1e3,
+                              "consumer_gap_max": r["consumer_gap_max_ns"] / 1e3}}
 
     def row(bmax):
         sat = tango.bench_stream(local, bmax, 0, *pool, nf, zero_copy=True, txn=True, expect_err=terr, expect_tag=tag,
@@ -719,12 +761,17 @@ def txn_stream_row(local, args):
                 runs[load].append(paced(bmax, load * sat["frags_per_s"]))
         for load, rs in runs.items():
             med = sorted(rs, key=lambda x: x["p50_us"])[1]
-            worst = max(rs, key=lambda x: x["p99_over_p50"])
+            worst, worst_clean, nstall = worst_of(rs)
             out["at_%d%%" % int(load * 100)] = {"p50_us": med["p50_us"], "txns_per_s": med["txns_per_s"],
                                                 "worst_p99_us": worst["p99_us"],
-                                                "worst_p99_over_p50": worst["p99_over_p50"], "runs": rs}
+                                                "worst_p99_over_p50": worst["p99_over_p50"],
+                                                "harness_stalled_runs": nstall,
+                                                "worst_p99_over_p50_unstalled": worst_clean, "runs": rs}
         out["p99_within_2_5x_p50"] = max(out["at_50%"]["worst_p99_over_p50"],
                                          out["at_80%"]["worst_p99_over_p50"]) <= 2.5
+        out["p99_within_2_5x_p50_unstalled"] = all(out[k]["worst_p99_over_p50_unstalled"] is None or
+                                                   out[k]["worst_p99_over_p50_unstalled"] <= 2.5
+                                                   for k in ("at_50%", "at_80%"))
         return out
 
     rows = [row(4096), row(16384)]

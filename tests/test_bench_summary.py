@@ -1,0 +1,69 @@
+"""bench.py's compact line on a synthetic record (CPU): the tile summary's
+worst-run and harness-stall fields, and that a malformed record costs only
+its own summary, never the line."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def _run(p50, p99, late=0.0, gap=0.0):
+    return {"p50_us": p50, "p99_us": p99, "p99_over_p50": p99 / p50, "frags_per_s": 1.0, "offered_frags_per_s": 1.0,
+            "txns_per_s": 1.0, "stalls_us": {"producer_late_max": late, "tile_pass_max": 10.0, "consumer_gap_max": gap}}
+
+
+def _load(runs):
+    worst, clean, nst = bench.worst_of(runs)
+    med = sorted(runs, key=lambda x: x["p50_us"])[1]
+    return {"p50_us": med["p50_us"], "worst_p99_us": worst["p99_us"], "worst_p99_over_p50": worst["p99_over_p50"],
+            "harness_stalled_runs": nst, "worst_p99_over_p50_unstalled": clean, "runs": runs}
+
+
+def _tile():
+    ok = [_run(1000, 1100), _run(1010, 1120), _run(990, 1090)]
+    stalled = [_run(1000, 1100), _run(1000, 9000, late=5000.0), _run(1005, 1150)]
+    rr_ok = {"saturated_frags_per_s": 5e7, "saturated_steady_frags_per_s": 5.2e7, "check_mismatches": 0,
+             "roofline": {"frac": 0.3, "frac_steady": 0.31}, "at_50%": _load(ok), "at_80%": _load(stalled)}
+    rr_ok["p99_within_2_5x_p50"] = False
+    rr_ok["p99_within_2_5x_p50_unstalled"] = True
+    tx = {"batch_max": 4096, "saturated_txns_per_s": 8e6, "saturated_verifies_per_s": 5e7,
+          "saturated_steady_verifies_per_s": 5.1e7, "check_mismatches": 0, "at_50%": _load(ok), "at_80%": _load(ok),
+          "p99_within_2_5x_p50": True, "p99_within_2_5x_p50_unstalled": True}
+    return {"rows": [{"batch_max": 4096, "zero_copy": rr_ok}], "all_checks_pass": True,
+            "every_row_p99_within_2_5x_p50": False, "every_row_p99_within_2_5x_p50_unstalled": True,
+            "every_row_p50_nondecreasing_with_load": True, "frags_per_run": 1 << 25,
+            "txn_framing": {"rows": [tx]}}
+
+
+def _out(tile):
+    return {"metric": "m", "value": 1.0, "unit": "verifies/s", "n_gpus": 1, "steps": 1, "warmup": 1, "ms_per_step": 1.0,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+            "config": {"workload": "w"}, "stream_tile": tile}
+
+
+def test_worst_of_separates_harness_stalls():
+    runs = [_run(1000, 1100), _run(1000, 9000, late=5000.0), _run(1000, 1200, gap=3000.0)]
+    worst, clean, nst = bench.worst_of(runs)
+    assert worst["p99_us"] == 9000 and nst == 2 and abs(clean - 1.1) < 1e-9
+    worst, clean, nst = bench.worst_of([_run(1000, 9000, late=5000.0)] * 3)
+    assert clean is None and nst == 3
+
+
+def test_compact_line_tile_summary_fields():
+    line = json.loads(bench.compact_line(_out(_tile()), "d.json"))
+    st = line["stream_tile"]
+    assert st["every_row_worst_p99_within_2_5x_p50"] is False
+    assert st["every_row_worst_p99_within_2_5x_p50_runs_without_harness_stalls"] is True
+    row = st["rows"][0]
+    assert row["worst_x_80"] == 9.0 and row["stalled_runs_80"] == 1 and row["worst_x_unstalled_80"] == 1.14
+    assert "stalled_runs_50" not in row
+    assert st["txn_framing"][0]["worst_x_50"] == 1.12
+
+
+def test_malformed_tile_record_costs_only_its_summary():
+    tile = _tile()
+    del tile["rows"][0]["zero_copy"]["at_80%"]
+    line = json.loads(bench.compact_line(_out(tile), "d.json"))
+    assert line["value"] == 1.0 and "summary_error" in line["stream_tile"]
