@@ -59,7 +59,7 @@ def test_compact_line_tile_summary_fields():
     row = st["rows"][0]
     assert row["worst_x_80"] == 9.0 and row["stalled_runs_80"] == 1 and row["worst_x_unstalled_80"] == 1.14
     assert "stalled_runs_50" not in row
-    assert st["txn_framing"][0]["worst_x_50"] == 1.12
+    assert st["txn_framing"][0]["worst_x_50"] == 1.11
 
 
 def test_malformed_tile_record_costs_only_its_summary():
