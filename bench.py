@@ -305,14 +305,17 @@ def _pick(d, keys):
     return {k: _r(d[k]) for k in keys if d is not None and k in d}
 
 
-# a paced run whose harness threads stalled: the producer (the NIC's stand-in) ran late or the consumer (the
-# dedup tile's stand-in) stopped polling for this long (a tile's own threads' stalls are not excused)
+# a paced run whose harness threads stalled: the producer (the NIC's stand-in) ran late by more than its longest
+# wait for input credit (that wait is the tile holding its input, never excused), or the consumer (the dedup
+# tile's stand-in) stopped polling for this long; the tile's own threads' stalls are not excused
 HARNESS_STALL_US = {"producer_late_max": 1000.0, "consumer_gap_max": 2000.0}
 
 
 def harness_stalled(run):
     st = run.get("stalls_us", {})
-    return any(st.get(k, 0.0) > v for k, v in HARNESS_STALL_US.items())
+    late = st.get("producer_late_max", 0.0) - st.get("producer_credit_wait_max", 0.0)
+    return late > HARNESS_STALL_US["producer_late_max"] or \
+        st.get("consumer_gap_max", 0.0) > HARNESS_STALL_US["consumer_gap_max"]
 
 
 def worst_of(rs):
@@ -617,6 +620,7 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
                 "mean_chunk": r["mean_batch"], "sv_filt": int(r["sv_filt"]),
                 "decomposition": _lat_parts(r),
                 "stalls_us": {"producer_late_max": r["producer_late_max_ns"] / 1e3,
+                              "producer_credit_wait_max": r["producer_credit_wait_max_ns"] / 1e3,
                               "tile_pass_max": r["tile_pass_max_ns"] / 1e3,
                               "consumer_gap_max": r["consumer_gap_max_ns"] / 1e3},
                 "copy_steals": int(r["copy_steals"]),
@@ -743,6 +747,7 @@ def txn_stream_row(local, args):
                 "p99_us": r["p99_ns"] / 1e3, "p99_over_p50": r["p99_ns"] / max(r["p50_ns"], 1.0),
                 "decomposition": _lat_parts(r),
                 "stalls_us": {"producer_late_max": r["producer_late_max_ns"] / 1e3,
+                              "producer_credit_wait_max": r["producer_credit_wait_max_ns"] / 1e3,
                               "tile_pass_max": r["tile_pass_max_ns"] / 1e3,
                               "consumer_gap_max": r["consumer_gap_max_ns"] / 1e3}}
 

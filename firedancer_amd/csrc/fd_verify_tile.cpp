@@ -275,11 +275,11 @@ struct orphan_t { ulong g, s, b; std::vector<uint> frames; };
 static ulong
 tile_window( fd_verify_amd_tile_cfg_t const * c ) {
   if( c->window ) return c->window;
-  /* in flight = rate x latency: ~1.3 ms at up to ~55 M frags/s under load,
-     plus a hand-off's worth of head-of-line wait (a window that binds at 80 %
-     load shows up as input wait in the tail) */
-  if( c->batch_max >= (1UL << 12) ) return 1UL << 18;
-  if( c->batch_max >= (1UL << 10) ) return 1UL << 17;
+  /* in flight = rate x latency: ~1.3-2.2 ms at up to ~60 M frags/s under
+     load, plus a hand-off's worth of head-of-line wait (a window that binds
+     at 80 % load shows up as input wait in the tail: 2^17 did at batch_max
+     1024 on a 60 M frags/s box, profiles/r05_bench_tile_window1024.json) */
+  if( c->batch_max >= (1UL << 10) ) return 1UL << 18;
   return std::max( 64UL * c->batch_max, 1UL << 15 );   /* latency chunks at ~18 M frags/s x ~1 ms */
 }
 
@@ -1539,7 +1539,7 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   ulong const warm_ns = 20000000UL;
   fd_verify_amd_diag_t diag; memset( &diag, 0, sizeof diag );
   int tile_rc = 0;
-  ulong mism = 0, checked = 0, late_max = 0, gap_max = 0;
+  ulong mism = 0, checked = 0, late_max = 0, gap_max = 0, credit_max = 0;
   ulong t0 = now_ns(), t_prod0 = 0UL;   /* the rate is timed from the producer's start */
 
   std::thread prod( [&]() {
@@ -1567,7 +1567,11 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
       /* credit: neither the mcache line nor (when writing) the data frame
          of a frag the tile still reads is reused; refreshed only when the
          cached credit runs out */
-      if( !lap ) while( seq >= cr ) cr = __atomic_load_n( &in_fseq, __ATOMIC_ACQUIRE ) + lim;
+      if( !lap && seq >= cr ) {   /* out of credit: the tile holds the input (its wait is timed apart from lateness) */
+        ulong const c0 = now_ns();
+        while( seq >= cr ) cr = __atomic_load_n( &in_fseq, __ATOMIC_ACQUIRE ) + lim;
+        credit_max = std::max( credit_max, now_ns() - c0 );
+      }
       ulong sz = frag_sz( k );
       ulong fr = writes ? fw : k;
       if( writes ) put_frame( dcache + fr * frame, k );
@@ -1699,7 +1703,7 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   out[8] = (double)mism; out[9] = (double)checked;
   out[10] = (double)diag.gpu_chunk_lat_cnt; out[11] = (double)diag.gpu_chunk_thr_cnt;
   out[12] = (double)diag.gpu_frag_lat_cnt;  out[13] = (double)diag.gpu_frag_thr_cnt;
-  out[14] = (double)late_max; out[15] = (double)pass_max; out[16] = (double)gap_max;
+  out[14] = (double)late_max; out[15] = (double)pass_max; out[16] = (double)gap_max; out[31] = (double)credit_max;
   return FD_ED25519_AMD_OK;
 }
 

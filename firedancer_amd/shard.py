@@ -113,10 +113,8 @@ def tile_window(batch_max, window=0):
     """The tile's default window (frags in flight), fd_verify_tile.cpp tile_window."""
     if window:
         return int(window)
-    if batch_max >= 1 << 12:
-        return 1 << 18
     if batch_max >= 1 << 10:
-        return 1 << 17
+        return 1 << 18
     return max(64 * batch_max, 1 << 15)
 
 

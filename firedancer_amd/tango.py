@@ -193,6 +193,6 @@ def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, bl
             "checked", "gpu_chunks_lat", "gpu_chunks_thr", "gpu_frags_lat", "gpu_frags_thr", "producer_late_max_ns",
             "tile_pass_max_ns", "consumer_gap_max_ns", "cut_p50_ns", "cut_p99_ns", "queue_p50_ns", "queue_p99_ns",
             "service_p50_ns", "service_p99_ns", "publish_p50_ns", "publish_p99_ns", "input_p50_ns", "input_p99_ns",
-            "service_lat_chunk_p50_ns", "service_thr_chunk_p50_ns", "mode_switches", "traced", "_reserved", "passes",
+            "service_lat_chunk_p50_ns", "service_thr_chunk_p50_ns", "mode_switches", "traced", "producer_credit_wait_max_ns", "passes",
             "hand_offs", "stop_window", "stop_frames", "stop_batch_max", "stop_pass_bound", "all_p50_ns", "all_p99_ns", "steady_frags_per_s", "copy_steals")
     return dict(zip(keys, list(out)))

@@ -149,7 +149,7 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    batch_max staged frags, when the window or the output frames run out,
    at the end of the input, and (batch_wait_ns != 0) once the oldest waited
    batch_wait_ns.  At most `window` frags are in flight (handed over, not
-   yet published; 0: 2^18 from batch_max 4096, 2^17 from 1024, else
+   yet published; 0: 2^18 from batch_max 1024, else
    64 x batch_max, >= 2^15).
    Host side.  The caller's thread polls, dedups and stages; publishing
    runs on a second host thread when publish_cpu >= 0 (pinned there) or,
@@ -194,7 +194,7 @@ typedef struct {
   ulong waves;            /* 0: the device's share */
   int   chunk_mode;       /* FD_VERIFY_AMD_CHUNK_* */
   int   publish_cpu;      /* FD_VERIFY_AMD_PUBLISH_AUTO / _INLINE, or a CPU */
-  ulong window;           /* frags in flight; 0: 2^18 from batch_max 4096, 2^17 from 1024,
+  ulong window;           /* frags in flight; 0: 2^18 from batch_max 1024,
                              else max( 64 x batch_max, 2^15 ) */
   ulong lat_fill_ns;
   ulong lat_free_chunks;
@@ -403,7 +403,8 @@ fd_verify_amd_tile_pack( uint const * slots, ulong cnt, int thr, ulong * nsl );
    the cut wait, queue wait, service, publish wait and input wait (latency
    minus the other four: producer publish -> staged), out[27] / out[28] =
    p50 service of latency / throughput chunks, out[29] = chunk-mode
-   switches, out[30] = frags traced, out[31] = 0; out[32..37] = the run
+   switches, out[30] = frags traced, out[31] = the producer's longest wait for
+   input credit (ns: the tile holding its input, not a producer stall); out[32..37] = the run
    loop's passes, hand-offs, and passes whose staging stopped at the
    window, the output frames, batch_max staged frags and the per-pass
    bound.  Paced runs start once the tile's kernel runs (+2 ms): a run's
