@@ -69,8 +69,12 @@ def build_engine(force=False, verbose=False, out=None, defines=(), vgpr_guard=Tr
 
     with ThreadPoolExecutor(max_workers=min(len(SOURCES), max(1, min(8, os.cpu_count() or 1)))) as ex:
         list(ex.map(cc, range(len(SOURCES))))
-    n = loop_spill_stores(objs[0], TILE_KERNEL)
-    if vgpr_guard and n:
+    n = loop_spill_stores(objs[0], TILE_KERNEL) if vgpr_guard else 0
+    if n is None:   # fail closed: a build whose tile kernel cannot be inspected is not shipped
+        raise RuntimeError("cannot inspect k_tile_persist for in-loop VGPR spills (the LLVM tools under "
+                           "/opt/rocm/lib/llvm/bin are missing, or the kernel symbol %s is not in the code "
+                           "object): refusing the build; see profiles/r05_scout_stop_cause.txt" % TILE_KERNEL)
+    if n:
         raise RuntimeError("k_tile_persist spills VGPRs to scratch inside its persistent loop (%d scratch stores after "
                            "the first s_sleep): every such build lost its scout wave on hardware; see "
                            "profiles/r05_scout_stop_cause.txt" % n)
@@ -97,7 +101,8 @@ def _device_object(obj):
 def loop_spill_stores(obj, kernel):
     """scratch_store instructions of `kernel` after its first s_sleep (the
     persistent loop's wait): 0 when the kernel spills only in its prologue,
-    None when the LLVM tools are missing."""
+    None when the LLVM tools are missing or the code object holds no such
+    kernel (or it has no s_sleep: then the loop cannot be located)."""
     d = _device_object(obj)
     if d is None:
         return None
@@ -117,7 +122,9 @@ def loop_spill_stores(obj, kernel):
             continue
         if inside:
             lines.append(ln)
-    first = next((i for i, ln in enumerate(lines) if "s_sleep" in ln), len(lines))
+    first = next((i for i, ln in enumerate(lines) if "s_sleep" in ln), None)
+    if not lines or first is None:
+        return None
     return sum("scratch_store" in ln for ln in lines[first:])
 
 

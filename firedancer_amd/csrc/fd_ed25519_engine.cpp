@@ -15,9 +15,13 @@
 #include <stdlib.h>
 #include <string.h>
 #include <stdint.h>
+#include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <vector>
 #include <pthread.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <thread>
 
 #include "../../include/fd_ed25519_amd.h"
@@ -759,9 +763,14 @@ fd_ed25519_amd_debug_digits_dev( ulong n, void const * d_ws, ushort * d_dig, int
 
 /* One engine per calling thread (the reference is reentrant with one
    fd_sha512_t per thread, fd_frank_verify.c:121-123), freed by a
-   pthread-key destructor when the thread exits. */
+   pthread-key destructor when the thread exits.  The reference boots N
+   verify tiles as threads of one process (fd_frank_main.c:118-143), so the
+   engine's device is a per-thread choice: the thread's own
+   (fd_ed25519_amd_dropin_set_device), else FD_ED25519_AMD_DEVICE, else
+   round robin over the GPUs local to the NUMA node of the CPU the thread
+   first verifies on (fd_ed25519_amd_dropin_pick). */
 namespace {
-struct dropin_t { fd_ed25519_amd_t * eng; ulong blob; };
+struct dropin_t { fd_ed25519_amd_t * eng; ulong blob; int want; int dev; };
 pthread_key_t  dropin_key;
 pthread_once_t dropin_once = PTHREAD_ONCE_INIT;
 void dropin_free( void * p ) {
@@ -770,37 +779,93 @@ void dropin_free( void * p ) {
   free( d );
 }
 void dropin_key_init( void ) { (void)pthread_key_create( &dropin_key, dropin_free ); }
+dropin_t * dropin_self( void ) {
+  (void)pthread_once( &dropin_once, dropin_key_init );
+  dropin_t * d = (dropin_t *)pthread_getspecific( dropin_key );
+  if( !d ) {
+    d = (dropin_t *)calloc( 1, sizeof(dropin_t) );
+    if( !d || pthread_setspecific( dropin_key, d ) ) { free( d ); return NULL; }
+    d->want = FD_ED25519_AMD_DROPIN_AUTO; d->dev = -1;
+  }
+  return d;
+}
+/* threads given a default device so far, per NUMA node of their CPU (the
+   last counter takes unknown and out-of-range nodes) */
+std::atomic<ulong> dropin_ordinal[65];
+
+/* The default device of a thread that set none. */
+int dropin_default_device( void ) {
+  char const * dv = getenv( "FD_ED25519_AMD_DEVICE" );
+  if( dv && *dv ) return atoi( dv );
+  int cnt = 0;
+  if( hipGetDeviceCount( &cnt ) != hipSuccess || cnt <= 0 ) { (void)hipGetLastError(); return 0; }
+  int node_of[FD_ED25519_AMD_DROPIN_DEV_MAX];
+  cnt = std::min( cnt, (int)FD_ED25519_AMD_DROPIN_DEV_MAX );
+  for( int k=0; k<cnt; k++ ) node_of[k] = fd_ed25519_amd_device_numa_node( k );
+  unsigned cpu = 0, node = 0;
+  int const cpu_node = syscall( SYS_getcpu, &cpu, &node, NULL ) ? -1 : (int)node;
+  ulong const o = dropin_ordinal[ cpu_node >= 0 && cpu_node < 64 ? cpu_node : 64 ].fetch_add( 1UL );
+  return fd_ed25519_amd_dropin_pick( node_of, cnt, cpu_node, o );
+}
+}
+
+extern "C" int
+fd_ed25519_amd_dropin_pick( int const * dev_node, int dev_cnt, int cpu_node, ulong ordinal ) {
+  if( dev_cnt <= 0 || !dev_node ) return 0;
+  int local = 0;
+  if( cpu_node >= 0 ) for( int k=0; k<dev_cnt; k++ ) local += dev_node[k] == cpu_node;
+  if( !local ) return (int)(ordinal % (ulong)dev_cnt);
+  ulong j = ordinal % (ulong)local;
+  for( int k=0; k<dev_cnt; k++ ) if( dev_node[k] == cpu_node && !j-- ) return k;
+  return 0;   /* not reached */
+}
+
+extern "C" int
+fd_ed25519_amd_dropin_set_device( int device ) {
+  if( device < FD_ED25519_AMD_DROPIN_AUTO ) return FD_ED25519_AMD_ERR_INVAL;
+  if( device >= 0 ) {
+    int cnt = 0;
+    if( hipGetDeviceCount( &cnt ) != hipSuccess ) { (void)hipGetLastError(); return FD_ED25519_AMD_ERR_DEVICE; }
+    if( device >= cnt ) return FD_ED25519_AMD_ERR_INVAL;
+  }
+  dropin_t * d = dropin_self();
+  if( !d ) return FD_ED25519_AMD_ERR_INVAL;
+  d->want = device;
+  return FD_ED25519_AMD_OK;
+}
+
+extern "C" int
+fd_ed25519_amd_dropin_device( void ) {
+  dropin_t * d = dropin_self();
+  return d && d->eng ? d->dev : -1;
 }
 
 extern "C" int
 fd_ed25519_verify( void const * msg, ulong sz, void const * sig, void const * public_key, fd_sha512_t * sha ) {
   (void)sha;   /* scratch of the reference; hashing happens on the GPU */
-  (void)pthread_once( &dropin_once, dropin_key_init );
-  dropin_t * d = (dropin_t *)pthread_getspecific( dropin_key );
+  dropin_t * d = dropin_self();
   if( !d ) {
-    d = (dropin_t *)calloc( 1, sizeof(dropin_t) );
-    if( !d || pthread_setspecific( dropin_key, d ) ) {
-      fprintf( stderr, "fd_ed25519_verify: out of memory\n" );
-      abort();
-    }
+    fprintf( stderr, "fd_ed25519_verify: out of memory\n" );
+    abort();
   }
   if( sz > 0xFFFFFFFFUL - 4096UL ) {
     fprintf( stderr, "fd_ed25519_verify: message of %lu bytes exceeds the engine's 32-bit offsets\n", sz );
     abort();
   }
+  /* the thread's device: its own choice, else the default picked once */
+  int const dev = d->want >= 0 ? d->want : d->dev >= 0 ? d->dev : dropin_default_device();
   /* the engine grows when a message exceeds its staging (the reference
-     accepts any size) */
-  if( !d->eng || sz > d->blob ) {
-    ulong want = 64UL*FD_ED25519_AMD_MSG_MAX;
+     accepts any size) and moves when the thread's device changed */
+  if( !d->eng || sz > d->blob || dev != d->dev ) {
+    ulong want = std::max( d->eng ? d->blob : 0UL, 64UL*FD_ED25519_AMD_MSG_MAX );
     while( want < sz ) want <<= 1;
     if( d->eng ) { fd_ed25519_amd_delete( d->eng ); d->eng = NULL; }
-    char const * dv = getenv( "FD_ED25519_AMD_DEVICE" );
-    d->eng = fd_ed25519_amd_new( dv ? atoi( dv ) : 0, 64UL, want );
+    d->eng = fd_ed25519_amd_new( dev, 64UL, want );
     if( !d->eng ) {
-      fprintf( stderr, "fd_ed25519_verify: no usable MI355X/HIP device; this library has no CPU path\n" );
+      fprintf( stderr, "fd_ed25519_verify: no usable MI355X/HIP device %d; this library has no CPU path\n", dev );
       abort();
     }
-    d->blob = want;
+    d->blob = want; d->dev = dev;
   }
   static uint8_t const zero = 0;
   uint32_t off = 0, s32 = (uint32_t)sz;

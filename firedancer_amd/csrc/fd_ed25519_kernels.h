@@ -67,10 +67,12 @@ int fd_amd_launch_sign( uint32_t n, uint8_t const * d_prv, uint32_t const * d_of
    (fd_amd_txn_slots1).  Entry of ring index j at ent[j & mask]. */
 typedef struct { uint32_t src_chunk, out_chunk, sz, slots; } fd_amd_tile_ent_t;
 /* chunk descriptor (host -> GPU): ring entries [first, first + count),
-   count <= 64 | FD_AMD_TILE_LAT (8 lanes per signature); the entries'
-   signature slots total <= 64 (<= 8 in a latency chunk) */
+   count <= 64 | FD_AMD_TILE_LAT (8 lanes per signature) or FD_AMD_TILE_QUAD
+   (4 lanes per signature); the entries' signature slots total <= 64 (<= 8
+   in a latency chunk, <= 16 in a quad chunk) */
 typedef struct { uint64_t first; uint32_t count; uint32_t pad; } fd_amd_tile_desc_t;
-#define FD_AMD_TILE_LAT (0x80000000u)
+#define FD_AMD_TILE_LAT  (0x80000000u)
+#define FD_AMD_TILE_QUAD (0x40000000u)
 /* result of ring index j (GPU -> host), two arrays of R words: tag[j & mask]
    and word[j & mask] = (j + 1) << 8 | (uint8_t)verdict, the word stored
    after the tag and after the frag's output bytes (system-scope release),
@@ -96,7 +98,7 @@ typedef struct {
   uint64_t             ticket;  uint64_t pad0[7];   /* next chunk ticket (one atomic add per chunk) */
   fd_amd_tile_mirror_t mw[FD_AMD_TILE_MIRRORS];     /* per XCD: descriptor head | heartbeat << 48 | err << 62 | stop << 63 */
   uint64_t             done;    uint64_t pad1[7];   /* chunks finished (one atomic add per chunk; the scout mirrors it) */
-  uint64_t             stat[4];                     /* chunks in latency mode, in throughput mode; frags in each */
+  uint64_t             stat[6];                     /* chunks in latency mode, in throughput mode; frags in each; quad chunks, their frags */
   uint64_t             prof[8];                     /* diagnostics build (FD_AMD_DIAG, args.prof): summed ticks gather, decomp, DSM, results, wait, fence, prep */
 } fd_amd_tile_dctl_t;
 typedef struct {

@@ -887,24 +887,12 @@ ai_table_quad( bool act, bool wr, int qd, u64 m1, u64 m2, i32 const * __restrict
 # undef AI_ROW4
 }
 
-__global__ void __launch_bounds__(64)
-k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats, i8 * __restrict__ out ) {
-  /* the base-point table in the Ai slab's row layout (see k_dsm8) */
-  __shared__ __attribute__((aligned(16))) i32 bi12[8][48];
-  for( int k=threadIdx.x; k<8*48; k+=64 ) {
-    int e = k / 48, c = (k % 48) / 12, l = k % 12;
-    i32 v = 0;
-    if( l < 10 ) {
-      if( c == 0 ) v = (l == 0);
-      else if( c == 1 ) v = BI_TABLE[e][1][l];
-      else if( c == 2 ) v = BI_TABLE[e][0][l];
-      else v = BI_TABLE[e][2][l];
-    }
-    bi12[e][k % 48] = v;
-  }
-  __syncthreads();
-
-  u32 gt = blockIdx.x * 64u + threadIdx.x;
+/* k_dsm4's body for lane gt of the launch (signature gt >> 2); bi12 filled
+   (bi12_fill), evl: 16 event rows of 33 words for the wave's 16 signatures.
+   Also the streaming tile's quad chunks (k_tile_persist). */
+__device__ __forceinline__ void
+dsm4_body( u32 gt, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats,
+           i32 (* __restrict__ bi12)[48], u64 (* __restrict__ evl)[33], u64 tc = 0UL ) {
   u32 i = gt >> 2;
   int qd = (int)(threadIdx.x & 3u);
   bool act = (i < n) && (err[i] == 1);
@@ -925,8 +913,7 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
   int ph  = act ? (p >= 0 ? PH_DBL : PH_FIN) : PH_DONE;
   evq eva, evb;                                      /* digit events of h and s */
   {
-    __shared__ u64 evl[16][33];                      /* one row per signature of the wave */
-    u64 * row = evl[threadIdx.x >> 2];
+    u64 * row = evl[(threadIdx.x & 63u) >> 2];       /* one row per signature of the wave */
     u32 ne = act ? ((u32 const *)(ws + L.evn))[ii] : 0u;
     u32 wa = ((ne & 0xffu) + 3u) >> 2, wb = (((ne >> 8) & 0xffu) + 3u) >> 2;
     for( u32 k=(u32)qd; k<wa; k+=4u ) row[k]       = dg[k];        /* the quad copies the row together */
@@ -941,8 +928,10 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
   bool qneg = false;
   fe qrow = fe_zero();
   fe C = (qd == 2) ? fe_zero() : fe_one();   /* identity: own coordinate (Z, T, X, Y)[q] = (1, 1, 0, 1) */
+  u32 lvl = 0u;
 
   for( ;; ) {
+    if( tc ) tile_age_prio( tc, lvl );
     fe pm = quad_p3_ownc( C );              /* q0 u.Z, q1 u.Y, q2 u.X, q3 u.T */
 
     bool fin = (ph == PH_FIN);
@@ -1014,12 +1003,23 @@ k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int w
     int both = qb<0>( e01 ) & qb<1>( e01 );
     if( act && qd == 0 ) err[i] = (i8)(both ? 0 : -3);
   }
-  if( out && i < n && qd == 0 ) out[i] = err[i];   /* every verdict, straight to mapped host memory */
 
   if( want_stats && i < n && qd == 0 ) {
     u32 * st = (u32 *)(ws + L.st);
     st[i] = act ? nit : 0u; st[N + i] = act ? nha : 0u; st[2*N + i] = act ? nhb : 0u;
   }
+}
+
+__global__ void __launch_bounds__(64)
+k_dsm4( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int want_stats, i8 * __restrict__ out ) {
+  __shared__ __attribute__((aligned(16))) i32 bi12[8][48];   /* the base-point table in the Ai slab's row layout */
+  __shared__ u64 evl[16][33];
+  bi12_fill( bi12 );
+  __syncthreads();
+  u32 const gt = blockIdx.x * 64u + threadIdx.x;
+  dsm4_body( gt, n, err, ws, L, want_stats, bi12, evl );
+  /* every verdict, straight to mapped host memory, by the lane that wrote it */
+  if( out && (gt >> 2) < n && !(threadIdx.x & 3u) ) out[gt >> 2] = err[gt >> 2];
 }
 
 /* ------------------------------------------------------------------ */
@@ -1888,6 +1888,9 @@ k_fin( u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, int wa
  * workspace per wave): identical limbs and verdicts. */
 
 #define TILE_FRAME (1408u)   /* FD_VERIFY_AMD_FRAME_SZ */
+#define TILE_MODE_THR   (0u)   /* 1 lane per signature, <= 64 slots (k_dsm's body) */
+#define TILE_MODE_LAT8  (1u)   /* 8 lanes per signature, <= 8 slots (k_dsm8's body) */
+#define TILE_MODE_QUAD4 (2u)   /* 4 lanes per signature, <= 16 slots (k_dsm4's body) */
 
 __device__ __forceinline__ u64 ld_sys64( u64 const * p ) { return __hip_atomic_load( (u64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
 __device__ __forceinline__ u32 ld_sys32( u32 const * p ) { return __hip_atomic_load( (u32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
@@ -2079,11 +2082,13 @@ tile_gather( fd_amd_tile_args_t const & A, u32 k, u32 l, u32 e_src, u32 e_out, u
 }
 
 /* Verify ring entries [c0, c0 + k) (k <= 64) on this wave, claimed at
-   s_memrealtime tc.  PUB_SIG_MSG: entry q is signature slot q.  TXN
+   s_memrealtime tc, in chunk mode `mode` (TILE_MODE_*: 1 lane per signature,
+   8 lanes (k_dsm8's body) or 4 lanes (k_dsm4's body); the host keeps a
+   chunk's slots within the mode's 64 / 8 / 16 lanes).  PUB_SIG_MSG: entry q is signature slot q.  TXN
    (A.txn): entry q is a wire transaction whose slots tile_txn_layout lays
    out, and its result is the transaction's verdict. */
 __device__ __forceinline__ void
-tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __restrict__ scr, ws_layout_t L,
+tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, u32 mode, u8 * __restrict__ scr, ws_layout_t L,
             tile_scratch_t const & S, i32 (* __restrict__ bi)[48], u64 (* __restrict__ evl)[33], u64 * pt, u64 tc ) {
   /* pt (A.prof, set by the diagnostics build's host only): s_memrealtime
      ticks spent in gather [0], prep [6], decomp [1], DSM [2], results [3];
@@ -2120,7 +2125,7 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __rest
   u32 const n = txn ? tile_txn_layout( l, k, e_sz, e_k, mir, pub, sig, off, sz, skp, tx, (u32 *)&evl[0][0] ) : k;
   if( txn ) __syncthreads();
   TILE_STAMP( 0 );
-  /* 3. the verify pipeline on the chunk (k_prep, k_decomp, k_dsm8 / k_dsm bodies) */
+  /* 3. the verify pipeline on the chunk (k_prep, k_decomp, k_dsm / k_dsm8 / k_dsm4 bodies) */
   prep_body( l, n, pub, sig, off, sz, mir, err, ws, L, txn ? (i8 const *)skp : (i8 const *)0 );
   __syncthreads();
   TILE_STAMP( 6 );
@@ -2128,8 +2133,9 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, bool eight, u8 * __rest
   if( n > 32u ) decomp_body( l + 64u, n, pub, sig, err, ws, L, true );
   __syncthreads();
   TILE_STAMP( 1 );
-  if( eight ) dsm8_body( l, n, err, ws, L, 0, bi, evl, tc );
-  else        dsm_lane_body( l, n, err, ws, L, 0, bi, evl, tc );
+  if( mode == TILE_MODE_LAT8 )       dsm8_body( l, n, err, ws, L, 0, bi, evl, tc );
+  else if( mode == TILE_MODE_QUAD4 ) dsm4_body( l, n, err, ws, L, 0, bi, evl, tc );
+  else                               dsm_lane_body( l, n, err, ws, L, 0, bi, evl, tc );
   __builtin_amdgcn_s_setprio( 0 );
   __syncthreads();
   TILE_STAMP( 2 );
@@ -2179,9 +2185,10 @@ k_tile_persist( fd_amd_tile_args_t A ) {
   u8 * scr = A.scratch + (size_t)blockIdx.x * S.total;
   /* per-wave tallies in LDS, not registers (the DSM bodies want every VGPR):
      [0..7] diagnostics build (A.prof) gather, front, DSM, results, wait,
-     fence, -, -; [8..11] latency chunks, throughput chunks, their frags */
-  __shared__ u64 s_tally[12];
-  if( l < 12u ) s_tally[l] = 0UL;
+     fence, -, -; [8..13] dctl->stat: latency chunks, throughput chunks,
+     their frags, quad chunks, their frags */
+  __shared__ u64 s_tally[16];
+  if( l < 16u ) s_tally[l] = 0UL;
   u64 * const pt = s_tally;
   /* A run-time flag (the host sets it only in the diagnostics build), not a
      compile-time constant: with the profiling branches folded away the
@@ -2216,29 +2223,30 @@ k_tile_persist( fd_amd_tile_args_t A ) {
     if( prof && !l ) pt[4] += __builtin_amdgcn_s_memrealtime() - t0;
     if( !go ) break;
     u64 const tc = __builtin_amdgcn_s_memrealtime();   /* claimed */
-    /* descriptor t (host memory): { first ring index, count | latency mode << 31 } */
+    /* descriptor t (host memory): { first ring index, count | FD_AMD_TILE_LAT | FD_AMD_TILE_QUAD } */
     u64 c = 0, cm = 0;
     if( l == 0u ) {
       u64 const * dp = (u64 const *)(A.desc + (t & A.mask));
       c = ld_sys64( dp ); cm = ld_sys64( dp + 1 );
     }
     c = rfl64( c ); cm = rfl64( cm );
-    u32 const take = (u32)cm & 0x7fffffffu;
-    bool const e8 = ((u32)cm >> 31) != 0u;
+    u32 const take = (u32)cm & 0x3fffffffu;
+    u32 const md = ((u32)cm & FD_AMD_TILE_LAT) ? TILE_MODE_LAT8 : ((u32)cm & FD_AMD_TILE_QUAD) ? TILE_MODE_QUAD4 : TILE_MODE_THR;
     /* the frames were written by the host (copy mode) or the producer
        (zero-copy) into host memory: drop this CU's stale lines first */
     u64 const tf = prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
     __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "" );
     asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
     if( prof && !l ) pt[5] += __builtin_amdgcn_s_memrealtime() - tf;
-    if( take && take <= 64u ) tile_chunk( A, c, take, e8, scr, L, S, bi, evl, pt, tc );
+    if( take && take <= 64u ) tile_chunk( A, c, take, md, scr, L, S, bi, evl, pt, tc );
     if( !l ) {
-      s_tally[e8 ? 8 : 9] += 1UL; s_tally[e8 ? 10 : 11] += take;
+      u32 const tk = md == TILE_MODE_LAT8 ? 0u : md == TILE_MODE_THR ? 1u : 4u;   /* dctl->stat chunk slot; frags at +2 */
+      s_tally[8u + tk] += 1UL; s_tally[10u + tk] += take;
       atomicAdd( (unsigned long long *)&D->done, 1ULL );   /* progress, mirrored to the host by the scout */
     }
   }
   if( l == 0u ) {
-    _Pragma("unroll") for( int q=0; q<4; q++ ) atomicAdd( (unsigned long long *)&D->stat[q], (unsigned long long)s_tally[8 + q] );
+    _Pragma("unroll") for( int q=0; q<6; q++ ) atomicAdd( (unsigned long long *)&D->stat[q], (unsigned long long)s_tally[8 + q] );
     if( prof ) { _Pragma("unroll") for( int q=0; q<8; q++ ) atomicAdd( (unsigned long long *)&D->prof[q], (unsigned long long)pt[q] ); }
   }
 }
@@ -2259,7 +2267,8 @@ k_tile_synth( fd_amd_tile_args_t A, u32 iters, u32 eight ) {
   __shared__ u64 pt[8];
   if( threadIdx.x < 8u ) pt[threadIdx.x] = 0UL;
   __syncthreads();
-  u32 const k = eight ? 8u : 64u;
+  u32 const md = eight == 1u ? TILE_MODE_LAT8 : eight == 2u ? TILE_MODE_QUAD4 : TILE_MODE_THR;   /* eight: 0 / 1 / 2 */
+  u32 const k = md == TILE_MODE_LAT8 ? 8u : md == TILE_MODE_QUAD4 ? 16u : 64u;
   if( A.hctl && blockIdx.x == gridDim.x - 1u ) {
     /* A/B: a scout-like wave polling the host control words until the
        others are done (bounded by the watchdog) */
@@ -2277,7 +2286,7 @@ k_tile_synth( fd_amd_tile_args_t A, u32 iters, u32 eight ) {
   }
   u8 * scr = A.scratch + (size_t)blockIdx.x * S.total;
   for( u32 it = 0; it < iters; it++ )
-    tile_chunk( A, ((u64)blockIdx.x * iters + it) * k, k, eight != 0u, scr, L, S, bi, evl, pt, 0UL );
+    tile_chunk( A, ((u64)blockIdx.x * iters + it) * k, k, md, scr, L, S, bi, evl, pt, 0UL );
   if( A.prof && threadIdx.x == 0u ) {
     _Pragma("unroll") for( int q=0; q<8; q++ ) atomicAdd( (unsigned long long *)&A.dctl->prof[q], (unsigned long long)pt[q] );
   }
@@ -2287,7 +2296,7 @@ k_tile_synth( fd_amd_tile_args_t A, u32 iters, u32 eight ) {
 int
 fd_amd_launch_tile_synth( fd_amd_tile_args_t const * a, uint32_t waves, uint32_t iters, int eight, hipStream_t stream ) {
   if( !waves || !iters ) return -1;
-  hipLaunchKernelGGL( k_tile_synth, dim3(waves), dim3(64), 0, stream, *a, iters, (u32)(eight != 0) );
+  hipLaunchKernelGGL( k_tile_synth, dim3(waves), dim3(64), 0, stream, *a, iters, (u32)eight );
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 #endif /* FD_AMD_DIAG */

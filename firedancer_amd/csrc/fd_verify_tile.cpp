@@ -157,6 +157,16 @@ inline ulong now_ns( void ) {
 #define STAGE_PASS   (256UL)        /* frags staged per pass of the run loop before it hands over */
 #define CHUNK_SLOTS  (64UL)         /* signature slots of a throughput chunk (one lane each) */
 #define LAT_SLOTS    (8UL)          /* ... of a latency chunk (8 lanes each) */
+#define QUAD_SLOTS   (16UL)         /* ... of a quad chunk (4 lanes each) */
+/* a quad chunk's service with every wave slot busy, and a frag's time in
+   flight in quad mode (the quad capacity and the window it needs) */
+#define QUAD_SVC_S    (0.9e-3)
+#define QUAD_FLIGHT_S (1.1e-3)
+
+/* slots of a chunk of chunk level lvl (FD_VERIFY_AMD_LVL_*) */
+static inline ulong lvl_slots( int lvl ) {
+  return lvl == FD_VERIFY_AMD_LVL_THR ? CHUNK_SLOTS : lvl == FD_VERIFY_AMD_LVL_QUAD ? QUAD_SLOTS : LAT_SLOTS;
+}
 
 /* Copy mode's helper protocol (below) */
 #define CP_NB       (2UL)                    /* copy blocks per pass: the two halves (one CAS each: finer blocks cost
@@ -236,8 +246,10 @@ copy_jobs( copy_job_t const * j, ulong lo, ulong hi ) {
    blocks is copied again by the stager into FRESH frames, and the frames the
    helper may still write stay reserved ("orphaned") until its done mark
    shows up -- nothing ever reads them, so a late helper write (its source
-   possibly rewritten by then) cannot reach a published frag.  A job array
-   is reused only when none of its blocks is orphaned. */
+   possibly rewritten by then) cannot reach a published frag.  The stager
+   never rewrites a posted job record (the helper may still be reading it):
+   the fresh frames of a re-copied block live in the stager's own frame
+   list.  A job array is reused only when none of its blocks is orphaned. */
 struct copier_t {
   alignas(64) std::atomic<ulong> claim;
   alignas(64) std::atomic<int>   quit;
@@ -246,10 +258,16 @@ struct copier_t {
   copy_job_t                     jobs[CP_NJ][STAGE_PASS];
 };
 
+/* Test hook (FD_VERIFY_AMD_BENCH_STALL_HELPER): the helper spins this long
+   before every 4th block it claims, so the stager's re-copy path runs */
+static std::atomic<ulong> copier_stall_ns( 0UL );
+
 static void
 copier_loop( copier_t * cp, int cpu ) {
   cpu_set_t one; CPU_ZERO( &one ); CPU_SET( cpu, &one );
   (void)pthread_setaffinity_np( pthread_self(), sizeof one, &one );
+  ulong const stall = copier_stall_ns.load( std::memory_order_relaxed );
+  ulong nclaim = 0UL;
   for( ;; ) {
     ulong c = cp->claim.load( std::memory_order_acquire );
     ulong const g = c >> 16, b = c & 0xffffUL;
@@ -257,6 +275,7 @@ copier_loop( copier_t * cp, int cpu ) {
       ulong const s = g % CP_NJ, nj = cp->nj[s].load( std::memory_order_relaxed ), bz = cp->bsz[s].load( std::memory_order_relaxed );
       if( b < CP_NB && b * bz < nj ) {
         if( cp->claim.compare_exchange_weak( c, c + 1UL, std::memory_order_acq_rel ) ) {
+          if( stall && !(nclaim++ & 3UL) ) { ulong const t0 = now_ns(); while( now_ns() - t0 < stall ) _mm_pause(); }
           copy_jobs( cp->jobs[s], b * bz, std::min( nj, (b + 1UL) * bz ) );
           _mm_sfence();   /* the copies before the done mark */
           cp->done[s][b].store( g, std::memory_order_release );
@@ -316,7 +335,8 @@ struct fd_verify_amd_tile {
   ulong                R;          /* ring size (power of 2) */
   ulong                window;     /* frags in flight at most (handed to the GPU, not yet published) */
   uint32_t             waves;      /* grid of a run (the share), fixed at the first run */
-  double               rate_hi, rate_lo;
+  double               rate_hi, rate_lo;     /* throughput chunks above / below (slots/s) */
+  double               quad_hi, quad_lo;     /* quad chunks (instead of latency chunks) above / below */
   bool                 counted;       /* in the per-device tile count */
   ulong                desc_seq;      /* descriptors published, monotonic over the tile's life */
   std::vector<pending_t> ppend;    /* per ring slot */
@@ -512,9 +532,19 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
      (batch_max 256: 8 M vs 18 M frags/s).  Rates are signature slots/s. */
   double const cap  = std::min( (double)std::min( (ulong)waves - 1UL, 4UL * (ulong)t->cus ) * 8.0 / 450e-6,
                                 (double)W / 550e-6 );
-  bool const   thr_ok = (double)W / 2e-3 > cap;
-  t->rate_hi = t->cfg.thr_rate_hi ? (double)t->cfg.thr_rate_hi : thr_ok ? 0.55 * cap : HUGE_VAL;
-  t->rate_lo = t->cfg.thr_rate_lo ? (double)t->cfg.thr_rate_lo : thr_ok ? 0.40 * cap : HUGE_VAL;
+  /* quad chunks (16 slots, 4 lanes each): two per SIMD at ~0.9 ms, a frag
+     ~1.1 ms in flight; used between the two when they carry well above the
+     latency chunks' capacity */
+  double const qcap = std::min( (double)std::min( (ulong)waves - 1UL, 8UL * (ulong)t->cus ) * (double)QUAD_SLOTS / QUAD_SVC_S,
+                                (double)W / QUAD_FLIGHT_S );
+  bool const   quad_ok = qcap > 1.25 * cap;
+  double const below = quad_ok ? qcap : cap;   /* the capacity under throughput chunks */
+  bool const   thr_ok = (double)W / 2e-3 > below;
+  t->quad_hi = t->cfg.quad_rate_hi ? (double)t->cfg.quad_rate_hi : quad_ok ? 0.55 * cap : HUGE_VAL;
+  t->quad_lo = t->cfg.quad_rate_lo ? (double)t->cfg.quad_rate_lo : quad_ok ? 0.40 * cap : HUGE_VAL;
+  if( t->quad_lo > t->quad_hi ) t->quad_lo = t->quad_hi;
+  t->rate_hi = t->cfg.thr_rate_hi ? (double)t->cfg.thr_rate_hi : thr_ok ? (quad_ok ? 0.80 : 0.55) * below : HUGE_VAL;
+  t->rate_lo = t->cfg.thr_rate_lo ? (double)t->cfg.thr_rate_lo : thr_ok ? (quad_ok ? 0.65 : 0.40) * below : HUGE_VAL;
   if( t->rate_lo > t->rate_hi ) t->rate_lo = t->rate_hi;
   unsigned const hf = hipHostMallocMapped | hipHostMallocCoherent;
   /* The run's kernel occupies its hardware queue for the whole run, and HIP
@@ -560,7 +590,7 @@ fd_verify_amd_tile_new_cfg( fd_verify_amd_tile_cfg_t const * cfg ) {
   if( !c.batch_max || c.batch_max > (1UL<<20) ) return NULL;
   if( c.framing != FD_VERIFY_AMD_FRAMING_PUB_SIG_MSG && c.framing != FD_VERIFY_AMD_FRAMING_TXN ) return NULL;
   if( c.framing == FD_VERIFY_AMD_FRAMING_TXN && c.batch_max < TXN_SIG_MAX_AT_MTU ) return NULL;
-  if( c.chunk_mode < FD_VERIFY_AMD_CHUNK_AUTO || c.chunk_mode > FD_VERIFY_AMD_CHUNK_THROUGHPUT ) return NULL;
+  if( c.chunk_mode < FD_VERIFY_AMD_CHUNK_AUTO || c.chunk_mode > FD_VERIFY_AMD_CHUNK_QUAD ) return NULL;
   if( c.publish_cpu < FD_VERIFY_AMD_PUBLISH_AUTO || c.publish_cpu >= CPU_SETSIZE ) return NULL;
   if( c.copy_cpu < FD_VERIFY_AMD_COPY_INLINE || c.copy_cpu >= CPU_SETSIZE ) return NULL;
   if( c.waves == 1UL || c.waves > 65536UL ) return NULL;
@@ -608,9 +638,9 @@ extern "C" ulong
 fd_verify_amd_tile_cut( fd_verify_amd_tile_cfg_t const * c, ulong staged, ulong handed, ulong chunks_in_flight,
                         int thr, ulong waited_ns, int flush ) {
   if( staged == handed ) return handed;
-  ulong const n = staged - handed, K = thr ? CHUNK_SLOTS : LAT_SLOTS;
+  ulong const n = staged - handed, K = lvl_slots( thr );
   if( flush || n >= c->batch_max || (c->batch_wait_ns && waited_ns >= c->batch_wait_ns) ) return staged;
-  bool const rest = thr ? waited_ns >= c->chunk_wait_ns
+  bool const rest = thr == FD_VERIFY_AMD_LVL_THR ? waited_ns >= c->chunk_wait_ns
                         : ( waited_ns >= c->lat_fill_ns || chunks_in_flight < c->lat_free_chunks );
   return rest ? staged : handed + (n & ~(K - 1UL));
 }
@@ -622,6 +652,21 @@ fd_verify_amd_tile_mode( int chunk_mode, int thr, double rate, double rate_hi, d
   return thr ? rate >= rate_lo : rate > rate_hi;
 }
 
+extern "C" int
+fd_verify_amd_tile_level( int chunk_mode, int lvl, double rate, double quad_hi, double quad_lo, double rate_hi,
+                          double rate_lo ) {
+  if( chunk_mode == FD_VERIFY_AMD_CHUNK_LATENCY )    return FD_VERIFY_AMD_LVL_LAT;
+  if( chunk_mode == FD_VERIFY_AMD_CHUNK_THROUGHPUT ) return FD_VERIFY_AMD_LVL_THR;
+  if( chunk_mode == FD_VERIFY_AMD_CHUNK_QUAD )       return FD_VERIFY_AMD_LVL_QUAD;
+  if( lvl == FD_VERIFY_AMD_LVL_THR ) {
+    if( rate >= rate_lo ) return FD_VERIFY_AMD_LVL_THR;
+    return rate >= quad_lo ? FD_VERIFY_AMD_LVL_QUAD : FD_VERIFY_AMD_LVL_LAT;
+  }
+  if( rate > rate_hi ) return FD_VERIFY_AMD_LVL_THR;
+  if( lvl == FD_VERIFY_AMD_LVL_QUAD ) return rate >= quad_lo ? FD_VERIFY_AMD_LVL_QUAD : FD_VERIFY_AMD_LVL_LAT;
+  return rate > quad_hi ? FD_VERIFY_AMD_LVL_QUAD : FD_VERIFY_AMD_LVL_LAT;
+}
+
 /* Chunk packing (pure; the CPU tests call it): from ring entries with
    slots[0..cnt) signature slots each, the next chunk starting at entry 0:
    returns its entry count and sets *nsl to its slots.  Up to 64 entries
@@ -631,7 +676,7 @@ fd_verify_amd_tile_mode( int chunk_mode, int thr, double rate, double rate_hi, d
    signature (slots > 8). */
 extern "C" ulong
 fd_verify_amd_tile_pack( uint const * slots, ulong cnt, int thr, ulong * nsl ) {
-  ulong const K = thr ? CHUNK_SLOTS : LAT_SLOTS;
+  ulong const K = lvl_slots( thr );
   ulong n = 0UL, s = 0UL;
   while( n < cnt && n < 64UL ) {
     ulong const k = slots[n];
@@ -915,6 +960,9 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   std::vector<orphan_t> orphans;
   ulong orphan_cnt[CP_NJ] = { 0, 0, 0, 0 };
   std::vector<copy_job_t> ljobs( zc_dev ? 0UL : STAGE_PASS );   /* a pass copied without the helper */
+  std::vector<uint>       jfr( zc_dev ? 0UL : STAGE_PASS );     /* the frame each listed frag is staged from (a
+                                                                  re-copied block's fresh frames: never written
+                                                                  into the posted jobs, which the helper reads) */
 
   ulong in_seq = in_seq0, staged = base, handed = base;
   ulong staged_sl = 0UL, handed_sl = 0UL;   /* signature slots staged / handed over in this run */
@@ -928,7 +976,8 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   ulong r_t0 = pass_t, r_n0 = 0UL;
   bool  r_blk = false;                   /* staging stopped on the window / frames / credit this interval */
   double rate = 0.0;
-  int thr = fd_verify_amd_tile_mode( t->cfg.chunk_mode, 0, 0.0, t->rate_hi, t->rate_lo );
+  int thr = fd_verify_amd_tile_level( t->cfg.chunk_mode, FD_VERIFY_AMD_LVL_LAT, 0.0, t->quad_hi, t->quad_lo, t->rate_hi,
+                                      t->rate_lo );   /* chunk level, FD_VERIFY_AMD_LVL_* */
   bool halted = false;
   uchar const * in_chunk0b = (uchar const *)in_chunk0;
   fd_verify_amd_tile_cfg_t cc = t->cfg;   /* the cut rule's parameters */
@@ -1061,6 +1110,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       staged++;
     }
     if( nj ) {
+      for( ulong k=0; k<nj; k++ ) jfr[k] = jobs[k].f;
       if( jobs != ljobs.data() && nj >= COPY_SPLIT_MIN ) {
         /* post the pass to the helper; claim blocks beside it */
         ulong const g = gnext, s = snext, bz = (nj + 1UL) / 2UL, nb = CP_NB;
@@ -1100,11 +1150,10 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
             continue;
           }
           for( ulong k = lo; k < hi; k++ ) {
-            copy_job_t & jb = jobs[k];
+            copy_job_t const & jb = jobs[k];
             o.frames.push_back( jb.f );
-            jb.f = fresh[k - lo];
-            jb.dst = t->out_base + (ulong)jb.f * FD_VERIFY_AMD_FRAME_SZ;
-            stage_copy_nt( jb.dst, jb.src, jb.sz );
+            jfr[k] = fresh[k - lo];
+            stage_copy_nt( t->out_base + (ulong)jfr[k] * FD_VERIFY_AMD_FRAME_SZ, jb.src, jb.sz );
           }
           orphan_cnt[s]++;
           orphans.push_back( std::move( o ) );
@@ -1116,18 +1165,19 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       __atomic_thread_fence( __ATOMIC_ACQUIRE );
       for( ulong k=0; k<nj; k++ ) {
         copy_job_t const & j = jobs[k];
+        uint const jf = jfr[k];
         /* a frag lapped while it was copied is dropped (speculative read,
            then seq re-check); its frame is free again */
-        if( __atomic_load_n( &j.m->seq, __ATOMIC_ACQUIRE ) != j.seq ) { ovrn++; unreserve( j.f ); continue; }
+        if( __atomic_load_n( &j.m->seq, __ATOMIC_ACQUIRE ) != j.seq ) { ovrn++; unreserve( jf ); continue; }
         in_cnt++;
-        if( t->tc.depth && t->tc.insert( j.tag ) ) { ha++; ha_sz += j.sz; unreserve( j.f ); continue; }
+        if( t->tc.depth && t->tc.insert( j.tag ) ) { ha++; ha_sz += j.sz; unreserve( jf ); continue; }
         fd_amd_tile_ent_t * en = t->ring + (staged & mask);
-        en->src_chunk = (uint32_t)(j.f * FRAME_CHUNKS);
-        en->out_chunk = (uint32_t)(j.f * FRAME_CHUNKS);
+        en->src_chunk = (uint32_t)(jf * FRAME_CHUNKS);
+        en->out_chunk = (uint32_t)(jf * FRAME_CHUNKS);
         en->sz        = (uint32_t)j.sz;
         en->slots     = j.slots;
         staged_sl += j.slots;
-        t->ppend[staged & mask] = pending_t{ j.seq, (ushort)j.sz, j.ctl, j.tsorig, j.f, ts32, 0u, (uint)staged_sl, j.slots, 0u };
+        t->ppend[staged & mask] = pending_t{ j.seq, (ushort)j.sz, j.ctl, j.tsorig, jf, ts32, 0u, (uint)staged_sl, j.slots, 0u };
         staged++;
       }
     }
@@ -1155,7 +1205,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       if( r_blk ) inst = std::max( inst, rate );
       rate = rate > 0.0 ? 0.75 * rate + 0.25 * inst : inst;   /* ~0.8 ms memory: a burst does not flip the mode */
       r_t0 = t3; r_n0 = staged_sl; r_blk = false;
-      int nthr = fd_verify_amd_tile_mode( t->cfg.chunk_mode, thr, rate, t->rate_hi, t->rate_lo );
+      int nthr = fd_verify_amd_tile_level( t->cfg.chunk_mode, thr, rate, t->quad_hi, t->quad_lo, t->rate_hi, t->rate_lo );
       switches += nthr != thr;
       thr = nthr;
     }
@@ -1178,6 +1228,11 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       if( upto_sl == staged_sl ) upto = staged;
       else if( !txn ) upto = handed + (upto_sl - handed_sl);
       else while( upto != staged && (uint)(t->ppend[upto & mask].sl_end - (uint)handed_sl) <= (uint)(upto_sl - handed_sl) ) upto++;
+      /* TXN: a head transaction that fills a chunk's slots on its own (more
+         signatures than a latency / quad chunk holds) is a chunk of its own
+         (fd_verify_amd_tile_pack) -- it goes at once instead of waiting for
+         the cut's whole chunks behind it */
+      if( txn && upto == handed && t->ppend[handed & mask].slots >= lvl_slots( thr ) ) upto = handed + 1UL;
       if( upto != handed ) {
         ulong ds = t->desc_seq;
         uint const th = (uint)t3 & ~1u;
@@ -1188,14 +1243,18 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
             for( ulong q = 0; q < avail; q++ ) pk_slots[q] = t->ppend[(c + q) & mask].slots;
             cnt = fd_verify_amd_tile_pack( pk_slots.data(), avail, thr, &nsl );
           } else {
-            cnt = nsl = std::min( avail, thr ? CHUNK_SLOTS : LAT_SLOTS );   /* the same rule, one slot per frag */
+            cnt = nsl = std::min( avail, lvl_slots( thr ) );   /* the same rule, one slot per frag */
           }
-          bool const lat_chunk = !thr && nsl <= LAT_SLOTS;
+          /* a chunk of more slots than its level's lanes allow (a TXN frag of
+             many signatures) runs 1 lane per signature */
+          bool const lat_chunk  = thr == FD_VERIFY_AMD_LVL_LAT  && nsl <= LAT_SLOTS;
+          bool const quad_chunk = thr == FD_VERIFY_AMD_LVL_QUAD && nsl <= QUAD_SLOTS;
           fd_amd_tile_desc_t * dd = t->desc + (ds & mask);
           dd->first = c;
-          dd->count = (uint32_t)cnt | (lat_chunk ? FD_AMD_TILE_LAT : 0u);
+          dd->count = (uint32_t)cnt | (lat_chunk ? FD_AMD_TILE_LAT : 0u) | (quad_chunk ? FD_AMD_TILE_QUAD : 0u);
           t->desc_end[ds & mask] = c + cnt;
-          for( ulong q = 0; q < cnt; q++ ) t->ppend[(c + q) & mask].t_hand = th | (lat_chunk ? 1u : 0u);   /* bit 0: latency chunk */
+          /* bit 0: a latency or quad chunk (the trace's service split) */
+          for( ulong q = 0; q < cnt; q++ ) t->ppend[(c + q) & mask].t_hand = th | ((lat_chunk || quad_chunk) ? 1u : 0u);
           c += cnt; ds++;
         }
         t->desc_seq = ds;
@@ -1268,7 +1327,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
                gc_host ? 1e-6 * (double)(t0 - gc_host) : -1.0, (ulong)__atomic_load_n( &H->gdone, __ATOMIC_ACQUIRE ),
                t->desc_seq - dbase, __atomic_load_n( &H->kerr, __ATOMIC_ACQUIRE ) );
   }
-  ulong st[4] = { 0, 0, 0, 0 };
+  ulong st[6] = { 0, 0, 0, 0, 0, 0 };
   if( !t->pending && ( hipMemcpyAsync( st, t->dctl->stat, sizeof st, hipMemcpyDeviceToHost, t->pst ) != hipSuccess ||
                        hipStreamSynchronize( t->pst ) != hipSuccess ) ) rc = FD_ED25519_AMD_ERR_DEVICE;
   if( __atomic_load_n( &H->kerr, __ATOMIC_ACQUIRE ) ) {
@@ -1280,6 +1339,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   for( ulong q = r.pubd; q != staged; q++ ) unreserve( t->ppend[q & mask].fidx );
   diag->gpu_chunk_lat_cnt += st[0]; diag->gpu_chunk_thr_cnt += st[1];
   diag->gpu_frag_lat_cnt  += st[2]; diag->gpu_frag_thr_cnt  += st[3];
+  diag->gpu_chunk_quad_cnt += st[4]; diag->gpu_frag_quad_cnt += st[5];
   diag->ovrn_cnt += ovrn + r.d.ovrn_cnt; diag->bad_frag_cnt += bad;
   diag->ha_filt_cnt += ha; diag->ha_filt_sz += ha_sz;
   diag->sv_filt_cnt += r.d.sv_filt_cnt; diag->sv_filt_sz += r.d.sv_filt_sz;
@@ -1517,10 +1577,20 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   cfg.out_frame_cnt = tile_window( &cfg ) + out_depth + batch_max + 4096UL;
   cfg.framing = txn ? FD_VERIFY_AMD_FRAMING_TXN : FD_VERIFY_AMD_FRAMING_PUB_SIG_MSG;
   cfg.chunk_mode = (flags & FD_VERIFY_AMD_BENCH_CHUNK_LAT) ? FD_VERIFY_AMD_CHUNK_LATENCY
-                 : (flags & FD_VERIFY_AMD_BENCH_CHUNK_THR) ? FD_VERIFY_AMD_CHUNK_THROUGHPUT : FD_VERIFY_AMD_CHUNK_AUTO;
+                 : (flags & FD_VERIFY_AMD_BENCH_CHUNK_THR) ? FD_VERIFY_AMD_CHUNK_THROUGHPUT
+                 : (flags & FD_VERIFY_AMD_BENCH_CHUNK_QUAD) ? FD_VERIFY_AMD_CHUNK_QUAD : FD_VERIFY_AMD_CHUNK_AUTO;
+  { /* A/B: "quad_hi,quad_lo,thr_hi,thr_lo" in slots/s (0 = the default) */
+    char const * q = getenv( "FD_AMD_BENCH_LEVELS" );
+    if( q && *q ) {
+      ulong v[4] = { 0, 0, 0, 0 }; char * e = (char *)q;
+      for( int k=0; k<4 && *e; k++ ) { v[k] = strtoul( e, &e, 0 ); if( *e == ',' ) e++; }
+      cfg.quad_rate_hi = v[0]; cfg.quad_rate_lo = v[1]; cfg.thr_rate_hi = v[2]; cfg.thr_rate_lo = v[3];
+    }
+  }
   cfg.publish_cpu = (flags & FD_VERIFY_AMD_BENCH_PUB_INLINE) || !pin ? FD_VERIFY_AMD_PUBLISH_INLINE : cpus[3];
   cfg.copy_cpu    = zero_copy || (flags & FD_VERIFY_AMD_BENCH_COPY_INLINE) || !pin || cpus[4] < 0 ? FD_VERIFY_AMD_COPY_INLINE
                                                                                                : cpus[4];
+  copier_stall_ns.store( (flags & FD_VERIFY_AMD_BENCH_STALL_HELPER) ? 200000UL : 0UL, std::memory_order_relaxed );
   fd_verify_amd_tile_t * tile = fd_verify_amd_tile_new_cfg( &cfg );
   if( !tile ) { free( dcache ); return FD_ED25519_AMD_ERR_DEVICE; }
   if( zero_copy && fd_verify_amd_tile_register_dcache( tile, dcache, region ) ) {
@@ -1647,12 +1717,14 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   ulong const pass_max = tile->pass_max_ns;
   ulong const stg[6] = { tile->n_pass, tile->n_hand, tile->n_stop_window, tile->n_stop_frames, tile->n_stop_bmax, tile->n_stop_pass };
   ulong const n_steal = tile->n_steal;
+  copier_stall_ns.store( 0UL, std::memory_order_relaxed );
   fd_verify_amd_tile_delete( tile );
   free( dcache );
   if( rc ) return rc;
   ulong n = std::min( (ulong)diag.out_cnt, frag_cnt );
-  for( int k=0; k<42; k++ ) out[k] = 0.0;
+  for( int k=0; k<44; k++ ) out[k] = 0.0;
   out[41] = (double)n_steal;
+  out[42] = (double)diag.gpu_chunk_quad_cnt; out[43] = (double)diag.gpu_frag_quad_cnt;
   if( t90 > t10 && t10 && s90 > s10 ) out[40] = (double)(s90 - s10) / ((double)(t90 - t10) * 1e-9);
   /* decomposition (before lat is sorted: the samples are per published frag) */
   /* paced runs: percentiles over the steady state (n_st samples); the
@@ -1724,7 +1796,7 @@ fd_amd_tile_synth( int device, uint32_t waves, uint32_t iters, int eight, uint32
   if( !frames || !nframes || !fsz || !out_ms || !verdict || !waves || !iters || waves > 65536u || iters > 4096u ) return FD_ED25519_AMD_ERR_INVAL;
   for( uint32_t f=0; f<nframes; f++ ) if( fsz[f] < 96u || fsz[f] > 96u + FD_ED25519_AMD_MSG_MAX ) return FD_ED25519_AMD_ERR_INVAL;
   if( hipSetDevice( device ) != hipSuccess ) return FD_ED25519_AMD_ERR_DEVICE;
-  ulong const k = eight ? 8UL : 64UL, n = (ulong)waves * iters * k;
+  ulong const k = eight == 1 ? 8UL : eight == 2 ? 16UL : 64UL, n = (ulong)waves * iters * k;   /* eight: 0 throughput, 1 latency, 2 quad */
   ulong R = 1UL; while( R < n ) R <<= 1;
   std::vector<fd_amd_tile_ent_t> ent( R );
   for( ulong j=0; j<R; j++ ) ent[j] = fd_amd_tile_ent_t{ (uint32_t)((j % nframes) * FRAME_CHUNKS), 0u, fsz[j % nframes], 0u };

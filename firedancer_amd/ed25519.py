@@ -42,6 +42,12 @@ def lib():
     vp, ul, ui, i = ctypes.c_void_p, ctypes.c_ulong, ctypes.c_uint, ctypes.c_int
     L.fd_ed25519_verify.argtypes = [vp, ul, vp, vp, vp]
     L.fd_ed25519_verify.restype = i
+    L.fd_ed25519_amd_dropin_set_device.argtypes = [i]
+    L.fd_ed25519_amd_dropin_set_device.restype = i
+    L.fd_ed25519_amd_dropin_device.argtypes = []
+    L.fd_ed25519_amd_dropin_device.restype = i
+    L.fd_ed25519_amd_dropin_pick.argtypes = [ctypes.POINTER(i), i, i, ul]
+    L.fd_ed25519_amd_dropin_pick.restype = i
     L.fd_ed25519_strerror.argtypes = [i]
     L.fd_ed25519_strerror.restype = ctypes.c_char_p
     L.fd_ed25519_public_from_private.argtypes = [vp, vp, vp]
@@ -98,6 +104,10 @@ def lib():
     L.fd_verify_amd_tile_cut.restype = ul
     L.fd_verify_amd_tile_mode.argtypes = [i, i, ctypes.c_double, ctypes.c_double, ctypes.c_double]
     L.fd_verify_amd_tile_mode.restype = i
+    L.fd_verify_amd_tile_level.argtypes = [i, i] + [ctypes.c_double] * 5
+    L.fd_verify_amd_tile_level.restype = i
+    L.fd_verify_amd_tile_pack.argtypes = [vp, ul, i, c_ulong_p]
+    L.fd_verify_amd_tile_pack.restype = ul
     L.fd_verify_amd_tile_out_chunk0.argtypes = [vp]
     L.fd_verify_amd_tile_out_chunk0.restype = vp
     L.fd_verify_amd_tile_out_data_sz.argtypes = [vp]
@@ -163,6 +173,28 @@ def verify(msg, sig, public_key):
     assert len(s) == 64 and len(p) == 32
     mb = ctypes.create_string_buffer(m, max(len(m), 1))
     return lib().fd_ed25519_verify(mb if m else None, len(m), s, p, None)
+
+
+DROPIN_AUTO = -1
+
+
+def dropin_set_device(device):
+    """fd_ed25519_amd_dropin_set_device: the calling thread's device for
+    verify() (DROPIN_AUTO: the default rule).  Raises on a bad device."""
+    rc = lib().fd_ed25519_amd_dropin_set_device(int(device))
+    if rc:
+        raise EngineError("fd_ed25519_amd_dropin_set_device(%d) rc=%d" % (device, rc))
+
+
+def dropin_device():
+    """The device of the calling thread's drop-in engine (-1 before its first call)."""
+    return int(lib().fd_ed25519_amd_dropin_device())
+
+
+def dropin_pick(dev_node, cpu_node, ordinal):
+    """fd_ed25519_amd_dropin_pick: the default device rule (pure)."""
+    a = (ctypes.c_int * max(len(dev_node), 1))(*dev_node)
+    return int(lib().fd_ed25519_amd_dropin_pick(a, len(dev_node), int(cpu_node), int(ordinal)))
 
 
 def public_from_private(private_key):

@@ -18,8 +18,9 @@ CHUNK_SZ = 64
 DIAG_FIELDS = ("in_cnt", "ha_filt_cnt", "ha_filt_sz", "sv_filt_cnt", "sv_filt_sz", "out_cnt", "out_sz",
                "ovrn_cnt", "backp_cnt", "batch_cnt", "batch_sig_cnt", "bad_frag_cnt", "gpu_chunk_lat_cnt",
                "gpu_chunk_thr_cnt", "gpu_frag_lat_cnt", "gpu_frag_thr_cnt", "sv_filt_sig_cnt", "sv_filt_pubkey_cnt",
-               "sv_filt_msg_cnt", "halt_drop_cnt", "mode_switch_cnt")
-CHUNK_AUTO, CHUNK_LATENCY, CHUNK_THROUGHPUT = 0, 1, 2
+               "sv_filt_msg_cnt", "halt_drop_cnt", "mode_switch_cnt", "gpu_chunk_quad_cnt", "gpu_frag_quad_cnt")
+CHUNK_AUTO, CHUNK_LATENCY, CHUNK_THROUGHPUT, CHUNK_QUAD = 0, 1, 2, 3
+LVL_LAT, LVL_THR, LVL_QUAD = 0, 1, 2
 PUBLISH_AUTO, PUBLISH_INLINE = -2, -1
 COPY_INLINE = -1
 
@@ -32,7 +33,7 @@ class TileCfg(ctypes.Structure):
                 ("window", ctypes.c_ulong), ("lat_fill_ns", ctypes.c_ulong), ("lat_free_chunks", ctypes.c_ulong),
                 ("chunk_wait_ns", ctypes.c_ulong), ("thr_rate_hi", ctypes.c_ulong), ("thr_rate_lo", ctypes.c_ulong),
                 ("halt_grace_ns", ctypes.c_ulong),
-                ("copy_cpu", ctypes.c_int)]
+                ("copy_cpu", ctypes.c_int), ("quad_rate_hi", ctypes.c_ulong), ("quad_rate_lo", ctypes.c_ulong)]
 
     @classmethod
     def default(cls, **kw):
@@ -165,21 +166,24 @@ class VerifyTile:
 
 BENCH_ZERO_COPY, BENCH_WRITE, BENCH_LAP, BENCH_SAMPLE_BYTES = 1, 2, 4, 8
 BENCH_CHUNK_LAT, BENCH_CHUNK_THR, BENCH_PUB_INLINE, BENCH_TXN, BENCH_COPY_INLINE = 16, 32, 64, 128, 256
+BENCH_STALL_HELPER, BENCH_CHUNK_QUAD = 512, 1024
 
 
 def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, blob, frag_cnt, rate=0.0,
                  zero_copy=False, writes=False, lap=False, dcache_frames=0, expect_err=None, expect_tag=None,
-                 sample_bytes=False, chunk_mode=0, pub_inline=False, txn=False, waves=0, copy_inline=False):
+                 sample_bytes=False, chunk_mode=0, pub_inline=False, txn=False, waves=0, copy_inline=False,
+                 stall_helper=False):
     """fd_verify_amd_bench_stream: producer (rate frags/s, 0 = saturate) -> tile -> consumer; returns
     dict(frags_per_s, p50_ns, p99_ns, p999_ns, mean_batch, published, sv_filt, ovrn, mismatches, checked).
     With expect_err/expect_tag (per pool entry) the consumer checks every published frag."""
-    out = (ctypes.c_double * 42)()
+    out = (ctypes.c_double * 44)()
     p = [np.ascontiguousarray(a) for a in (pub, sig, msg_off, msg_sz, blob)]
     ee = np.ascontiguousarray(expect_err, np.int8) if expect_err is not None else None
     et = np.ascontiguousarray(expect_tag, np.uint64) if expect_tag is not None else None
     flags = (BENCH_ZERO_COPY if zero_copy else 0) | (BENCH_WRITE if writes else 0) | (BENCH_LAP if lap else 0) | \
-        (BENCH_SAMPLE_BYTES if sample_bytes else 0) | {0: 0, 1: BENCH_CHUNK_LAT, 2: BENCH_CHUNK_THR}[chunk_mode] | \
-        (BENCH_PUB_INLINE if pub_inline else 0) | (BENCH_TXN if txn else 0) | (BENCH_COPY_INLINE if copy_inline else 0)
+        (BENCH_SAMPLE_BYTES if sample_bytes else 0) | {0: 0, 1: BENCH_CHUNK_LAT, 2: BENCH_CHUNK_THR, 3: BENCH_CHUNK_QUAD}[chunk_mode] | \
+        (BENCH_PUB_INLINE if pub_inline else 0) | (BENCH_TXN if txn else 0) | (BENCH_COPY_INLINE if copy_inline else 0) | \
+        (BENCH_STALL_HELPER if stall_helper else 0)
     vp = ctypes.c_void_p
     rc = ed25519.lib().fd_verify_amd_bench_stream(int(device), int(batch_max), int(batch_wait_ns), float(rate), flags,
                                                   int(dcache_frames), p[2].shape[0],
@@ -194,5 +198,6 @@ def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, bl
             "tile_pass_max_ns", "consumer_gap_max_ns", "cut_p50_ns", "cut_p99_ns", "queue_p50_ns", "queue_p99_ns",
             "service_p50_ns", "service_p99_ns", "publish_p50_ns", "publish_p99_ns", "input_p50_ns", "input_p99_ns",
             "service_lat_chunk_p50_ns", "service_thr_chunk_p50_ns", "mode_switches", "traced", "producer_credit_wait_max_ns", "passes",
-            "hand_offs", "stop_window", "stop_frames", "stop_batch_max", "stop_pass_bound", "all_p50_ns", "all_p99_ns", "steady_frags_per_s", "copy_steals")
+            "hand_offs", "stop_window", "stop_frames", "stop_batch_max", "stop_pass_bound", "all_p50_ns", "all_p99_ns", "steady_frags_per_s", "copy_steals",
+            "gpu_chunks_quad", "gpu_frags_quad")
     return dict(zip(keys, list(out)))

@@ -60,14 +60,45 @@ typedef struct fd_sha512_private fd_sha512_t;
 /* fd_ed25519_verify -- replaces fd_ed25519.h:96-101 (impl
    fd_ed25519_user.c:345-431).  Returns FD_ED25519_SUCCESS or an
    FD_ED25519_ERR_* code, bit-exact with the reference.  Reentrant; runs as
-   a batch of one on the calling thread's default engine (device 0 unless
-   FD_ED25519_AMD_DEVICE is set).  msg==NULL fine when sz==0. */
+   a batch of one on the calling thread's own engine, on the thread's
+   device (fd_ed25519_amd_dropin_set_device below).  msg==NULL fine when
+   sz==0. */
 int
 fd_ed25519_verify( void const *  msg,
                    ulong         sz,
                    void const *  sig,
                    void const *  public_key,
                    fd_sha512_t * sha );
+
+/* Device routing of the drop-in call.  The reference runs N verify tiles
+   as threads of one process (src/app/frank/fd_frank_main.c:118-143), each
+   calling fd_ed25519_verify (fd_frank_verify_synth_load.c:380), so the
+   device is chosen per calling thread:
+   - fd_ed25519_amd_dropin_set_device( d ) (d >= 0) from the thread (e.g. at
+     its tile's boot) pins the thread's calls to HIP device d; its next call
+     moves its engine there.  FD_ED25519_AMD_DROPIN_AUTO returns the thread
+     to the default.  0, ERR_INVAL (d < -1 or not a device) or ERR_DEVICE
+     (no HIP).
+   - default (picked once, at the thread's first call):
+     FD_ED25519_AMD_DEVICE when set; else round robin over the GPUs on the
+     NUMA node of the CPU the thread runs on (a tile pinned to a core gets a
+     GPU of its own socket), over all GPUs when none is local: the rule of
+     fd_ed25519_amd_dropin_pick, with ordinal = the threads of that node that
+     took a default before it.
+   fd_ed25519_amd_dropin_device: the device of the calling thread's engine
+   (-1 before its first call).  fd_ed25519_amd_dropin_pick (pure): of
+   dev_cnt devices on NUMA nodes dev_node[] (-1 unknown), the device for
+   the ordinal-th thread on node cpu_node (-1 unknown). */
+#define FD_ED25519_AMD_DROPIN_AUTO    (-1)
+#define FD_ED25519_AMD_DROPIN_DEV_MAX (64)
+int
+fd_ed25519_amd_dropin_set_device( int device );
+
+int
+fd_ed25519_amd_dropin_device( void );
+
+int
+fd_ed25519_amd_dropin_pick( int const * dev_node, int dev_cnt, int cpu_node, ulong ordinal );
 
 /* fd_ed25519_strerror -- replaces fd_ed25519.h:108-109 (impl
    fd_ed25519_user.c:433-443): same strings. */

@@ -108,7 +108,9 @@ typedef struct {
                                 FD_TXN_AMD_ERR_PARSE, counts in sv_filt_cnt only) */
   ulong halt_drop_cnt;       /* frags taken in but neither published nor filtered: the run halted (*stop) while
                                 its output stayed backpressured past the halt grace */
-  ulong mode_switch_cnt;     /* switches between latency and throughput chunks */
+  ulong mode_switch_cnt;     /* switches between chunk levels (latency / quad / throughput) */
+  ulong gpu_chunk_quad_cnt;  /* chunks the GPU verified 4 lanes per signature (quad chunks) */
+  ulong gpu_frag_quad_cnt;   /* frags in those chunks */
 } fd_verify_amd_diag_t;
 
 typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
@@ -131,21 +133,29 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    returns FD_ED25519_AMD_ERR_DEVICE instead of waiting.
 
    Chunks.  A chunk takes one wave whatever its size and holds whole frags.
-   Latency chunks hold up to 8 signature slots verified 8 lanes per
-   signature (~0.45 ms on a SIMD of its own); throughput chunks up to 64
-   slots, 1 lane per signature (~1.2 ms alone, ~2.2 ms with every wave slot
-   busy), 3-4x the signatures per wave-ms.  A PUB_SIG_MSG frag is one slot;
-   a TXN frag takes as many slots as its signature count (its first byte),
-   and one of more than 8 signatures makes a 1-lane chunk of its own even
-   in latency mode.  All rates and counts below are in slots.
-   chunk_mode AUTO picks by the staging rate (EWMA over ~0.8 ms): throughput
-   chunks above thr_rate_hi frags/s, latency chunks again below thr_rate_lo
-   (0: 55 % / 40 % of the latency chunks' capacity, min(min(waves, 4 x CUs)
-   x 8 frags / 0.45 ms, window / 0.55 ms); never throughput chunks when the
-   window caps them below that capacity, window / 2 ms).  Whole chunks go at once; a partial latency chunk
-   goes once its oldest frag waited lat_fill_ns, or at once while fewer
-   than lat_free_chunks chunks are in flight; a partial throughput chunk
-   once its oldest waited chunk_wait_ns.  Everything staged goes at
+   Three chunk levels: latency chunks hold up to 8 signature slots verified
+   8 lanes per signature (~0.45 ms on a SIMD of its own); quad chunks up to
+   16 slots, 4 lanes per signature (~0.5 ms alone, ~0.9 ms with every wave
+   slot busy); throughput chunks up to 64 slots, 1 lane per signature (~1.2
+   ms alone, ~2.2 ms with every wave slot busy), 3-4x the latency chunks'
+   signatures per wave-ms.  A PUB_SIG_MSG frag is one slot; a TXN frag takes
+   as many slots as its signature count (its first byte), and one of more
+   slots than its level's chunk holds makes a 1-lane chunk of its own, handed
+   over at once.  All rates and counts below are in slots.
+   chunk_mode AUTO picks the level by the staging rate (EWMA over ~0.8 ms;
+   fd_verify_amd_tile_level): quad chunks above quad_rate_hi, latency chunks
+   again below quad_rate_lo (0: 55 % / 40 % of the latency chunks' capacity,
+   min(min(waves, 4 x CUs) x 8 / 0.45 ms, window / 0.55 ms)); throughput
+   chunks above thr_rate_hi, back below thr_rate_lo (0: 80 % / 65 % of the
+   quad chunks' capacity, min(min(waves, 8 x CUs) x 16 / 0.9 ms, window /
+   1.1 ms)).  Quad chunks are skipped (quad thresholds infinite, the
+   throughput ones 55 % / 40 % of the latency capacity) when their capacity
+   is under 1.25 x the latency chunks'; never throughput chunks when the
+   window caps them below the level under them, window / 2 ms.  Whole chunks
+   go at once; a partial latency or quad chunk goes once its oldest frag
+   waited lat_fill_ns, or at once while fewer than lat_free_chunks chunks are
+   in flight; a partial throughput chunk once its oldest waited
+   chunk_wait_ns.  Everything staged goes at
    batch_max staged frags, when the window or the output frames run out,
    at the end of the input, and (batch_wait_ns != 0) once the oldest waited
    batch_wait_ns.  At most `window` frags are in flight (handed over, not
@@ -180,6 +190,11 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
 #define FD_VERIFY_AMD_CHUNK_AUTO       (0)
 #define FD_VERIFY_AMD_CHUNK_LATENCY    (1)   /* every chunk a latency chunk */
 #define FD_VERIFY_AMD_CHUNK_THROUGHPUT (2)   /* every chunk a throughput chunk */
+#define FD_VERIFY_AMD_CHUNK_QUAD       (3)   /* every chunk a quad chunk */
+/* chunk levels (fd_verify_amd_tile_level, the thr argument of _cut / _pack) */
+#define FD_VERIFY_AMD_LVL_LAT  (0)           /* 8 slots, 8 lanes per signature */
+#define FD_VERIFY_AMD_LVL_THR  (1)           /* 64 slots, 1 lane per signature */
+#define FD_VERIFY_AMD_LVL_QUAD (2)           /* 16 slots, 4 lanes per signature */
 #define FD_VERIFY_AMD_PUBLISH_AUTO   (-2)
 #define FD_VERIFY_AMD_PUBLISH_INLINE (-1)
 #define FD_VERIFY_AMD_COPY_INLINE    (-1)
@@ -203,12 +218,15 @@ typedef struct {
   ulong thr_rate_lo;
   ulong halt_grace_ns;
   int   copy_cpu;         /* FD_VERIFY_AMD_COPY_INLINE, or a CPU for the copy helper */
+  ulong quad_rate_hi;     /* slots/s, 0: default (~0UL: never quad chunks in AUTO) */
+  ulong quad_rate_lo;
 } fd_verify_amd_tile_cfg_t;
 
 /* Defaults: device 0, PUB_SIG_MSG, batch_max 4096, batch_wait_ns 0,
    tcache_depth 2^16, out_frame_cnt 0, waves 0, AUTO chunks, AUTO
    publisher, window 0, lat_fill_ns 20 us, lat_free_chunks CUs / 2,
-   chunk_wait_ns 50 us, thr rates 0, halt_grace_ns 50 ms, copy inline. */
+   chunk_wait_ns 50 us, thr rates 0, halt_grace_ns 50 ms, copy inline,
+   quad rates 0. */
 void
 fd_verify_amd_tile_cfg_default( fd_verify_amd_tile_cfg_t * cfg );
 
@@ -332,10 +350,10 @@ fd_verify_amd_tile_set_verdict_log( fd_verify_amd_tile_t * tile, schar * log, ul
 
 /* The hand-off rule (pure; what fd_verify_amd_tile_run applies to its
    staged signature slots [handed, staged)): returns how far to hand over
-   now (the run then hands over the whole frags below that).  thr:
-   throughput chunks (64 slots) else latency chunks (8).
-   Whole chunks go at once; a partial latency chunk once waited_ns (its
-   oldest frag's wait) >= lat_fill_ns or while chunks_in_flight <
+   now (the run then hands over the whole frags below that).  thr: the
+   chunk level, FD_VERIFY_AMD_LVL_THR (64 slots), _QUAD (16) or _LAT (8).
+   Whole chunks go at once; a partial latency or quad chunk once waited_ns
+   (its oldest frag's wait) >= lat_fill_ns or while chunks_in_flight <
    lat_free_chunks; a partial throughput chunk once waited_ns >=
    chunk_wait_ns; everything at batch_max staged, on flush (end of input,
    or the window / frames ran out while nothing handed over is still
@@ -350,11 +368,21 @@ fd_verify_amd_tile_cut( fd_verify_amd_tile_cfg_t const * cfg, ulong staged, ulon
 int
 fd_verify_amd_tile_mode( int chunk_mode, int thr, double rate, double rate_hi, double rate_lo );
 
+/* The persistent path's chunk-level rule (pure): the next level
+   (FD_VERIFY_AMD_LVL_*) from the current one.  AUTO: a latency level moves
+   to throughput above rate_hi, else to quad above quad_hi; quad moves to
+   throughput above rate_hi and back to latency below quad_lo; throughput
+   moves down below rate_lo, to quad unless the rate is also below quad_lo.
+   The fixed modes return their level. */
+int
+fd_verify_amd_tile_level( int chunk_mode, int lvl, double rate, double quad_hi, double quad_lo, double rate_hi,
+                          double rate_lo );
+
 /* The chunk packing rule (pure): of cnt staged frags carrying slots[i]
    signature slots each, the next chunk takes the first n (returned; *nsl =
-   their slots): at most 64 frags and 64 slots (thr) or 8 slots (latency),
-   whole frags only, so a frag of more slots than that is a chunk of its
-   own (verified 1 lane per signature). */
+   their slots): at most 64 frags and the level's slots (thr:
+   FD_VERIFY_AMD_LVL_*, 64 / 16 / 8), whole frags only, so a frag of more
+   slots than that is a chunk of its own (verified 1 lane per signature). */
 ulong
 fd_verify_amd_tile_pack( uint const * slots, ulong cnt, int thr, ulong * nsl );
 
@@ -414,8 +442,9 @@ fd_verify_amd_tile_pack( uint const * slots, ulong cnt, int thr, ulong * nsl );
    frag.  out[40] (check mode) = the steady-state rate: input frags between
    10 % and 90 % of the run over the time the consumer took from one to the
    other (out[0] includes the run's ramp and drain); out[41] = copy blocks
-   the tile's stager re-copied because its helper had stalled.  out holds
-   42 doubles.
+   the tile's stager re-copied because its helper had stalled; out[42] /
+   out[43] = the GPU's quad chunks and the frags in them.  out holds 44
+   doubles.
    Threads: producer, tile, the tile's publisher and consumer each pinned
    to a CPU of their own when the process may use 5 or more (else unpinned,
    publisher inline); copy mode adds the tile's copy helper on a fifth CPU
@@ -433,6 +462,9 @@ fd_verify_amd_tile_pack( uint const * slots, ulong cnt, int thr, ulong * nsl );
                                                 blob[msg_off[k], +msg_sz[k]) (pub, sig unused); expect_err /
                                                 expect_tag per transaction (verdict, first signature's tag) */
 #define FD_VERIFY_AMD_BENCH_COPY_INLINE (256) /* copy mode: no copy helper thread */
+#define FD_VERIFY_AMD_BENCH_CHUNK_QUAD   (1024) /* chunk_mode QUAD */
+#define FD_VERIFY_AMD_BENCH_STALL_HELPER (512) /* test hook: the copy helper spins 200 us before every 4th
+                                                 block it claims, so the stager re-copies blocks (out[41]) */
 
 int
 fd_verify_amd_bench_stream( int           device,

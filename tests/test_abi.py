@@ -145,3 +145,34 @@ def test_plain_c_client_on_gpu():
     verdict equal to the drop-in call's."""
     r = subprocess.run([_client(), "gpu"], capture_output=True, text=True, timeout=100)
     assert r.returncode == 0 and "dropin_client gpu: OK" in r.stdout, r.stdout + r.stderr
+
+
+def test_dropin_default_device_rule():
+    """fd_ed25519_amd_dropin_pick: a drop-in thread that set no device gets
+    a GPU of its own NUMA node, round robin by its ordinal among that node's
+    threads (8 tiles on a 2-socket node with 4 GPUs per socket spread 1:1);
+    all GPUs round robin when none is local or the node is unknown."""
+    from firedancer_amd import ed25519
+    nodes = [0, 0, 0, 0, 1, 1, 1, 1]
+    assert [ed25519.dropin_pick(nodes, 0, k) for k in range(5)] == [0, 1, 2, 3, 0]
+    assert [ed25519.dropin_pick(nodes, 1, k) for k in range(5)] == [4, 5, 6, 7, 4]
+    assert [ed25519.dropin_pick(nodes, -1, k) for k in range(9)] == [0, 1, 2, 3, 4, 5, 6, 7, 0]
+    assert [ed25519.dropin_pick(nodes, 3, k) for k in range(3)] == [0, 1, 2]          # no GPU on node 3
+    assert [ed25519.dropin_pick([1, 0, 1, 0], 1, k) for k in range(3)] == [0, 2, 0]   # interleaved enumeration
+    assert [ed25519.dropin_pick([-1, -1], 0, k) for k in range(3)] == [0, 1, 0]       # nodes unknown
+    assert ed25519.dropin_pick([], 0, 5) == 0
+
+
+def test_dropin_set_device_refuses_bad_devices():
+    """Out-of-range devices are refused; without a HIP device any explicit
+    choice fails (no CPU fallback), the default is always accepted."""
+    from firedancer_amd import ed25519, hip
+    with pytest.raises(ed25519.EngineError):
+        ed25519.dropin_set_device(-2)
+    with pytest.raises(ed25519.EngineError):
+        ed25519.dropin_set_device(1 << 20)
+    ed25519.dropin_set_device(ed25519.DROPIN_AUTO)
+    assert ed25519.dropin_device() == -1                 # no call made on this thread yet
+    if hip.device_count() == 0:
+        with pytest.raises(ed25519.EngineError):
+            ed25519.dropin_set_device(0)

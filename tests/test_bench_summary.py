@@ -67,3 +67,12 @@ def test_malformed_tile_record_costs_only_its_summary():
     del tile["rows"][0]["zero_copy"]["at_80%"]
     line = json.loads(bench.compact_line(_out(tile), "d.json"))
     assert line["value"] == 1.0 and "summary_error" in line["stream_tile"]
+
+
+def test_unstalled_check_fails_when_every_run_stalled():
+    """A load with no stall-free run cannot pass the harness-stall view of the tail check."""
+    import bench
+    ok = {"worst_p99_over_p50_unstalled": 1.2}
+    assert bench.unstalled_ok([ok, ok])
+    assert not bench.unstalled_ok([ok, {"worst_p99_over_p50_unstalled": None}])
+    assert not bench.unstalled_ok([ok, {"worst_p99_over_p50_unstalled": 2.6}])

@@ -174,3 +174,35 @@ def test_registered_plane_must_be_registered_to_its_end(golden):
         eng.close()
         r.close()
         ed25519.host_unregister(pub[:4096])
+
+
+def test_dropin_threads_route_to_their_devices(golden):
+    """Drop-in callers on several threads, as the reference's verify tiles
+    are threads of one process (fd_frank_main.c:118-143): each thread's
+    fd_ed25519_amd_dropin_set_device holds for its own calls only (two
+    threads set device 0 -- the one GPU of this box, listed twice as the
+    multi-device tests do), a thread that set nothing takes the default
+    (a valid device), and every verdict is the reference's."""
+    import threading
+    from firedancer_amd import ed25519, hip
+    idx = [int(i) for i in np.arange(0, len(golden), 37)]
+    out, errs = {}, []
+
+    def tile(name, dev):
+        try:
+            if dev is not None:
+                ed25519.dropin_set_device(dev)
+            got = [ed25519.verify(golden.msg(i), bytes(golden.sig[i]), bytes(golden.pub[i])) for i in idx]
+            out[name] = (ed25519.dropin_device(), got)
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append(repr(e))
+
+    ths = [threading.Thread(target=tile, args=a) for a in (("a", 0), ("b", 0), ("c", None))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
+    want = [int(golden.expect[i]) for i in idx]
+    assert out["a"] == (0, want) and out["b"] == (0, want)
+    assert 0 <= out["c"][0] < hip.device_count() and out["c"][1] == want

@@ -1,11 +1,11 @@
-"""The streaming tile's hand-off and chunk-mode rules
-(fd_verify_amd_tile_cut, fd_verify_amd_tile_mode: the pure functions
+"""The streaming tile's hand-off, packing and chunk-level rules
+(fd_verify_amd_tile_cut, _pack, _mode, _level: the pure functions
 fd_verify_amd_tile_run applies to its staged frags; CPU only).  Whole chunks
-go at once (8 frags in latency mode, 64 in throughput mode); a partial
-latency chunk waits up to lat_fill_ns for company unless the GPU has few
-chunks in flight; a partial throughput chunk waits up to chunk_wait_ns;
-every flush condition hands over everything.  The mode follows the
-staging rate with hysteresis."""
+go at once (8 frags in latency mode, 16 in quad mode, 64 in throughput
+mode); a partial latency or quad chunk waits up to lat_fill_ns for company
+unless the GPU has few chunks in flight; a partial throughput chunk waits up
+to chunk_wait_ns; every flush condition hands over everything.  The level
+follows the staging rate with hysteresis."""
 import ctypes
 
 import pytest
@@ -35,7 +35,8 @@ def test_defaults():
     ed25519.lib().fd_verify_amd_tile_cfg_default(ctypes.byref(c))
     assert (c.batch_max, c.lat_fill_ns, c.chunk_wait_ns, c.halt_grace_ns) == (4096, 20000, 50000, 50000000)
     assert (c.chunk_mode, c.publish_cpu, c.waves, c.window) == (tango.CHUNK_AUTO, tango.PUBLISH_AUTO, 0, 0)
-    assert c.copy_cpu == tango.COPY_INLINE                # the copy helper is opt-in (the last field of the struct)
+    assert c.copy_cpu == tango.COPY_INLINE                # the copy helper is opt-in
+    assert (c.quad_rate_hi, c.quad_rate_lo) == (0, 0)     # quad thresholds from the tile's capacity (the last fields)
 
 
 def test_nothing_staged():
@@ -77,3 +78,52 @@ def test_mode_hysteresis_and_fixed_modes():
     assert m(tango.CHUNK_AUTO, 1, 6e6, hi, lo) == 0
     assert m(tango.CHUNK_LATENCY, 1, 50e6, hi, lo) == 0
     assert m(tango.CHUNK_THROUGHPUT, 0, 0.0, hi, lo) == 1
+
+
+def test_quad_mode_cuts_16_slot_chunks_with_the_latency_fill_rule():
+    q = tango.LVL_QUAD
+    assert cut(100 + 40, 100, thr=q) == 132              # two whole 16-frag chunks, 8 wait
+    assert cut(100 + 15, 100, thr=q) == 100              # busy GPU: a partial chunk waits for company
+    assert cut(100 + 15, 100, thr=q, waited=FILL) == 115
+    assert cut(100 + 15, 100, thr=q, inflight=FREE - 1) == 115
+    assert cut(100 + 15, 100, thr=q, flush=True) == 115
+
+
+def pack(slots, lvl):
+    a = (ctypes.c_uint * max(len(slots), 1))(*slots)
+    nsl = ctypes.c_ulong(0)
+    n = ed25519.lib().fd_verify_amd_tile_pack(a, len(slots), lvl, ctypes.byref(nsl))
+    return n, nsl.value
+
+
+def test_pack_by_level():
+    assert pack([1] * 100, tango.LVL_LAT) == (8, 8)
+    assert pack([1] * 100, tango.LVL_QUAD) == (16, 16)
+    assert pack([1] * 100, tango.LVL_THR) == (64, 64)
+    assert pack([3, 5, 6, 2, 1], tango.LVL_QUAD) == (4, 16)    # whole frags up to 16 slots
+    assert pack([3, 5, 6, 4], tango.LVL_QUAD) == (3, 14)       # 14 + 4 > 16: the 4 waits for the next chunk
+    assert pack([12, 1, 1], tango.LVL_LAT) == (1, 12)          # more than 8: a chunk of its own (1 lane each)
+    assert pack([12, 4, 1], tango.LVL_QUAD) == (2, 16)
+    assert pack([19, 1], tango.LVL_QUAD) == (1, 19)
+    assert pack([7] * 20, tango.LVL_THR) == (9, 63)
+
+
+def level(mode, cur, rate, qhi=10e6, qlo=7e6, thi=30e6, tlo=24e6):
+    return ed25519.lib().fd_verify_amd_tile_level(mode, cur, rate, qhi, qlo, thi, tlo)
+
+
+def test_level_rule_three_way_hysteresis():
+    L, Q, T = tango.LVL_LAT, tango.LVL_QUAD, tango.LVL_THR
+    A = tango.CHUNK_AUTO
+    assert level(A, L, 9e6) == L and level(A, L, 11e6) == Q and level(A, L, 31e6) == T   # a jump goes straight up
+    assert level(A, Q, 8e6) == Q and level(A, Q, 6e6) == L                                # quad holds to quad_lo
+    assert level(A, Q, 29e6) == Q and level(A, Q, 31e6) == T
+    assert level(A, T, 25e6) == T and level(A, T, 20e6) == Q and level(A, T, 5e6) == L   # throughput holds to rate_lo
+    # quad disabled (thresholds infinite): the two-level rule of fd_verify_amd_tile_mode
+    inf = float("inf")
+    for cur, rate in ((L, 9e6), (L, 31e6), (T, 25e6), (T, 20e6)):
+        two = ed25519.lib().fd_verify_amd_tile_mode(A, int(cur == T), rate, 30e6, 24e6)
+        assert level(A, cur, rate, inf, inf) == (T if two else L)
+    assert level(tango.CHUNK_LATENCY, T, 50e6) == L
+    assert level(tango.CHUNK_THROUGHPUT, L, 0.0) == T
+    assert level(tango.CHUNK_QUAD, T, 0.0) == Q and level(tango.CHUNK_QUAD, L, 50e6) == Q

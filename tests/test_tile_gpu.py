@@ -204,7 +204,7 @@ def test_tile_large_batches_vs_oracle(batch_max, zero_copy):
     signatures with 10 % corrupted frags through the persistent consumer;
     the published stream equals the oracle's accepted set, in order, with
     the right tags and bytes; every frag went through exactly one chunk of
-    at most 8 (latency) or 64 (throughput) frags."""
+    at most 8 (latency), 16 (quad) or 64 (throughput) frags."""
     from firedancer_amd import tango
     pub, sig, off, sz, blob, err, tag = _stream_pool(4096 + batch_max + zero_copy, 8192, 400)
     nf = 8 * batch_max + 12345
@@ -213,8 +213,9 @@ def test_tile_large_batches_vs_oracle(batch_max, zero_copy):
     want = int((err[np.arange(nf) % err.size] == 0).sum())
     assert r["mismatches"] == 0 and r["ovrn"] == 0
     assert r["checked"] == r["published"] == want and r["sv_filt"] == nf - want
-    assert r["gpu_frags_lat"] + r["gpu_frags_thr"] == nf
+    assert r["gpu_frags_lat"] + r["gpu_frags_quad"] + r["gpu_frags_thr"] == nf
     assert r["gpu_frags_lat"] <= 8 * r["gpu_chunks_lat"] and r["gpu_frags_thr"] <= 64 * r["gpu_chunks_thr"]
+    assert r["gpu_frags_quad"] <= 16 * r["gpu_chunks_quad"]
 
 
 def test_tile_copy_without_helper_vs_oracle():
@@ -228,6 +229,27 @@ def test_tile_copy_without_helper_vs_oracle():
     r = tango.bench_stream(0, batch_max, 0, pub, sig, off, sz, blob, nf, expect_err=err, expect_tag=tag,
                            copy_inline=True)
     want = int((err[np.arange(nf) % err.size] == 0).sum())
+    assert r["mismatches"] == 0 and r["ovrn"] == 0
+    assert r["checked"] == r["published"] == want and r["sv_filt"] == nf - want
+
+
+def test_tile_copy_helper_stalls_are_recopied_exactly():
+    """Copy mode with the copy helper (the bench pins it when the process
+    may use 6 CPUs) stalled 200 us before every 4th block it claims, under a
+    producer that rewrites a small wrapping data region: the stager re-copies
+    the stalled blocks into fresh frames (copy_steals > 0) while the late
+    helper still writes the old ones, and every published frag's verdict,
+    tag, bytes and order still equal the oracle's."""
+    import os
+    from firedancer_amd import tango
+    if len(os.sched_getaffinity(0)) < 6:
+        pytest.skip("the bench runs the copy helper only with 6 or more CPUs")
+    pub, sig, off, sz, blob, err, tag = _stream_pool(5151, 4096, 400)
+    nf = 200000
+    r = tango.bench_stream(0, 4096, 0, pub, sig, off, sz, blob, nf, writes=True, expect_err=err, expect_tag=tag,
+                           stall_helper=True)
+    want = int((err[np.arange(nf) % err.size] == 0).sum())
+    assert r["copy_steals"] > 0
     assert r["mismatches"] == 0 and r["ovrn"] == 0
     assert r["checked"] == r["published"] == want and r["sv_filt"] == nf - want
 
@@ -361,13 +383,15 @@ def test_tile_txn_reference_mutations_vs_oracle(zero_copy):
         assert tags == [_txn_tag(muts[i]) for i in acc]
 
 
-@pytest.mark.parametrize("chunk_mode", [0, 1, 2])   # AUTO, LATENCY (8 slots; > 8 signers alone, 1 lane each), THROUGHPUT
+# AUTO, LATENCY (8 slots; > 8 signers alone, 1 lane each), THROUGHPUT, QUAD (16 slots)
+@pytest.mark.parametrize("chunk_mode", [0, 1, 2, 3])
 def test_tile_txn_mixed_vs_oracle_per_chunk_mode(chunk_mode):
     """1500 multi-signer transactions (1..12 signers, 64..1232 B, legacy and
     v0) with corrupted signatures, signer keys, headers and truncations,
     through the persistent kernel with each chunk mode: every transaction's
     verdict equals the oracle's; accepted ones publish in order with their
-    first signature's tag; slots are packed <= 64 (<= 8 in latency chunks)."""
+    first signature's tag; slots are packed <= 64 (<= 8 in latency chunks,
+    <= 16 in quad chunks)."""
     import test_txn_gpu
     pays = test_txn_gpu._mixed_batch(77 + chunk_mode, 1500)
     blob, off, sz = __import__("_txn").pack(pays)
@@ -379,10 +403,63 @@ def test_tile_txn_mixed_vs_oracle_per_chunk_mode(chunk_mode):
     assert seqs == acc and tags == [_txn_tag(pays[i]) for i in acc]
     assert set(np.unique(eterr).tolist()) >= {0, -3, -4}
     if chunk_mode == 2:
-        assert diag["gpu_chunk_lat_cnt"] == 0
+        assert diag["gpu_chunk_lat_cnt"] == 0 and diag["gpu_chunk_quad_cnt"] == 0
     if chunk_mode == 1:
-        assert diag["gpu_chunk_lat_cnt"] > 0
+        assert diag["gpu_chunk_lat_cnt"] > 0 and diag["gpu_chunk_quad_cnt"] == 0
+    if chunk_mode == 3:
+        assert diag["gpu_chunk_quad_cnt"] > 0 and diag["gpu_chunk_lat_cnt"] == 0
+        assert diag["gpu_frag_quad_cnt"] <= 16 * diag["gpu_chunk_quad_cnt"]
 
+
+def test_tile_txn_many_signers_at_the_head_go_at_once():
+    """Latency chunks hold 8 slots: a head transaction of 12 signers is a
+    chunk of its own (1 lane per signature) and is handed over at once
+    rather than waiting lat_fill_ns for more staged slots -- with the fill
+    wait set to 2 s, every transaction of 9..12 signers still publishes
+    within the run, each with the oracle's verdict."""
+    import _txn
+    pays, _ = _txn.build_txns(91, 40, nsig_lo=9, nsig_hi=12, msg_hi=600)
+    blob, off, sz = _txn.pack(pays)
+    eterr, _, _ = _oracle.txn_verify_batch(blob, off, sz)
+    from firedancer_amd import tango
+    mtu_chunks = ((1232 + 127) >> 7) << 1
+    n = len(pays)
+    dcache = tango._aligned((64 * mtu_chunks * (n + 2) + 4095) & ~4095, 4096)
+    mc_in, mc_out = tango.mcache_new(1024), tango.mcache_new(1024)
+    for seq, p in enumerate(pays):
+        c = seq * mtu_chunks
+        dcache[64 * c:64 * c + len(p)] = np.frombuffer(p, np.uint8)
+        tango.publish(mc_in, seq, 0, c, len(p), 3, seq, 0)
+    tile = tango.VerifyTile(0, batch_max=4096, tcache_depth=0, framing=tango.VerifyTile.FRAMING_TXN,
+                            chunk_mode=tango.CHUNK_LATENCY, lat_fill_ns=2_000_000_000, lat_free_chunks=0)
+    log = np.full(n, 99, np.int8)
+    tile.set_verdict_log(log)
+    # the run never sees the end of its input (frag_cnt 0): only the hand-off
+    # rule can release the last staged transaction before the 2 s fill wait
+    import ctypes
+    import threading
+    import time
+    want = int((eterr == 0).sum())
+    stop, seen = ctypes.c_int(0), []
+
+    def watch():
+        t0 = time.time()
+        while time.time() - t0 < 1.5:
+            if want == 0 or int(mc_out[(want - 1) % 1024]["seq"]) == want - 1:
+                seen.append(time.time() - t0)
+                break
+            time.sleep(0.0005)
+        stop.value = 1
+    th = threading.Thread(target=watch)
+    th.start()
+    try:
+        diag, _ = tile.run(mc_in, dcache, 0, mc_out, 0, 0, stop=stop)
+    finally:
+        th.join()
+        tile.close()
+    assert seen, "the last transactions waited for the 2 s fill"
+    assert np.array_equal(log, eterr)
+    assert diag["out_cnt"] == want and diag["gpu_chunk_lat_cnt"] == 0
 
 def test_tile_txn_framing_needs_room_for_a_full_transaction():
     """TXN framing with batch_max < 19 could never stage a 19-signer
@@ -490,13 +567,13 @@ def test_tile_runs_until_stop_and_continues(zero_copy):
     assert [int(mc_out[o]["sig"]) for o in range(len(exp))] == [t for _, t in exp]
 
 
-@pytest.mark.parametrize("chunk_mode", [1, 2])      # tango.CHUNK_LATENCY, tango.CHUNK_THROUGHPUT
+@pytest.mark.parametrize("chunk_mode", [1, 2, 3])   # tango.CHUNK_LATENCY, CHUNK_THROUGHPUT, CHUNK_QUAD
 @pytest.mark.parametrize("zero_copy", [False, True])
 def test_tile_golden_codes_per_chunk_mode(golden, chunk_mode, zero_copy):
     """Every golden vector (the reference's codes, the 156 limb-compare false
     rejects included) through k_tile_persist with every chunk forced to one
-    mode: 8-lane latency chunks (k_dsm8's body) or 64-frag throughput chunks
-    (k_dsm's body).  The tile's verdict log must equal the reference's code
+    mode: 8-lane latency chunks (k_dsm8's body), 64-frag throughput chunks
+    (k_dsm's body) or 16-frag quad chunks (k_dsm4's body).  The tile's verdict log must equal the reference's code
     for every frag; the published set and the per-code SV_FILT counts follow."""
     from firedancer_amd import tango
     n = len(golden)
@@ -521,7 +598,7 @@ def test_tile_golden_codes_per_chunk_mode(golden, chunk_mode, zero_copy):
     assert diag["out_cnt"] == int((exp == 0).sum())
     assert [diag["sv_filt_sig_cnt"], diag["sv_filt_pubkey_cnt"], diag["sv_filt_msg_cnt"]] == \
         [int((exp == c).sum()) for c in (-1, -2, -3)]
-    key = "gpu_frag_lat_cnt" if chunk_mode == 1 else "gpu_frag_thr_cnt"
+    key = {1: "gpu_frag_lat_cnt", 2: "gpu_frag_thr_cnt", 3: "gpu_frag_quad_cnt"}[chunk_mode]
     assert diag[key] == n
     assert all(int(mc_out[o]["seq"]) == o for o in range(diag["out_cnt"]))
 

@@ -6,7 +6,8 @@ the box's host cores, and each stream's code histogram with the reference's
 histogram recorded in PARITY_LOG.md.  Stream k forces kernel k % 3 (k_dsm,
 k_dsm4, k_dsm8) for every chunk, or FD_SWEEP_KERNEL (e.g. k_dsmp) for all.
 
-usage: python tools/gpu_sweep.py [stream indices...] > gpurun_out/sweep.jsonl
+usage: python tools/gpu_sweep.py [stream[:kernel]...] > gpurun_out/sweep.jsonl
+       (e.g. `0:k_dsmp 1:k_dsm8`; a bare index uses FD_SWEEP_KERNEL or k % 3)
 """
 import json
 import os
@@ -36,14 +37,14 @@ STREAMS = [
 CH = 1 << 21   # signatures per sub-batch: keeps every blob under the SoA API's 32-bit offsets
 
 
-def run(k):
+def run(k, kern=None):
     seed, szlo, szhi, ref_hist = STREAMS[k]
     t0 = time.time()
     rs = (seed * 0x2545F4914F6CDD1D + 1) & 0xFFFFFFFFFFFFFFFF   # check_vs_ref.c's seeding
     prv, blob, _, sz, fk, fp = _oracle.stream_inputs(rs, N, szlo, szhi, True)
     off64 = np.zeros(N, np.int64)
     off64[1:] = np.cumsum(sz[:-1], dtype=np.int64)      # the generator's u32 offsets wrap past 4 GB
-    kern = os.environ.get("FD_SWEEP_KERNEL") or ("k_dsm", "k_dsm4", "k_dsm8")[k % 3]
+    kern = kern or os.environ.get("FD_SWEEP_KERNEL") or ("k_dsm", "k_dsm4", "k_dsm8")[k % 3]
     ed25519.select_dsm_kernel(kern)
     eng = ed25519.Engine(device=0, batch_max=1 << 20, blob_max=(1 << 20) * max(szhi, 1))
     err = np.zeros(N, np.int8)
@@ -83,9 +84,10 @@ def run(k):
 
 
 if __name__ == "__main__":
-    ks = [int(a) for a in sys.argv[1:]] or list(range(len(STREAMS)))
-    for k in ks:
-        r = run(k)
+    ks = [(int(a.split(":")[0]), a.split(":")[1] if ":" in a else None) for a in sys.argv[1:]] \
+        or [(k, None) for k in range(len(STREAMS))]
+    for k, kern in ks:
+        r = run(k, kern)
         print(json.dumps(r), flush=True)
         if r["mismatches_vs_oracle"] or not r["hist_equals_reference"]:
             sys.exit(1)

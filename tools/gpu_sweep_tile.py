@@ -27,7 +27,9 @@ from firedancer_amd import ed25519, tango  # noqa: E402
 from gpu_sweep import STREAMS, N, CH  # noqa: E402
 
 SUB = 1 << 20          # frags per tile run
-MODES = ((tango.CHUNK_LATENCY, "latency"), (tango.CHUNK_THROUGHPUT, "throughput"))
+MODES = ((tango.CHUNK_LATENCY, "latency"), (tango.CHUNK_THROUGHPUT, "throughput"), (tango.CHUNK_QUAD, "quad"))
+if os.environ.get("FD_SWEEP_TILE_MODES"):   # e.g. "quad" or "latency,quad"
+    MODES = tuple(m for m in MODES if m[1] in os.environ["FD_SWEEP_TILE_MODES"].split(","))
 
 
 def frames(pub, sig, o, z, b):
@@ -87,7 +89,7 @@ def run(k, tiles):
     off64[1:] = np.cumsum(sz[:-1], dtype=np.int64)      # the generator's u32 offsets wrap past 4 GB
     exp = np.zeros(N, np.int8)
     got = {name: np.zeros(N, np.int8) for _, name in MODES}
-    chunks = {name: [0, 0] for _, name in MODES}
+    chunks = {name: [0, 0, 0] for _, name in MODES}
     t_tile = {name: 0.0 for _, name in MODES}
     t_cpu = 0.0
     for c0 in range(0, N, CH):
@@ -121,6 +123,7 @@ def run(k, tiles):
                 got[name][c0 + s0:c0 + s1] = log
                 chunks[name][0] += diag["gpu_chunk_lat_cnt"]
                 chunks[name][1] += diag["gpu_chunk_thr_cnt"]
+                chunks[name][2] += diag["gpu_chunk_quad_cnt"]
         print("  stream %d: %d/%d" % (seed, c1, N), file=sys.stderr, flush=True)
     out = []
     for _, name in MODES:
@@ -129,7 +132,8 @@ def run(k, tiles):
         bad = np.nonzero(err != exp)[0]
         out.append({"seed": seed, "szlo": szlo, "szhi": szhi, "signatures": N, "path": "k_tile_persist",
                     "staging": "zero_copy" if ZERO_COPY else "copy",
-                    "chunk_mode": name, "gpu_chunks": {"latency": chunks[name][0], "throughput": chunks[name][1]},
+                    "chunk_mode": name, "gpu_chunks": {"latency": chunks[name][0], "throughput": chunks[name][1],
+                                                             "quad": chunks[name][2]},
                     "mismatches_vs_oracle": int(bad.size), "first_mismatches": [int(i) for i in bad[:5]],
                     "hist": hist, "hist_equals_reference": hist == ref_hist,
                     "false_rejects": int(((fk == 0) & (err == -3)).sum()),

@@ -35,7 +35,7 @@ cfgs = [(2048, 4, 0, 0), (2048, 4, 0, 1), (2048, 4, 0, 2), (2048, 4, 0, 4), (204
 if len(sys.argv) > 1:
     cfgs = [tuple(int(x) for x in a.split(",")) for a in sys.argv[1:]]
 for waves, iters, eight, where in cfgs:
-    k = 8 if eight else 64
+    k = {0: 64, 1: 8, 2: 16}[eight]
     n = waves * iters * k
     v = np.zeros(n, np.int8)
     ms = ctypes.c_double(0)
