@@ -653,6 +653,8 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
                                                                 "gpu_chunks_thr", "gpu_frags_lat", "gpu_frags_thr",
                                                                 "gpu_chunks_quad", "gpu_frags_quad",
                                                                 "mode_switches", "copy_steals")},
+                  "saturated_stager_ns_per_frag": {k: _r(sat["stager_%s_ns" % k]) for k in ("list", "copy", "stage",
+                                                                                             "hand")},
                   "saturated_stalls_us": {"producer_late_max": sat["producer_late_max_ns"] / 1e3,
                                           "tile_pass_max": sat["tile_pass_max_ns"] / 1e3,
                                           "consumer_gap_max": sat["consumer_gap_max_ns"] / 1e3}}

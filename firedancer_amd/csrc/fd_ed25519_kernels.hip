@@ -2240,8 +2240,10 @@ k_tile_persist( fd_amd_tile_args_t A ) {
     if( prof && !l ) pt[5] += __builtin_amdgcn_s_memrealtime() - tf;
     if( take && take <= 64u ) tile_chunk( A, c, take, md, scr, L, S, bi, evl, pt, tc );
     if( !l ) {
-      u32 const tk = md == TILE_MODE_LAT8 ? 0u : md == TILE_MODE_THR ? 1u : 4u;   /* dctl->stat chunk slot; frags at +2 */
-      s_tally[8u + tk] += 1UL; s_tally[10u + tk] += take;
+      /* dctl->stat slots: chunks, frags -- latency 0, 2; throughput 1, 3; quad 4, 5 */
+      u32 const tc_ = md == TILE_MODE_LAT8 ? 0u : md == TILE_MODE_THR ? 1u : 4u;
+      u32 const tf_ = md == TILE_MODE_LAT8 ? 2u : md == TILE_MODE_THR ? 3u : 5u;
+      s_tally[8u + tc_] += 1UL; s_tally[8u + tf_] += take;
       atomicAdd( (unsigned long long *)&D->done, 1ULL );   /* progress, mirrored to the host by the scout */
     }
   }

@@ -144,8 +144,13 @@ struct tsc_clock_t {
   }
 };
 
-inline ulong now_ns( void ) {
+inline tsc_clock_t const & tsc_clock( void ) {
   static tsc_clock_t const c;   /* thread-safe one-time init */
+  return c;
+}
+
+inline ulong now_ns( void ) {
+  tsc_clock_t const & c = tsc_clock();
   return c.ns0 + (ulong)((double)(long)(__rdtsc() - c.tsc0) * c.ns_per_tick);
 }
 
@@ -158,9 +163,11 @@ inline ulong now_ns( void ) {
 #define CHUNK_SLOTS  (64UL)         /* signature slots of a throughput chunk (one lane each) */
 #define LAT_SLOTS    (8UL)          /* ... of a latency chunk (8 lanes each) */
 #define QUAD_SLOTS   (16UL)         /* ... of a quad chunk (4 lanes each) */
-/* a quad chunk's service with every wave slot busy, and a frag's time in
-   flight in quad mode (the quad capacity and the window it needs) */
-#define QUAD_SVC_S    (0.9e-3)
+/* a quad chunk's service with every wave slot busy (0.97 ms measured:
+   2047 waves x 16 frags saturate at 33 M frags/s, profiles/
+   r06_quad_probe_a.jsonl), and a frag's time in flight in quad mode (the
+   quad capacity and the window it needs) */
+#define QUAD_SVC_S    (0.97e-3)
 #define QUAD_FLIGHT_S (1.1e-3)
 
 /* slots of a chunk of chunk level lvl (FD_VERIFY_AMD_LVL_*) */
@@ -349,6 +356,10 @@ struct fd_verify_amd_tile {
      stopped at the window, the output frames, batch_max staged, or the
      STAGE_PASS bound; copy blocks the stager re-copied (helper stalls) */
   ulong                n_pass, n_hand, n_stop_window, n_stop_frames, n_stop_bmax, n_stop_pass, n_steal;
+  /* the last run's stager time (TSC ticks) in passes that staged something:
+     listing, copying (copy mode), re-check + staging, hand-off; and the
+     frags those passes staged */
+  ulong                ph_tick[4], ph_frags;
   volatile int         started;    /* the current run's kernel wrote its first clock word */
 };
 
@@ -543,8 +554,11 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
   t->quad_hi = t->cfg.quad_rate_hi ? (double)t->cfg.quad_rate_hi : quad_ok ? 0.55 * cap : HUGE_VAL;
   t->quad_lo = t->cfg.quad_rate_lo ? (double)t->cfg.quad_rate_lo : quad_ok ? 0.40 * cap : HUGE_VAL;
   if( t->quad_lo > t->quad_hi ) t->quad_lo = t->quad_hi;
-  t->rate_hi = t->cfg.thr_rate_hi ? (double)t->cfg.thr_rate_hi : thr_ok ? (quad_ok ? 0.80 : 0.55) * below : HUGE_VAL;
-  t->rate_lo = t->cfg.thr_rate_lo ? (double)t->cfg.thr_rate_lo : thr_ok ? (quad_ok ? 0.65 : 0.40) * below : HUGE_VAL;
+  /* quad chunks serve up to ~90 % of their capacity at p50 ~0.8 ms (0.80 ms
+     at 30 M frags/s, against 1.28 ms in throughput chunks; 0.67 ms at 25 M),
+     so they hold until 92 % of it */
+  t->rate_hi = t->cfg.thr_rate_hi ? (double)t->cfg.thr_rate_hi : thr_ok ? (quad_ok ? 0.92 : 0.55) * below : HUGE_VAL;
+  t->rate_lo = t->cfg.thr_rate_lo ? (double)t->cfg.thr_rate_lo : thr_ok ? (quad_ok ? 0.80 : 0.40) * below : HUGE_VAL;
   if( t->rate_lo > t->rate_hi ) t->rate_lo = t->rate_hi;
   unsigned const hf = hipHostMallocMapped | hipHostMallocCoherent;
   /* The run's kernel occupies its hardware queue for the whole run, and HIP
@@ -970,6 +984,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   ulong ovrn = 0, bad = 0, ha = 0, ha_sz = 0, backp = 0, nbatch = 0, nsig = 0, switches = 0;
   ulong cdone = dbase;                   /* first descriptor not known to be finished */
   ulong n_pass = 0, n_hand = 0, n_stop_window = 0, n_stop_frames = 0, n_stop_bmax = 0, n_stop_pass = 0, n_steal = 0;
+  ulong ph_tick[4] = { 0, 0, 0, 0 }, ph_frags = 0;
   t->started = 0;
   ulong iter = 0UL, pass_t = now_ns(), pass_max = 0UL;
   ulong t_chk = pass_t, g_seen = 0UL, t_prog = pass_t, gc_first = 0UL, gc_last = 0UL, gc_host = 0UL;
@@ -1049,6 +1064,8 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
           re-checks and stages each frag in input order */
     bool full = false;
     ulong const stage_end = staged + STAGE_PASS;
+    ulong const staged_a = staged, pt0 = __rdtsc();
+    ulong pt1 = 0UL, pt2 = 0UL;
     n_pass++;
     uint const ts32 = (uint)tn;
     ulong nj = 0UL;
@@ -1109,6 +1126,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
                                            (uint)k2, 0u };
       staged++;
     }
+    pt1 = __rdtsc();
     if( nj ) {
       for( ulong k=0; k<nj; k++ ) jfr[k] = jobs[k].f;
       if( jobs != ljobs.data() && nj >= COPY_SPLIT_MIN ) {
@@ -1162,6 +1180,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       } else {
         copy_jobs( jobs, 0UL, nj );
       }
+      pt2 = __rdtsc();
       __atomic_thread_fence( __ATOMIC_ACQUIRE );
       for( ulong k=0; k<nj; k++ ) {
         copy_job_t const & j = jobs[k];
@@ -1180,6 +1199,13 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
         t->ppend[staged & mask] = pending_t{ j.seq, (ushort)j.sz, j.ctl, j.tsorig, jf, ts32, 0u, (uint)staged_sl, j.slots, 0u };
         staged++;
       }
+    }
+    ulong const pt3 = __rdtsc();
+    if( staged != staged_a || nj ) {
+      ph_tick[0] += pt1 - pt0;
+      if( pt2 ) { ph_tick[1] += pt2 - pt1; ph_tick[2] += pt3 - pt2; }
+      else        ph_tick[2] += pt3 - pt1;
+      ph_frags += staged - staged_a;
     }
     r_blk = r_blk || full;
     n_stop_bmax += staged_sl - handed_sl >= t->batch_max;
@@ -1234,6 +1260,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
          the cut's whole chunks behind it */
       if( txn && upto == handed && t->ppend[handed & mask].slots >= lvl_slots( thr ) ) upto = handed + 1UL;
       if( upto != handed ) {
+        ulong const ph0 = __rdtsc();
         ulong ds = t->desc_seq;
         uint const th = (uint)t3 & ~1u;
         for( ulong c = handed; c < upto; ) {
@@ -1264,6 +1291,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
         r.handed.store( handed, std::memory_order_release );
         if( !zc_dev ) _mm_sfence();   /* the staged copies (non-temporal stores) before the head */
         __atomic_store_n( &H->head, ds, __ATOMIC_RELEASE );
+        ph_tick[3] += __rdtsc() - ph0;
       }
     }
 
@@ -1353,6 +1381,8 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   t->pass_max_ns = pass_max;
   t->n_pass = n_pass; t->n_hand = n_hand; t->n_stop_window = n_stop_window; t->n_stop_frames = n_stop_frames;
   t->n_stop_bmax = n_stop_bmax; t->n_stop_pass = n_stop_pass; t->n_steal = n_steal;
+  for( int k=0; k<4; k++ ) t->ph_tick[k] = ph_tick[k];
+  t->ph_frags = ph_frags;
   __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
   if( in_fseq ) __atomic_store_n( in_fseq, in_seq, __ATOMIC_RELEASE );
   t->out_seq_end = r.out_seq;
@@ -1717,12 +1747,15 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   ulong const pass_max = tile->pass_max_ns;
   ulong const stg[6] = { tile->n_pass, tile->n_hand, tile->n_stop_window, tile->n_stop_frames, tile->n_stop_bmax, tile->n_stop_pass };
   ulong const n_steal = tile->n_steal;
+  double ph_ns[4];
+  for( int k=0; k<4; k++ ) ph_ns[k] = (double)tile->ph_tick[k] * tsc_clock().ns_per_tick / (double)std::max( tile->ph_frags, 1UL );
   copier_stall_ns.store( 0UL, std::memory_order_relaxed );
   fd_verify_amd_tile_delete( tile );
   free( dcache );
   if( rc ) return rc;
   ulong n = std::min( (ulong)diag.out_cnt, frag_cnt );
-  for( int k=0; k<44; k++ ) out[k] = 0.0;
+  for( int k=0; k<48; k++ ) out[k] = 0.0;
+  for( int k=0; k<4; k++ ) out[44 + k] = ph_ns[k];
   out[41] = (double)n_steal;
   out[42] = (double)diag.gpu_chunk_quad_cnt; out[43] = (double)diag.gpu_frag_quad_cnt;
   if( t90 > t10 && t10 && s90 > s10 ) out[40] = (double)(s90 - s10) / ((double)(t90 - t10) * 1e-9);

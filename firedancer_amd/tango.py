@@ -176,7 +176,7 @@ def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, bl
     """fd_verify_amd_bench_stream: producer (rate frags/s, 0 = saturate) -> tile -> consumer; returns
     dict(frags_per_s, p50_ns, p99_ns, p999_ns, mean_batch, published, sv_filt, ovrn, mismatches, checked).
     With expect_err/expect_tag (per pool entry) the consumer checks every published frag."""
-    out = (ctypes.c_double * 44)()
+    out = (ctypes.c_double * 48)()
     p = [np.ascontiguousarray(a) for a in (pub, sig, msg_off, msg_sz, blob)]
     ee = np.ascontiguousarray(expect_err, np.int8) if expect_err is not None else None
     et = np.ascontiguousarray(expect_tag, np.uint64) if expect_tag is not None else None
@@ -199,5 +199,6 @@ def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, bl
             "service_p50_ns", "service_p99_ns", "publish_p50_ns", "publish_p99_ns", "input_p50_ns", "input_p99_ns",
             "service_lat_chunk_p50_ns", "service_thr_chunk_p50_ns", "mode_switches", "traced", "producer_credit_wait_max_ns", "passes",
             "hand_offs", "stop_window", "stop_frames", "stop_batch_max", "stop_pass_bound", "all_p50_ns", "all_p99_ns", "steady_frags_per_s", "copy_steals",
-            "gpu_chunks_quad", "gpu_frags_quad")
+            "gpu_chunks_quad", "gpu_frags_quad", "stager_list_ns", "stager_copy_ns", "stager_stage_ns",
+            "stager_hand_ns")
     return dict(zip(keys, list(out)))

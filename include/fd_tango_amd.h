@@ -135,7 +135,7 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    Chunks.  A chunk takes one wave whatever its size and holds whole frags.
    Three chunk levels: latency chunks hold up to 8 signature slots verified
    8 lanes per signature (~0.45 ms on a SIMD of its own); quad chunks up to
-   16 slots, 4 lanes per signature (~0.5 ms alone, ~0.9 ms with every wave
+   16 slots, 4 lanes per signature (~0.6 ms alone, ~0.97 ms with every wave
    slot busy); throughput chunks up to 64 slots, 1 lane per signature (~1.2
    ms alone, ~2.2 ms with every wave slot busy), 3-4x the latency chunks'
    signatures per wave-ms.  A PUB_SIG_MSG frag is one slot; a TXN frag takes
@@ -146,8 +146,8 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    fd_verify_amd_tile_level): quad chunks above quad_rate_hi, latency chunks
    again below quad_rate_lo (0: 55 % / 40 % of the latency chunks' capacity,
    min(min(waves, 4 x CUs) x 8 / 0.45 ms, window / 0.55 ms)); throughput
-   chunks above thr_rate_hi, back below thr_rate_lo (0: 80 % / 65 % of the
-   quad chunks' capacity, min(min(waves, 8 x CUs) x 16 / 0.9 ms, window /
+   chunks above thr_rate_hi, back below thr_rate_lo (0: 92 % / 80 % of the
+   quad chunks' capacity, min(min(waves, 8 x CUs) x 16 / 0.97 ms, window /
    1.1 ms)).  Quad chunks are skipped (quad thresholds infinite, the
    throughput ones 55 % / 40 % of the latency capacity) when their capacity
    is under 1.25 x the latency chunks'; never throughput chunks when the
@@ -443,7 +443,10 @@ fd_verify_amd_tile_pack( uint const * slots, ulong cnt, int thr, ulong * nsl );
    10 % and 90 % of the run over the time the consumer took from one to the
    other (out[0] includes the run's ramp and drain); out[41] = copy blocks
    the tile's stager re-copied because its helper had stalled; out[42] /
-   out[43] = the GPU's quad chunks and the frags in them.  out holds 44
+   out[43] = the GPU's quad chunks and the frags in them; out[44..47] =
+   the tile thread's time per staged frag (ns, over its passes that staged
+   something): listing the pass's frags, copying them (copy mode),
+   re-checking and staging them, handing chunks over.  out holds 48
    doubles.
    Threads: producer, tile, the tile's publisher and consumer each pinned
    to a CPU of their own when the process may use 5 or more (else unpinned,

@@ -1,4 +1,4 @@
-"""PMC helper: one saturated persistent-tile run (zero copy, 1 M frags)
+"""PMC helper: one saturated persistent-tile run (zero copy, 2^20 frags or argv[2])
 and, for comparison, one resident batch of 2^18 through the batch kernels
 (k_prep, k_decomp, k_dsm forced).  Run under rocprofv3 --pmc.
     python tools/pmc_tile.py [tile|batch|both]"""
@@ -11,9 +11,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from firedancer_amd import ed25519, hip, tango, workload  # noqa: E402
 
 what = sys.argv[1] if len(sys.argv) > 1 else "both"
+frags = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
 pub, sig, off, sz, blob = workload.sig_batch(1 << 16, 200, 9)
 if what in ("tile", "both"):
-    r = tango.bench_stream(0, 16384, 0, pub, sig, off, sz, blob, 1 << 20, zero_copy=True)
+    r = tango.bench_stream(0, 16384, 0, pub, sig, off, sz, blob, frags, zero_copy=True)
     print("tile", {k: round(v) for k, v in r.items()}, flush=True)
 if what in ("batch", "both"):
     n = 1 << 18

@@ -19,7 +19,7 @@ import bench  # noqa: E402
 from firedancer_amd import ed25519, tango  # noqa: E402
 
 what = sys.argv[1] if len(sys.argv) > 1 else "all"
-rates = [float(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [10e6, 20e6, 25e6, 30e6, 35e6]
+rates = [float(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [10e6, 15e6, 20e6, 25e6, 28e6, 30e6, 32e6, 35e6]
 m = 1 << 16
 pub, sig, off, sz, blob = bench.make_workload(m, 200, 7)
 off = (off - off[0]).astype(np.uint32)
@@ -39,7 +39,8 @@ def keep(r):
             "p99_us": r["p99_ns"] / 1e3, "service_p50_us_lat_quad": r["service_lat_chunk_p50_ns"] / 1e3,
             "service_p50_us_thr": r["service_thr_chunk_p50_ns"] / 1e3, "queue_p50_us": r["queue_p50_ns"] / 1e3,
             "chunks": [int(r["gpu_chunks_lat"]), int(r["gpu_chunks_quad"]), int(r["gpu_chunks_thr"])],
-            "switches": int(r["mode_switches"]), "mismatches": int(r["mismatches"])}
+            "switches": int(r["mode_switches"]), "mismatches": int(r["mismatches"]),
+            "stager_ns": [round(r[k], 1) for k in ("stager_list_ns", "stager_copy_ns", "stager_stage_ns", "stager_hand_ns")]}
 
 
 if what in ("sat", "all"):
@@ -48,6 +49,9 @@ if what in ("sat", "all"):
             t0 = time.time()
             r = tango.bench_stream(0, bmax, 0, *pool, 1 << 22, zero_copy=True, chunk_mode=mode)
             line(kind="saturated", bmax=bmax, mode=names[mode], s=time.time() - t0, **keep(r))
+    for zc in (False, True):   # AUTO, both stagings: the stager's time per frag by phase
+        r = tango.bench_stream(0, 4096, 0, *pool, 1 << 22, zero_copy=zc)
+        line(kind="saturated", bmax=4096, mode="auto", staging="zero_copy" if zc else "copy", **keep(r))
 if what in ("paced", "all"):
     for bmax in (4096,):
         for rate in rates:
