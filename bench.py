@@ -233,13 +233,31 @@ def dsm_roofline(st, kernel_ms, n, kernel="k_dsm", note=None):
     live = float((st[0] > 0).sum())
     mac = MAC_MUL * (68 * live + 3 * I + 8 * nh + 7 * ns + 2 * live) + MAC_SQ * (4 * live + 4 * I)
     achieved = mac / (kernel_ms * 1e-3) / 1e12
-    traffic = [pmc_traffic(k, n) for k in kernel.split("+")] if "(" not in kernel else [None]
+    names = kernel.split("+") if "(" not in kernel else []
+    traffic = [pmc_traffic(k, n) for k in names] or [None]
+    raw = [pmc_traffic(k, n, corrected=False) for k in names] or [None]
     r = {"bound": "valu-imad64", "kernel": kernel, "achieved": achieved, "peak": PEAK_TMAC, "unit": "TMAC/s",
          "frac": achieved / PEAK_TMAC, "traffic": None if None in traffic else sum(traffic),
-         "traffic_note": "HBM bytes per launch from the committed PMC pass (profiles/%s: "
-                         "2*FETCH_SIZE+WRITE_SIZE KB, gfx950 correction), scaled to this batch"
+         "traffic_raw": None if None in raw else sum(raw),
+         "traffic_note": "HBM bytes per launch from the committed PMC pass (profiles/%s), scaled to this batch: "
+                         "traffic = 2*FETCH_SIZE+WRITE_SIZE (the guide's gfx950 FETCH correction, stated for wide "
+                         "coalesced reads), traffic_raw = FETCH_SIZE+WRITE_SIZE (k_dsmp's reads are 16-B row "
+                         "gathers and one-word event pops, so the truth may lie nearer the raw figure)"
                          % os.path.basename(pmc_summary_path() or "none"),
          "mac_per_sig": mac / max(live, 1.0)}
+    # the same MACs over the committed rocprofv3 kernel durations of the stage (a profiler-timed figure beside
+    # the HIP-event one), and against the clock the chip held under the kernel (GRBM_GUI_ACTIVE / 8 XCDs over
+    # the kernel's duration) instead of the 2.4 GHz the peak assumes
+    rp = rocprof_stage_ms(names) if names else None
+    if rp:
+        ms, src = rp
+        r["rocprof_stage_ms"] = ms
+        r["frac_rocprof"] = mac / (ms * 1e-3) / 1e12 / PEAK_TMAC
+        r["rocprof_source"] = "profiles/" + os.path.basename(src)
+        clk = held_clock_ghz("k_dsmp" if "k_dsmp" in names else names[-1])
+        if clk:
+            r["held_clock_ghz"] = clk
+            r["frac_at_held_clock"] = achieved / (64 * 256 * clk * 1e9 / 1e12)
     if note:
         r["note"] = note
     return r
@@ -264,16 +282,51 @@ def pmc_summary_path():
     return paths[-1] if paths else None
 
 
-def pmc_traffic(kernel, n):
+def pmc_traffic(kernel, n, corrected=True):
     """HBM bytes per launch of `kernel` at batch n, from the PMC summary
     committed under profiles/ (tools/prof_pmc.sh + tools/pmc_summary.py on
-    the same build), scaled linearly from the profiled batch size."""
+    the same build), scaled linearly from the profiled batch size.
+    corrected: 2*FETCH_SIZE+WRITE_SIZE (the guide's gfx950 correction), else
+    FETCH_SIZE+WRITE_SIZE as counted."""
     path = pmc_summary_path()
     try:
         d = json.load(open(path or ""))
-        b = d[kernel]["derived"]["hbm_bytes_per_launch"]
+        der = d[kernel]["derived"]
+        b = der["hbm_bytes_per_launch"] if corrected else (der["fetch_kb_raw"] + der["write_kb_raw"]) * 1024
         return b * n / d.get("_sigs_per_launch", 262144)
     except (OSError, KeyError, ValueError):
+        return None
+
+
+def rocprof_stats_path():
+    """The newest round's committed rocprofv3 --stats summary of the headline
+    kernels (profiles/rNN_rocprof_kernel_stats.csv, tools/final_measure.sh)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_rocprof_kernel_stats.csv")))
+    return paths[-1] if paths else None
+
+
+def rocprof_stage_ms(names):
+    """Sum of the rocprofv3 average durations of the launches `names`, ms, and the file; None if missing."""
+    import csv
+    path = rocprof_stats_path()
+    try:
+        rows = list(csv.DictReader(open(path or "")))
+        avg = {r["Name"].split("(")[0]: float(r["AverageNs"]) for r in rows}
+        return sum(avg[k] for k in names) / 1e6, path
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def held_clock_ghz(kernel):
+    """The clock the chip held under `kernel`: GRBM_GUI_ACTIVE of the committed PMC pass / 8 XCDs over the
+    kernel's committed rocprofv3 average duration (GHz), or None."""
+    try:
+        d = json.load(open(pmc_summary_path() or ""))
+        busy = d[kernel]["counters"]["GRBM_GUI_ACTIVE"] / 8.0
+        ms, _ = rocprof_stage_ms([kernel])
+        return busy / (ms * 1e-3) / 1e9
+    except (OSError, KeyError, ValueError, TypeError):
         return None
 
 
@@ -410,7 +463,8 @@ def compact_line(out, detail):
     line["config"] = out["config"]
     if out.get("roofline"):
         line["roofline"] = _pick(out["roofline"], ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic",
-                                                   "mac_per_sig"))
+                                                   "traffic_raw", "mac_per_sig", "frac_rocprof", "rocprof_source",
+                                                   "held_clock_ghz", "frac_at_held_clock"))
         line["roofline"]["traffic_unit"] = "bytes per launch (PMC)"
     if out.get("cpu_baseline"):
         cb = out["cpu_baseline"]

@@ -2081,6 +2081,14 @@ tile_gather( fd_amd_tile_args_t const & A, u32 k, u32 l, u32 e_src, u32 e_out, u
   }
 }
 
+#ifdef FD_AMD_TILE_QUAD_NOINLINE
+__device__ __noinline__ void
+tile_dsm4_call( u32 l, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_layout_t L, i32 (* __restrict__ bi)[48],
+                u64 (* __restrict__ evl)[33], u64 tc ) {
+  dsm4_body( l, n, err, ws, L, 0, bi, evl, tc );
+}
+#endif
+
 /* Verify ring entries [c0, c0 + k) (k <= 64) on this wave, claimed at
    s_memrealtime tc, in chunk mode `mode` (TILE_MODE_*: 1 lane per signature,
    8 lanes (k_dsm8's body) or 4 lanes (k_dsm4's body); the host keeps a
@@ -2133,9 +2141,21 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, u32 mode, u8 * __restri
   if( n > 32u ) decomp_body( l + 64u, n, pub, sig, err, ws, L, true );
   __syncthreads();
   TILE_STAMP( 1 );
+#if defined(FD_AMD_TILE_QUAD_LAST)   /* A/B: code placement of the three bodies */
+  if( mode == TILE_MODE_THR )        dsm_lane_body( l, n, err, ws, L, 0, bi, evl, tc );
+  else if( mode == TILE_MODE_LAT8 )  dsm8_body( l, n, err, ws, L, 0, bi, evl, tc );
+  else                               dsm4_body( l, n, err, ws, L, 0, bi, evl, tc );
+#elif defined(FD_AMD_TILE_QUAD_NOINLINE)
   if( mode == TILE_MODE_LAT8 )       dsm8_body( l, n, err, ws, L, 0, bi, evl, tc );
-  else if( mode == TILE_MODE_QUAD4 ) dsm4_body( l, n, err, ws, L, 0, bi, evl, tc );
+  else if( mode == TILE_MODE_QUAD4 ) tile_dsm4_call( l, n, err, ws, L, bi, evl, tc );
   else                               dsm_lane_body( l, n, err, ws, L, 0, bi, evl, tc );
+#else
+  if( mode == TILE_MODE_LAT8 )       dsm8_body( l, n, err, ws, L, 0, bi, evl, tc );
+#ifndef FD_AMD_TILE_NO_QUAD   /* A/B only: the tile kernel without the quad body (quad chunks run 1 lane each) */
+  else if( mode == TILE_MODE_QUAD4 ) dsm4_body( l, n, err, ws, L, 0, bi, evl, tc );
+#endif
+  else                               dsm_lane_body( l, n, err, ws, L, 0, bi, evl, tc );
+#endif
   __builtin_amdgcn_s_setprio( 0 );
   __syncthreads();
   TILE_STAMP( 2 );

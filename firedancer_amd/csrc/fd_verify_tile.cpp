@@ -170,6 +170,14 @@ inline ulong now_ns( void ) {
 #define QUAD_SVC_S    (0.97e-3)
 #define QUAD_FLIGHT_S (1.1e-3)
 
+/* a lower chunk level is taken only once the rule asked for it this long */
+#define LVL_HOLD_NS (2000000UL)
+
+/* order of the chunk levels by capacity: latency < quad < throughput */
+static inline int lvl_rank( int lvl ) {
+  return lvl == FD_VERIFY_AMD_LVL_THR ? 2 : lvl == FD_VERIFY_AMD_LVL_QUAD ? 1 : 0;
+}
+
 /* slots of a chunk of chunk level lvl (FD_VERIFY_AMD_LVL_*) */
 static inline ulong lvl_slots( int lvl ) {
   return lvl == FD_VERIFY_AMD_LVL_THR ? CHUNK_SLOTS : lvl == FD_VERIFY_AMD_LVL_QUAD ? QUAD_SLOTS : LAT_SLOTS;
@@ -993,6 +1001,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   double rate = 0.0;
   int thr = fd_verify_amd_tile_level( t->cfg.chunk_mode, FD_VERIFY_AMD_LVL_LAT, 0.0, t->quad_hi, t->quad_lo, t->rate_hi,
                                       t->rate_lo );   /* chunk level, FD_VERIFY_AMD_LVL_* */
+  ulong t_down = 0UL;                    /* since when the rule has asked for a lower level (0: it has not) */
   bool halted = false;
   uchar const * in_chunk0b = (uchar const *)in_chunk0;
   fd_verify_amd_tile_cfg_t cc = t->cfg;   /* the cut rule's parameters */
@@ -1232,6 +1241,16 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       rate = rate > 0.0 ? 0.75 * rate + 0.25 * inst : inst;   /* ~0.8 ms memory: a burst does not flip the mode */
       r_t0 = t3; r_n0 = staged_sl; r_blk = false;
       int nthr = fd_verify_amd_tile_level( t->cfg.chunk_mode, thr, rate, t->quad_hi, t->quad_lo, t->rate_hi, t->rate_lo );
+      /* up at once, down only after the rate stayed low for LVL_HOLD_NS: a
+         producer stall of a few hundred us dips the EWMA below the lower
+         threshold, and a dip from throughput into quad chunks at 80 % load
+         left a backlog that flipped the level dozens of times per run
+         (p99 5.8 ms; profiles/r06_bench_quad_a_detail.json) */
+      if( lvl_rank( nthr ) < lvl_rank( thr ) ) {
+        if( !t_down ) t_down = t3;
+        if( t3 - t_down < LVL_HOLD_NS ) nthr = thr;
+        else t_down = 0UL;
+      } else t_down = 0UL;
       switches += nthr != thr;
       thr = nthr;
     }

@@ -42,12 +42,6 @@ def lib():
     vp, ul, ui, i = ctypes.c_void_p, ctypes.c_ulong, ctypes.c_uint, ctypes.c_int
     L.fd_ed25519_verify.argtypes = [vp, ul, vp, vp, vp]
     L.fd_ed25519_verify.restype = i
-    L.fd_ed25519_amd_dropin_set_device.argtypes = [i]
-    L.fd_ed25519_amd_dropin_set_device.restype = i
-    L.fd_ed25519_amd_dropin_device.argtypes = []
-    L.fd_ed25519_amd_dropin_device.restype = i
-    L.fd_ed25519_amd_dropin_pick.argtypes = [ctypes.POINTER(i), i, i, ul]
-    L.fd_ed25519_amd_dropin_pick.restype = i
     L.fd_ed25519_strerror.argtypes = [i]
     L.fd_ed25519_strerror.restype = ctypes.c_char_p
     L.fd_ed25519_public_from_private.argtypes = [vp, vp, vp]
@@ -104,8 +98,7 @@ def lib():
     L.fd_verify_amd_tile_cut.restype = ul
     L.fd_verify_amd_tile_mode.argtypes = [i, i, ctypes.c_double, ctypes.c_double, ctypes.c_double]
     L.fd_verify_amd_tile_mode.restype = i
-    L.fd_verify_amd_tile_level.argtypes = [i, i] + [ctypes.c_double] * 5
-    L.fd_verify_amd_tile_level.restype = i
+
     L.fd_verify_amd_tile_pack.argtypes = [vp, ul, i, c_ulong_p]
     L.fd_verify_amd_tile_pack.restype = ul
     L.fd_verify_amd_tile_out_chunk0.argtypes = [vp]
@@ -145,6 +138,14 @@ def lib():
     L.fd_verify_amd_bench_stream.argtypes = [i, ul, ul, ctypes.c_double, i, ul, ul, vp, vp, vp, vp, vp, vp, vp, ul,
                                              ul, vp]
     L.fd_verify_amd_bench_stream.restype = i
+    # entry points added in round 6 (an A/B build of an earlier round, FD_AMD_LIB, lacks them)
+    opt = {"fd_ed25519_amd_dropin_set_device": ([i], i), "fd_ed25519_amd_dropin_device": ([], i),
+           "fd_ed25519_amd_dropin_pick": ([ctypes.POINTER(i), i, i, ul], i),
+           "fd_verify_amd_tile_level": ([i, i] + [ctypes.c_double] * 5, i)}
+    for name, (args, res) in opt.items():
+        if hasattr(L, name) or not os.environ.get("FD_AMD_LIB"):
+            f = getattr(L, name)
+            f.argtypes, f.restype = args, res
     _lib = L
     return L
 

@@ -143,7 +143,8 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    slots than its level's chunk holds makes a 1-lane chunk of its own, handed
    over at once.  All rates and counts below are in slots.
    chunk_mode AUTO picks the level by the staging rate (EWMA over ~0.8 ms;
-   fd_verify_amd_tile_level): quad chunks above quad_rate_hi, latency chunks
+   fd_verify_amd_tile_level; a higher level at once, a lower one only after
+   the rule asked for it for 2 ms): quad chunks above quad_rate_hi, latency chunks
    again below quad_rate_lo (0: 55 % / 40 % of the latency chunks' capacity,
    min(min(waves, 4 x CUs) x 8 / 0.45 ms, window / 0.55 ms)); throughput
    chunks above thr_rate_hi, back below thr_rate_lo (0: 92 % / 80 % of the

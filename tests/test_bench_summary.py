@@ -76,3 +76,35 @@ def test_unstalled_check_fails_when_every_run_stalled():
     assert bench.unstalled_ok([ok, ok])
     assert not bench.unstalled_ok([ok, {"worst_p99_over_p50_unstalled": None}])
     assert not bench.unstalled_ok([ok, {"worst_p99_over_p50_unstalled": 2.6}])
+
+
+def test_roofline_from_rocprof_and_held_clock(tmp_path, monkeypatch):
+    """The line's profiler-timed DSM fraction and held clock: the committed rocprofv3 averages of the stage's
+    launches, GRBM_GUI_ACTIVE / 8 XCDs over k_dsmp's duration; the traffic raw and 2x-corrected."""
+    import json
+    import numpy as np
+    import bench
+    csv = tmp_path / "r99_rocprof_kernel_stats.csv"
+    csv.write_text('"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\n'
+                   '"k_dsmp(unsigned int)",2,26000000,13000000.0,90,1,1,0\n'
+                   '"k_ai(unsigned int)",2,1000000,500000.0,5,1,1,0\n'
+                   '"k_fin(unsigned int)",2,200000,100000.0,1,1,1,0\n')
+    pmc = tmp_path / "r99_pmc_latest.json"
+    pmc.write_text(json.dumps({"_sigs_per_launch": 1 << 20, "k_dsmp": {
+        "counters": {"GRBM_GUI_ACTIVE": 8 * 2.2e9 * 13e-3},
+        "derived": {"hbm_bytes_per_launch": 2.0e10, "fetch_kb_raw": 9.0e6, "write_kb_raw": 1.0e6}},
+        **{k: {"counters": {}, "derived": {"hbm_bytes_per_launch": 0.0, "fetch_kb_raw": 0.0, "write_kb_raw": 0.0}}
+           for k in ("k_ai", "k_fin")}}))
+    monkeypatch.setattr(bench, "rocprof_stats_path", lambda: str(csv))
+    monkeypatch.setattr(bench, "pmc_summary_path", lambda: str(pmc))
+    assert abs(bench.rocprof_stage_ms(["k_ai", "k_dsmp", "k_fin"])[0] - 13.6) < 1e-9
+    assert abs(bench.held_clock_ghz("k_dsmp") - 2.2) < 1e-9
+    n = 1 << 20
+    st = np.zeros((3, n), np.uint32)
+    st[0] = 250
+    st[1] = 42
+    st[2] = 43
+    r = bench.dsm_roofline(st, 13.0, n, kernel="k_ai+k_dsmp+k_fin")
+    assert abs(r["frac_rocprof"] / r["frac"] - 13.0 / 13.6) < 1e-9
+    assert abs(r["frac_at_held_clock"] / r["frac"] - 2.4 / 2.2) < 1e-9
+    assert r["traffic"] == 2.0e10 and r["traffic_raw"] == 1.0e7 * 1024
