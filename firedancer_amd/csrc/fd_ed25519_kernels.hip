@@ -2199,6 +2199,16 @@ k_tile_persist( fd_amd_tile_args_t A ) {
   }
   bi12_fill( bi );
   __syncthreads();
+#ifdef FD_AMD_TILE_SCRATCH_TOUCH
+  /* experiment only (profiles/r06_scout_stop_fix.txt): every dword of the
+     wave's private segment (FD_AMD_TILE_SCRATCH_TOUCH bytes, the kernel's
+     private_segment_fixed_size) written once under full exec before the
+     persistent loop, so the loop's spill slots are not first touched inside
+     it */
+  _Pragma("unroll") for( int o = 0; o < FD_AMD_TILE_SCRATCH_TOUCH; o += 4 )
+    asm volatile( "scratch_store_dword off, %0, off offset:%1" :: "v"(0), "i"(o) : "memory" );
+  asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
+#endif
   /* this wave's mirror word: its XCD's (HW_REG_XCC_ID) */
   u32 const xcc = __builtin_amdgcn_s_getreg( 20 | (0 << 6) | (3 << 11) ) % FD_AMD_TILE_MIRRORS;
   u64 const * mw = &D->mw[xcc].w;

@@ -5,6 +5,8 @@ plus paced runs at fixed offered rates (zero copy 4096).  Each build runs in
 its own process (FD_AMD_LIB); one JSON line per run.
 
 usage: python tools/tile_lib_ab.py <rounds> <frags> lib1.so [lib2.so ...]   (a lib "-" = the product)
+env: AB_RATES="27e6, 43e6" paced rates (empty: none), AB_SAT="((4096, True),)" saturated (batch_max, zero copy)
+     runs, AB_CONTINUE=1 records a failing build and goes on (an experiment's control)
 """
 import json
 import os
@@ -33,7 +35,7 @@ tag = np.array([int.from_bytes(hashlib.sha512(bytes(sig[i][:32]) + bytes(pub[i])
                 bytes(blob[off[i]:off[i] + sz[i]])).digest()[:8], "little") for i in range(m)], np.uint64)
 pool = (pub, sig, off, sz, blob)
 out = []
-for bmax, zc in ((4096, True), (16384, True), (16384, False)):
+for bmax, zc in %(sat)s:
     r = tango.bench_stream(0, bmax, 0, *pool, frags, zero_copy=zc, expect_err=err, expect_tag=tag, sample_bytes=True)
     out.append({"kind": "sat", "bmax": bmax, "zc": zc, "mfps": round(r["frags_per_s"] / 1e6, 2),
                 "steady_mfps": round(r["steady_frags_per_s"] / 1e6, 2), "mismatches": int(r["mismatches"]),
@@ -54,10 +56,13 @@ if __name__ == "__main__":
             env = dict(os.environ)
             if lib != "-":
                 env["FD_AMD_LIB"] = os.path.abspath(lib)
-            p = subprocess.run([sys.executable, "-c", CHILD % {"root": ROOT, "frags": frags, "rates": rates}],
+            sat = os.environ.get("AB_SAT", "((4096, True), (16384, True), (16384, False))")
+            p = subprocess.run([sys.executable, "-c", CHILD % {"root": ROOT, "frags": frags, "rates": rates, "sat": sat}],
                                env=env, capture_output=True, text=True, timeout=300)
             if p.returncode:
                 print(json.dumps({"round": r, "lib": lib, "rc": p.returncode, "err": p.stderr[-800:]}), flush=True)
+                if os.environ.get("AB_CONTINUE"):   # a build expected to fail (an experiment's control)
+                    continue
                 sys.exit(1)
             for x in json.loads(p.stdout.strip().splitlines()[-1]):
                 x.update(round=r, lib=lib)

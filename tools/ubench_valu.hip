@@ -2,7 +2,7 @@
 // instructions the verify kernels are built from (the roofline denominator,
 // BASELINE.md "Roofline framing": v_mad_i64_i32 issue rate x 256 CU x clock).
 //
-//   hipcc --offload-arch=gfx950 -O3 tools/ubench_valu.hip -o tools/ubench_valu && tools/ubench_valu
+//   hipcc --offload-arch=gfx950 -O3 tools/ubench_valu.hip -o tools/ubench_valu && tools/ubench_valu [lone]
 //
 // Each kernel runs 16 independent dependency chains per lane of one
 // instruction (inline asm, so nothing is folded), 8 waves per SIMD.
@@ -63,7 +63,59 @@ static void run( char const * name ) {
   (void)hipFree( out ); (void)hipFree( clk );
 }
 
-int main() {
+/* One wave alone on the chip (one 64-lane block): cycles per instruction
+   (s_memtime) with NC independent chains per lane -- NC = 1 is the
+   dependent latency, large NC the lone wave's issue interval (the regime of
+   the latency kernels, one wave per SIMD). */
+template<int OP, int NC>
+__global__ void __launch_bounds__(64) k_lone( uint64_t * out, int iters, uint64_t * clk ) {
+  uint64_t acc[NC];
+  uint32_t a = threadIdx.x * 2654435761u, b = a ^ 0x9e3779b9u;
+#pragma unroll
+  for( int k=0; k<NC; k++ ) acc[k] = ((uint64_t)(a + k) << 32) | (b + 3*k);
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for( int i=0; i<iters; i++ ) {
+#pragma unroll
+    for( int k=0; k<NC; k++ ) {
+      if( OP==0 ) { uint64_t sd; asm volatile( "v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(acc[k]), "=s"(sd) : "v"(a), "v"(b) ); }
+      if( OP==3 ) { asm volatile( "v_lshl_add_u64 %0, %0, 0, %1" : "+v"(acc[k]) : "v"(acc[(k+1)%NC]) ); }
+      if( OP==4 ) { asm volatile( "v_ashrrev_i64 %0, 3, %0" : "+v"(acc[k]) ); }
+      if( OP==5 ) { uint32_t lo = (uint32_t)acc[k]; asm volatile( "v_add_u32 %0, %0, %1" : "+v"(lo) : "v"(b) ); acc[k] = (acc[k] & ~0xffffffffull) | lo; }
+      if( OP==8 ) { uint32_t lo = (uint32_t)acc[k]; asm volatile( "v_cndmask_b32 %0, %0, %1, vcc" : "+v"(lo) : "v"(b) ); acc[k] = (acc[k] & ~0xffffffffull) | lo; }
+      if( OP==9 ) { uint32_t lo = (uint32_t)acc[k]; asm volatile( "v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(lo) ); acc[k] = (acc[k] & ~0xffffffffull) | lo; }
+    }
+  }
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  uint64_t x = 0;
+#pragma unroll
+  for( int k=0; k<NC; k++ ) x ^= acc[k];
+  out[threadIdx.x] = x;
+  if( threadIdx.x == 0 ) clk[0] = t1 - t0;
+}
+
+template<int OP, int NC>
+static void lone( char const * name ) {
+  uint64_t *out, *clk;
+  int iters = 4000;
+  (void)hipMalloc( &out, 8UL * 64 ); (void)hipMalloc( &clk, 16 );
+  hipLaunchKernelGGL( (k_lone<OP, NC>), dim3(1), dim3(64), 0, 0, out, 10, clk );
+  hipLaunchKernelGGL( (k_lone<OP, NC>), dim3(1), dim3(64), 0, 0, out, iters, clk );
+  (void)hipDeviceSynchronize();
+  uint64_t c; (void)hipMemcpy( &c, clk, 8, hipMemcpyDeviceToHost );
+  printf( "lone wave %-16s %2d chains  %6.2f cycles per instruction\n", name, NC, (double)c / ((double)iters * NC) );
+  (void)hipFree( out ); (void)hipFree( clk );
+}
+
+int main( int argc, char ** argv ) {
+  if( argc > 1 ) {   /* "lone": the one-wave table */
+    lone<0,1>( "v_mad_i64_i32" ); lone<0,2>( "v_mad_i64_i32" ); lone<0,5>( "v_mad_i64_i32" ); lone<0,16>( "v_mad_i64_i32" );
+    lone<3,1>( "v_lshl_add_u64" ); lone<3,16>( "v_lshl_add_u64" );
+    lone<4,1>( "v_ashrrev_i64" ); lone<4,16>( "v_ashrrev_i64" );
+    lone<5,1>( "v_add_u32" ); lone<5,16>( "v_add_u32" );
+    lone<8,1>( "v_cndmask_b32" ); lone<8,16>( "v_cndmask_b32" );
+    lone<9,1>( "v_mov_b32_dpp" ); lone<9,16>( "v_mov_b32_dpp" );
+    return 0;
+  }
   run<0>( "v_mad_i64_i32" );
   run<1>( "v_mad_u64_u32" );
   run<2>( "v_mul_lo_u32" );
