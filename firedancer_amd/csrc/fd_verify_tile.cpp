@@ -314,7 +314,10 @@ tile_window( fd_verify_amd_tile_cfg_t const * c ) {
      at 80 % load shows up as input wait in the tail: 2^17 did at batch_max
      1024 on a 60 M frags/s box, profiles/r05_bench_tile_window1024.json) */
   if( c->batch_max >= (1UL << 10) ) return 1UL << 18;
-  return std::max( 64UL * c->batch_max, 1UL << 15 );   /* latency chunks at ~18 M frags/s x ~1 ms */
+  /* small batch caps: quad chunks carry ~26 M frags/s at 80 % load for
+     ~0.7 ms each; a 2^15 window bound them there (input wait p99 ~1 ms,
+     p99 3 x p50; profiles/r06_bench_quad_b_detail.json) */
+  return std::max( 64UL * c->batch_max, 1UL << 16 );
 }
 
 struct fd_verify_amd_tile {
@@ -985,6 +988,12 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   std::vector<uint>       jfr( zc_dev ? 0UL : STAGE_PASS );     /* the frame each listed frag is staged from (a
                                                                   re-copied block's fresh frames: never written
                                                                   into the posted jobs, which the helper reads) */
+  /* copy mode with the helper is pipelined: a pass posted to the helper is
+     copied while the stager lists the next one, and staged (in input order,
+     before that next pass) once its blocks are done -- the stager copies
+     what the helper has not claimed by then */
+  struct { bool on; ulong g, s, nj, sl, seq0; std::vector<uint> jf; } pend = { false, 0UL, 0UL, 0UL, 0UL, 0UL, {} };
+  if( !zc_dev ) pend.jf.resize( STAGE_PASS );
 
   ulong in_seq = in_seq0, staged = base, handed = base;
   ulong staged_sl = 0UL, handed_sl = 0UL;   /* signature slots staged / handed over in this run */
@@ -1028,9 +1037,80 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   /* copy mode's producer credit: everything copied -- but never past a frag
      whose source an orphaned helper block may still be reading */
   auto copy_rel = [&]() -> ulong {
-    ulong rel = in_seq;
+    ulong rel = pend.on ? pend.seq0 : in_seq;   /* a posted pass is not copied yet */
     for( orphan_t const & o : orphans ) rel = std::min( rel, cp->jobs[o.s][o.b * cp->bsz[o.s].load( std::memory_order_relaxed )].seq );
     return rel;
+  };
+  /* re-check each copied frag's mcache line and stage it, in input order */
+  auto stage_jobs = [&]( copy_job_t const * js, uint const * jf_, ulong n, uint ts ) {
+    __atomic_thread_fence( __ATOMIC_ACQUIRE );
+    for( ulong k=0; k<n; k++ ) {
+      copy_job_t const & j = js[k];
+      uint const jf = jf_[k];
+      /* a frag lapped while it was copied is dropped (speculative read,
+         then seq re-check); its frame is free again */
+      if( __atomic_load_n( &j.m->seq, __ATOMIC_ACQUIRE ) != j.seq ) { ovrn++; unreserve( jf ); continue; }
+      in_cnt++;
+      if( t->tc.depth && t->tc.insert( j.tag ) ) { ha++; ha_sz += j.sz; unreserve( jf ); continue; }
+      fd_amd_tile_ent_t * en = t->ring + (staged & mask);
+      en->src_chunk = (uint32_t)(jf * FRAME_CHUNKS);
+      en->out_chunk = (uint32_t)(jf * FRAME_CHUNKS);
+      en->sz        = (uint32_t)j.sz;
+      en->slots     = j.slots;
+      staged_sl += j.slots;
+      t->ppend[staged & mask] = pending_t{ j.seq, (ushort)j.sz, j.ctl, j.tsorig, jf, ts, 0u, (uint)staged_sl, j.slots, 0u };
+      staged++;
+    }
+  };
+  /* the posted pass: claim the blocks the helper has not, wait a little for
+     the helper's own, re-copy what is still missing into fresh frames (the
+     old ones become orphans), then stage it */
+  auto finish_pend = [&]( uint ts ) {
+    ulong const tA = __rdtsc();
+    ulong const g = pend.g, s = pend.s, nj_ = pend.nj, bz = cp->bsz[s].load( std::memory_order_relaxed ), nb = CP_NB;
+    copy_job_t const * js = cp->jobs[s];
+    ulong mine = 0UL;   /* bit b: the stager copied block b */
+    for( ;; ) {
+      ulong c = cp->claim.load( std::memory_order_acquire );
+      ulong const b = c & 0xffffUL;
+      if( (c >> 16) != g || b >= nb ) break;
+      if( cp->claim.compare_exchange_weak( c, c + 1UL, std::memory_order_acq_rel ) ) {
+        copy_jobs( js, b * bz, std::min( nj_, (b + 1UL) * bz ) );
+        mine |= 1UL << b;
+      }
+    }
+    ulong const tw = now_ns();
+    for( ulong b = 0; b < nb && b * bz < nj_; b++ ) {
+      if( mine >> b & 1UL ) continue;
+      while( cp->done[s][b].load( std::memory_order_acquire ) != g && now_ns() - tw < CP_STEAL_NS ) _mm_pause();
+      if( cp->done[s][b].load( std::memory_order_acquire ) == g ) continue;
+      orphan_t o; o.g = g; o.s = s; o.b = b;
+      ulong const lo = b * bz, hi = std::min( nj_, lo + bz );
+      bool okb = true;
+      std::vector<uint> fresh;
+      for( ulong k = lo; k < hi && okb; k++ ) {
+        uint f2; bool credit;
+        okb = reserve( &f2, &credit );
+        if( okb ) fresh.push_back( f2 );
+      }
+      if( !okb ) {   /* no frames to re-copy into: wait for the helper after all */
+        for( uint f2 : fresh ) unreserve( f2 );
+        while( cp->done[s][b].load( std::memory_order_acquire ) != g ) _mm_pause();
+        continue;
+      }
+      for( ulong k = lo; k < hi; k++ ) {
+        o.frames.push_back( js[k].f );
+        pend.jf[k] = fresh[k - lo];
+        stage_copy_nt( t->out_base + (ulong)pend.jf[k] * FD_VERIFY_AMD_FRAME_SZ, js[k].src, js[k].sz );
+      }
+      orphan_cnt[s]++;
+      orphans.push_back( std::move( o ) );
+      n_steal++;
+    }
+    ulong const tB = __rdtsc();
+    stage_jobs( js, pend.jf.data(), nj_, ts );
+    pend.on = false;
+    ph_tick[1] += tB - tA; ph_tick[2] += __rdtsc() - tB;
   };
 
   for( ;; ) {
@@ -1064,7 +1144,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
        reports the output backpressured past the halt grace */
     bool const stopping = stop && __atomic_load_n( stop, __ATOMIC_ACQUIRE ) != 0;
     bool done_in = (frag_cnt && in_seq - in_seq0 >= frag_cnt) || stopping;
-    if( done_in && pubd == staged ) break;
+    if( done_in && pubd == staged && !pend.on ) break;
     if( r.halt.load( std::memory_order_acquire ) ) { halted = true; break; }
 
     /* 2. stage (at most STAGE_PASS frags, so hand-offs keep flowing).  Copy
@@ -1082,9 +1162,10 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     ulong const gnext = cgen + 1UL, snext = gnext % CP_NJ;
     copy_job_t * jobs = ( cp && !orphan_cnt[snext] ) ? cp->jobs[snext] : ljobs.data();
     ulong sl_pass = 0UL;                   /* slots listed in this pass (copy mode) */
-    while( !done_in && staged_sl + sl_pass - handed_sl < t->batch_max && staged + nj != stage_end ) {
+    ulong const pnj = pend.on ? pend.nj : 0UL, psl = pend.on ? pend.sl : 0UL;   /* the posted pass, not staged yet */
+    while( !done_in && staged_sl + psl + sl_pass - handed_sl < t->batch_max && staged + nj != stage_end ) {
       if( frag_cnt && in_seq - in_seq0 >= frag_cnt ) break;
-      if( staged + nj - pubd >= W ) { full = true; n_stop_window++; break; }
+      if( staged + pnj + nj - pubd >= W ) { full = true; n_stop_window++; break; }
       fd_frag_meta_t const * m = in_mcache + (in_seq & (in_depth-1UL));
       __builtin_prefetch( in_mcache + ((in_seq + 16UL) & (in_depth-1UL)) );
       ulong seq_found = __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE );
@@ -1136,89 +1217,35 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       staged++;
     }
     pt1 = __rdtsc();
+    /* copy mode: first the posted pass (its frags precede this pass's) */
+    if( pend.on ) finish_pend( ts32 );
     if( nj ) {
       for( ulong k=0; k<nj; k++ ) jfr[k] = jobs[k].f;
       if( jobs != ljobs.data() && nj >= COPY_SPLIT_MIN ) {
-        /* post the pass to the helper; claim blocks beside it */
-        ulong const g = gnext, s = snext, bz = (nj + 1UL) / 2UL, nb = CP_NB;
+        /* post the pass to the helper; it is staged after the next pass's listing */
+        ulong const g = gnext, s = snext, bz = (nj + 1UL) / 2UL;
         cgen = g;
         cp->nj[s].store( nj, std::memory_order_relaxed );
         cp->bsz[s].store( bz, std::memory_order_relaxed );
         cp->claim.store( g << 16, std::memory_order_release );
-        ulong mine = 0UL;   /* bit b: the stager copied block b */
-        for( ;; ) {
-          ulong c = cp->claim.load( std::memory_order_acquire );
-          ulong const b = c & 0xffffUL;
-          if( b >= nb ) break;
-          if( cp->claim.compare_exchange_weak( c, c + 1UL, std::memory_order_acq_rel ) ) {
-            copy_jobs( jobs, b * bz, std::min( nj, (b + 1UL) * bz ) );
-            mine |= 1UL << b;
-          }
-        }
-        /* the helper's blocks: wait a little, then re-copy what is still
-           missing into fresh frames (the old ones become orphans) */
-        ulong const tw = now_ns();
-        for( ulong b = 0; b < nb; b++ ) {
-          if( mine >> b & 1UL ) continue;
-          while( cp->done[s][b].load( std::memory_order_acquire ) != g && now_ns() - tw < CP_STEAL_NS ) _mm_pause();
-          if( cp->done[s][b].load( std::memory_order_acquire ) == g ) continue;
-          orphan_t o; o.g = g; o.s = s; o.b = b;
-          ulong const lo = b * bz, hi = std::min( nj, lo + bz );
-          bool okb = true;
-          std::vector<uint> fresh;
-          for( ulong k = lo; k < hi && okb; k++ ) {
-            uint f2; bool credit;
-            okb = reserve( &f2, &credit );
-            if( okb ) fresh.push_back( f2 );
-          }
-          if( !okb ) {   /* no frames to re-copy into: wait for the helper after all */
-            for( uint f2 : fresh ) unreserve( f2 );
-            while( cp->done[s][b].load( std::memory_order_acquire ) != g ) _mm_pause();
-            continue;
-          }
-          for( ulong k = lo; k < hi; k++ ) {
-            copy_job_t const & jb = jobs[k];
-            o.frames.push_back( jb.f );
-            jfr[k] = fresh[k - lo];
-            stage_copy_nt( t->out_base + (ulong)jfr[k] * FD_VERIFY_AMD_FRAME_SZ, jb.src, jb.sz );
-          }
-          orphan_cnt[s]++;
-          orphans.push_back( std::move( o ) );
-          n_steal++;
-        }
+        pend.on = true; pend.g = g; pend.s = s; pend.nj = nj; pend.sl = sl_pass; pend.seq0 = jobs[0].seq;
+        std::swap( pend.jf, jfr );
+        if( jfr.size() < STAGE_PASS ) jfr.resize( STAGE_PASS );
       } else {
+        ulong const c0 = __rdtsc();
         copy_jobs( jobs, 0UL, nj );
-      }
-      pt2 = __rdtsc();
-      __atomic_thread_fence( __ATOMIC_ACQUIRE );
-      for( ulong k=0; k<nj; k++ ) {
-        copy_job_t const & j = jobs[k];
-        uint const jf = jfr[k];
-        /* a frag lapped while it was copied is dropped (speculative read,
-           then seq re-check); its frame is free again */
-        if( __atomic_load_n( &j.m->seq, __ATOMIC_ACQUIRE ) != j.seq ) { ovrn++; unreserve( jf ); continue; }
-        in_cnt++;
-        if( t->tc.depth && t->tc.insert( j.tag ) ) { ha++; ha_sz += j.sz; unreserve( jf ); continue; }
-        fd_amd_tile_ent_t * en = t->ring + (staged & mask);
-        en->src_chunk = (uint32_t)(jf * FRAME_CHUNKS);
-        en->out_chunk = (uint32_t)(jf * FRAME_CHUNKS);
-        en->sz        = (uint32_t)j.sz;
-        en->slots     = j.slots;
-        staged_sl += j.slots;
-        t->ppend[staged & mask] = pending_t{ j.seq, (ushort)j.sz, j.ctl, j.tsorig, jf, ts32, 0u, (uint)staged_sl, j.slots, 0u };
-        staged++;
+        pt2 = __rdtsc();
+        stage_jobs( jobs, jfr.data(), nj, ts32 );
+        ph_tick[1] += pt2 - c0; ph_tick[2] += __rdtsc() - pt2;
       }
     }
-    ulong const pt3 = __rdtsc();
-    if( staged != staged_a || nj ) {
+    if( staged != staged_a || nj ) {   /* listing (zero copy: listing and staging); copy mode timed its copy and stage above */
       ph_tick[0] += pt1 - pt0;
-      if( pt2 ) { ph_tick[1] += pt2 - pt1; ph_tick[2] += pt3 - pt2; }
-      else        ph_tick[2] += pt3 - pt1;
       ph_frags += staged - staged_a;
     }
     r_blk = r_blk || full;
     n_stop_bmax += staged_sl - handed_sl >= t->batch_max;
-    n_stop_pass += staged == stage_end;
+    n_stop_pass += staged == stage_end || nj == STAGE_PASS;
     __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
     /* copy mode releases what it copied -- but never past a frag whose copy
        an orphaned helper block may still be reading */
@@ -1353,6 +1380,8 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     if( cth.joinable() ) cth.join();   /* it finishes the block it holds first */
     for( orphan_t const & o : orphans ) for( uint f : o.frames ) unreserve( f );
     orphans.clear();
+    /* a posted pass never staged (halted, or an error): its frames are free */
+    if( pend.on ) { for( ulong k=0; k<pend.nj; k++ ) unreserve( pend.jf[k] ); pend.on = false; }
     delete cp;
   }
   __atomic_store_n( &H->stop, 1u, __ATOMIC_RELEASE );

@@ -115,7 +115,7 @@ def tile_window(batch_max, window=0):
         return int(window)
     if batch_max >= 1 << 10:
         return 1 << 18
-    return max(64 * batch_max, 1 << 15)
+    return max(64 * batch_max, 1 << 16)
 
 
 def tile_budget(batch_max, cpus, zero_copy=True, window=0, out_frame_cnt=0):

@@ -161,7 +161,7 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    at the end of the input, and (batch_wait_ns != 0) once the oldest waited
    batch_wait_ns.  At most `window` frags are in flight (handed over, not
    yet published; 0: 2^18 from batch_max 1024, else
-   64 x batch_max, >= 2^15).
+   64 x batch_max, >= 2^16).
    Host side.  The caller's thread polls, dedups and stages; publishing
    runs on a second host thread when publish_cpu >= 0 (pinned there) or,
    with FD_VERIFY_AMD_PUBLISH_AUTO, when the caller's CPU set holds another
@@ -211,7 +211,7 @@ typedef struct {
   int   chunk_mode;       /* FD_VERIFY_AMD_CHUNK_* */
   int   publish_cpu;      /* FD_VERIFY_AMD_PUBLISH_AUTO / _INLINE, or a CPU */
   ulong window;           /* frags in flight; 0: 2^18 from batch_max 1024,
-                             else max( 64 x batch_max, 2^15 ) */
+                             else max( 64 x batch_max, 2^16 ) */
   ulong lat_fill_ns;
   ulong lat_free_chunks;
   ulong chunk_wait_ns;
