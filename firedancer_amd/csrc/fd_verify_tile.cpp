@@ -534,6 +534,41 @@ fd_verify_amd_tile_delete( fd_verify_amd_tile_t * t ) {
   delete t;
 }
 
+/* The chunk levels' rate thresholds (slots/s) for the tile's share and
+   window, at the start of every run (the framing may change between runs).
+   TXN chunks hold whole transactions, so a quad chunk's 16 slots are ~3/4
+   filled on a mix of 1..12 signers: its capacity in slots is taken at
+   0.75 x (at 92 % of the full figure, TXN quad chunks queued for ms at 28 M
+   slots/s, profiles/r06_bench_quad_c_detail.json). */
+static void
+tile_set_levels( fd_verify_amd_tile_t * t ) {
+  /* latency chunks' capacity: one 8-slot chunk per SIMD at ~0.45 ms, and
+     the window over their ~0.55 ms in flight.  Throughput chunks keep a frag
+     in flight 1.3-2.2 ms, so a small window caps them at W / 2 ms: when that
+     is below the latency chunks' capacity the tile stays in latency chunks
+     (batch_max 256: 8 M vs 18 M frags/s).  Rates are signature slots/s. */
+  double const cap  = std::min( (double)std::min( (ulong)t->waves - 1UL, 4UL * (ulong)t->cus ) * 8.0 / 450e-6,
+                                (double)t->window / 550e-6 );
+  /* quad chunks (16 slots, 4 lanes each): two per SIMD at ~0.9 ms, a frag
+     ~1.1 ms in flight; used between the two when they carry well above the
+     latency chunks' capacity */
+  double const qpack = t->framing == FD_VERIFY_AMD_FRAMING_TXN ? 0.75 : 1.0;
+  double const qcap = qpack * std::min( (double)std::min( (ulong)t->waves - 1UL, 8UL * (ulong)t->cus ) * (double)QUAD_SLOTS / QUAD_SVC_S,
+                                (double)t->window / QUAD_FLIGHT_S );
+  bool const   quad_ok = qcap > 1.25 * cap;
+  double const below = quad_ok ? qcap : cap;   /* the capacity under throughput chunks */
+  bool const   thr_ok = (double)t->window / 2e-3 > below;
+  t->quad_hi = t->cfg.quad_rate_hi ? (double)t->cfg.quad_rate_hi : quad_ok ? 0.55 * cap : HUGE_VAL;
+  t->quad_lo = t->cfg.quad_rate_lo ? (double)t->cfg.quad_rate_lo : quad_ok ? 0.40 * cap : HUGE_VAL;
+  if( t->quad_lo > t->quad_hi ) t->quad_lo = t->quad_hi;
+  /* quad chunks serve up to ~90 % of their capacity at p50 ~0.8 ms (0.80 ms
+     at 30 M frags/s, against 1.28 ms in throughput chunks; 0.67 ms at 25 M),
+     so they hold until 92 % of it */
+  t->rate_hi = t->cfg.thr_rate_hi ? (double)t->cfg.thr_rate_hi : thr_ok ? (quad_ok ? 0.92 : 0.55) * below : HUGE_VAL;
+  t->rate_lo = t->cfg.thr_rate_lo ? (double)t->cfg.thr_rate_lo : thr_ok ? (quad_ok ? 0.80 : 0.40) * below : HUGE_VAL;
+  if( t->rate_lo > t->rate_hi ) t->rate_lo = t->rate_hi;
+}
+
 /* The persistent consumer's resources (allocated at the first run):
    control words, ring, descriptors and results in mapped coherent host
    memory, the device control block, per-wave scratch.  A failure frees
@@ -547,30 +582,7 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
   uint32_t waves = tile_share( t );
   if( waves < 2u || waves > 65536u ) return FD_ED25519_AMD_ERR_INVAL;
   t->window = W; t->R = R; t->waves = waves;
-  /* latency chunks' capacity: one 8-slot chunk per SIMD at ~0.45 ms, and
-     the window over their ~0.55 ms in flight.  Throughput chunks keep a frag
-     in flight 1.3-2.2 ms, so a small window caps them at W / 2 ms: when that
-     is below the latency chunks' capacity the tile stays in latency chunks
-     (batch_max 256: 8 M vs 18 M frags/s).  Rates are signature slots/s. */
-  double const cap  = std::min( (double)std::min( (ulong)waves - 1UL, 4UL * (ulong)t->cus ) * 8.0 / 450e-6,
-                                (double)W / 550e-6 );
-  /* quad chunks (16 slots, 4 lanes each): two per SIMD at ~0.9 ms, a frag
-     ~1.1 ms in flight; used between the two when they carry well above the
-     latency chunks' capacity */
-  double const qcap = std::min( (double)std::min( (ulong)waves - 1UL, 8UL * (ulong)t->cus ) * (double)QUAD_SLOTS / QUAD_SVC_S,
-                                (double)W / QUAD_FLIGHT_S );
-  bool const   quad_ok = qcap > 1.25 * cap;
-  double const below = quad_ok ? qcap : cap;   /* the capacity under throughput chunks */
-  bool const   thr_ok = (double)W / 2e-3 > below;
-  t->quad_hi = t->cfg.quad_rate_hi ? (double)t->cfg.quad_rate_hi : quad_ok ? 0.55 * cap : HUGE_VAL;
-  t->quad_lo = t->cfg.quad_rate_lo ? (double)t->cfg.quad_rate_lo : quad_ok ? 0.40 * cap : HUGE_VAL;
-  if( t->quad_lo > t->quad_hi ) t->quad_lo = t->quad_hi;
-  /* quad chunks serve up to ~90 % of their capacity at p50 ~0.8 ms (0.80 ms
-     at 30 M frags/s, against 1.28 ms in throughput chunks; 0.67 ms at 25 M),
-     so they hold until 92 % of it */
-  t->rate_hi = t->cfg.thr_rate_hi ? (double)t->cfg.thr_rate_hi : thr_ok ? (quad_ok ? 0.92 : 0.55) * below : HUGE_VAL;
-  t->rate_lo = t->cfg.thr_rate_lo ? (double)t->cfg.thr_rate_lo : thr_ok ? (quad_ok ? 0.80 : 0.40) * below : HUGE_VAL;
-  if( t->rate_lo > t->rate_hi ) t->rate_lo = t->rate_hi;
+  tile_set_levels( t );
   unsigned const hf = hipHostMallocMapped | hipHostMallocCoherent;
   /* The run's kernel occupies its hardware queue for the whole run, and HIP
      multiplexes streams onto a few hardware queues per priority
@@ -881,6 +893,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
                   ulong lat_max, uint8_t const * zc_dev, ulong zc_lim ) {
   int rc = tile_persist_alloc( t );
   if( rc ) { fprintf( stderr, "fd_verify_amd_tile_run: allocating the persistent consumer failed (%d)\n", rc ); return rc; }
+  tile_set_levels( t );   /* this run's framing */
   if( tile_kernel_busy( t ) ) {
     fprintf( stderr, "fd_verify_amd_tile_run: the kernel of an earlier run of this tile has not finished\n" );
     return FD_ED25519_AMD_ERR_DEVICE;
@@ -1181,7 +1194,10 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       }
       uchar const * p = (uchar const *)fd_chunk_to_laddr_const( in_chunk0b, chunk );
       if( !zc_dev || t->tc.depth || txn ) {
-        /* the frag 8 ahead: its bytes are read next (copy; the HA tag; TXN's signature count) */
+        /* the frag 8 ahead: its bytes are read next (copy; the HA tag; TXN's signature count).
+           Kept for the copy helper's passes too: without it the helper's copy took 11-12 ns per
+           frag instead of 2-5 and copy mode fell from 52-58 to 40-43 M frags/s
+           (profiles/r06_copy_prefetch_ab.jsonl) */
         fd_frag_meta_t const * m8 = in_mcache + ((in_seq + 8UL) & (in_depth-1UL));
         uchar const * p8 = (uchar const *)fd_chunk_to_laddr_const( in_chunk0b, __atomic_load_n( &m8->chunk, __ATOMIC_RELAXED ) );
         ulong const n8 = zc_dev ? 1UL : std::min( (ulong)__atomic_load_n( &m8->sz, __ATOMIC_RELAXED ), (ulong)FD_VERIFY_AMD_FRAME_SZ );

@@ -149,7 +149,8 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    min(min(waves, 4 x CUs) x 8 / 0.45 ms, window / 0.55 ms)); throughput
    chunks above thr_rate_hi, back below thr_rate_lo (0: 92 % / 80 % of the
    quad chunks' capacity, min(min(waves, 8 x CUs) x 16 / 0.97 ms, window /
-   1.1 ms)).  Quad chunks are skipped (quad thresholds infinite, the
+   1.1 ms), x 0.75 in TXN framing, whose whole transactions fill ~3/4 of a
+   quad chunk's slots).  Quad chunks are skipped (quad thresholds infinite, the
    throughput ones 55 % / 40 % of the latency capacity) when their capacity
    is under 1.25 x the latency chunks'; never throughput chunks when the
    window caps them below the level under them, window / 2 ms.  Whole chunks

@@ -39,7 +39,9 @@ for bmax, zc in %(sat)s:
     r = tango.bench_stream(0, bmax, 0, *pool, frags, zero_copy=zc, expect_err=err, expect_tag=tag, sample_bytes=True)
     out.append({"kind": "sat", "bmax": bmax, "zc": zc, "mfps": round(r["frags_per_s"] / 1e6, 2),
                 "steady_mfps": round(r["steady_frags_per_s"] / 1e6, 2), "mismatches": int(r["mismatches"]),
-                "chunks": [int(r["gpu_chunks_lat"]), int(r.get("gpu_chunks_quad", 0)), int(r["gpu_chunks_thr"])]})
+                "chunks": [int(r["gpu_chunks_lat"]), int(r.get("gpu_chunks_quad", 0)), int(r["gpu_chunks_thr"])],
+                "stager_ns": [round(r.get(k, 0.0), 2) for k in ("stager_list_ns", "stager_copy_ns", "stager_stage_ns",
+                                                                  "stager_hand_ns")]})
 for rate in (%(rates)s):
     r = tango.bench_stream(0, 4096, 0, *pool, int(rate * 0.4), rate=rate, zero_copy=True)
     out.append({"kind": "paced", "offered_m": rate / 1e6, "p50_us": round(r["p50_ns"] / 1e3, 1),
