@@ -28,6 +28,8 @@ from gpu_sweep import STREAMS, N, CH  # noqa: E402
 
 SUB = 1 << 20          # frags per tile run
 MODES = ((tango.CHUNK_LATENCY, "latency"), (tango.CHUNK_THROUGHPUT, "throughput"), (tango.CHUNK_QUAD, "quad"))
+# copy mode with the copy helper (cfg.copy_cpu) on the last CPU this process may use, when FD_SWEEP_TILE_HELPER=1
+HELPER = {"copy_cpu": max(os.sched_getaffinity(0))} if os.environ.get("FD_SWEEP_TILE_HELPER") else {}
 if os.environ.get("FD_SWEEP_TILE_MODES"):   # e.g. "quad" or "latency,quad"
     MODES = tuple(m for m in MODES if m[1] in os.environ["FD_SWEEP_TILE_MODES"].split(","))
 
@@ -117,7 +119,7 @@ def run(k, tiles):
                 if ZERO_COPY:   # one live tile per run: a region is registered (mapped into the GPU) by one tile
                     for t in tiles.values():
                         t.close()
-                    tiles[name] = tango.VerifyTile(0, batch_max=16384, tcache_depth=0, chunk_mode=mode)
+                    tiles[name] = tango.VerifyTile(0, batch_max=16384, tcache_depth=0, chunk_mode=mode, **HELPER)
                 log, diag = run_tile(tiles[name], region, chunk, fsz, ZERO_COPY)
                 t_tile[name] += time.time() - t3
                 got[name][c0 + s0:c0 + s1] = log
@@ -131,7 +133,7 @@ def run(k, tiles):
         hist = tuple(int((err == -c).sum()) for c in range(4))
         bad = np.nonzero(err != exp)[0]
         out.append({"seed": seed, "szlo": szlo, "szhi": szhi, "signatures": N, "path": "k_tile_persist",
-                    "staging": "zero_copy" if ZERO_COPY else "copy",
+                    "staging": "zero_copy" if ZERO_COPY else ("copy+helper" if HELPER else "copy"),
                     "chunk_mode": name, "gpu_chunks": {"latency": chunks[name][0], "throughput": chunks[name][1],
                                                              "quad": chunks[name][2]},
                     "mismatches_vs_oracle": int(bad.size), "first_mismatches": [int(i) for i in bad[:5]],
@@ -146,7 +148,7 @@ ZERO_COPY = "--zero-copy" in sys.argv
 
 if __name__ == "__main__":
     ks = [int(a) for a in sys.argv[1:] if not a.startswith("--")] or list(range(len(STREAMS)))
-    tiles = {name: tango.VerifyTile(0, batch_max=16384, tcache_depth=0, chunk_mode=mode) for mode, name in MODES}
+    tiles = {name: tango.VerifyTile(0, batch_max=16384, tcache_depth=0, chunk_mode=mode, **HELPER) for mode, name in MODES}
     fail = False
     try:
         for k in ks:
