@@ -70,9 +70,16 @@ typedef struct { uint32_t src_chunk, out_chunk, sz, slots; } fd_amd_tile_ent_t;
    count <= 64 | FD_AMD_TILE_LAT (8 lanes per signature) or FD_AMD_TILE_QUAD
    (4 lanes per signature); the entries' signature slots total <= 64 (<= 8
    in a latency chunk, <= 16 in a quad chunk) */
-typedef struct { uint64_t first; uint32_t count; uint32_t pad; } fd_amd_tile_desc_t;
+typedef struct { uint64_t first; uint32_t count; uint32_t pad; } fd_amd_tile_desc_t;   /* pad: pair sub | seq << 1 */
 #define FD_AMD_TILE_LAT  (0x80000000u)
 #define FD_AMD_TILE_QUAD (0x40000000u)
+/* a quad PAIR (PUB_SIG_MSG): two descriptors over the same 17..32 entries,
+   pad = sub | pair_seq << 1.  Sub 0 hashes and decompresses all of them
+   into pair workspace pair_seq & pair_mask, raises its flag, and verifies
+   entries 0..15; sub 1 waits for the flag and verifies entries 16.. -- one
+   front pass (all lanes busy) serves two quad chunks */
+#define FD_AMD_TILE_PAIR (0x20000000u)
+#define FD_AMD_TILE_COUNT(c) ((c) & 0x1fffffffu)
 /* result of ring index j (GPU -> host), two arrays of R words: tag[j & mask]
    and word[j & mask] = (j + 1) << 8 | (uint8_t)verdict, the word stored
    after the tag and after the frag's output bytes (system-scope release),
@@ -117,6 +124,10 @@ typedef struct {
   uint64_t                   watchdog; /* s_memrealtime ticks (100 MHz) without a host heartbeat before the kernel gives up */
   uint32_t                   prof;     /* diagnostics build only: sum per-phase time stamps into dctl->prof */
   uint32_t                   txn;      /* TXN framing: entries are wire transactions, results per transaction */
+  uint8_t *                  pair_ws;  /* quad pairs: pair_mask + 1 workspaces, fd_amd_tile_scratch_stride() apart */
+  uint32_t *                 pair_flag;/*   and their flags (pair_seq + 1 once a pair's front is done) */
+  uint32_t                   pair_mask;
+  uint32_t                   pad_;
 } fd_amd_tile_args_t;
 size_t fd_amd_tile_scratch_stride( void );
 /* waves: grid size (wave 0 is the scout that mirrors the host words) */

@@ -1897,6 +1897,8 @@ __device__ __forceinline__ u32 ld_sys32( u32 const * p ) { return __hip_atomic_l
 __device__ __forceinline__ void st_sys64( u64 * p, u64 v ) { __hip_atomic_store( p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
 __device__ __forceinline__ void st_sys32( u32 * p, u32 v ) { __hip_atomic_store( p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
 __device__ __forceinline__ u64 ld_dev64( u64 const * p ) { return __hip_atomic_load( (u64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
+__device__ __forceinline__ u32 ld_dev32( u32 const * p ) { return __hip_atomic_load( (u32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
+__device__ __forceinline__ void st_dev32( u32 * p, u32 v ) { __hip_atomic_store( p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
 __device__ __forceinline__ void st_dev64( u64 * p, u64 v ) { __hip_atomic_store( p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
 __device__ __forceinline__ u64 rfl64( u64 v ) {
   return ((u64)(u32)__builtin_amdgcn_readfirstlane( (int)(u32)(v >> 32) ) << 32) | (u32)__builtin_amdgcn_readfirstlane( (int)(u32)v );
@@ -2097,7 +2099,13 @@ tile_dsm4_call( u32 l, u32 n, i8 * __restrict__ err, u8 * __restrict__ ws, ws_la
    out, and its result is the transaction's verdict. */
 __device__ __forceinline__ void
 tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, u32 mode, u8 * __restrict__ scr, ws_layout_t L,
-            tile_scratch_t const & S, i32 (* __restrict__ bi)[48], u64 (* __restrict__ evl)[33], u64 * pt, u64 tc ) {
+            tile_scratch_t const & S, i32 (* __restrict__ bi)[48], u64 (* __restrict__ evl)[33], u64 * pt, u64 tc,
+            u32 pp = 0u ) {
+  /* pp = pair | pair_seq << 2 (quad pairs, FD_AMD_TILE_PAIR); pair: 0 none;
+     1 sub 0 -- the front of all k entries, then the pair's flag =
+     pair_seq + 1, then entries [0, 16); 2 sub 1 (the caller saw that flag)
+     -- entries [16, k) on sub 0's front */
+  u32 const pair = pp & 3u;
   /* pt (A.prof, set by the diagnostics build's host only): s_memrealtime
      ticks spent in gather [0], prep [6], decomp [1], DSM [2], results [3];
      wave-uniform */
@@ -2117,20 +2125,23 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, u32 mode, u8 * __restri
 
   /* 1. the chunk's ring entries, lane q holds entry q (host memory: system-scope loads) */
   bool const txn = A.txn != 0u;
+  /* a pair's sub 1 runs the front on no entries (its barriers only: a
+     branch round the front costs the loop a VGPR spill) */
+  u32 const kf = pair == 2u ? 0u : k;
   u32 e_src = 0u, e_out = 0u, e_sz = 96u, e_k = 0u;
-  if( l < k ) {
+  if( l < kf ) {
     u64 const * ep = (u64 const *)(A.ent + ((c0 + l) & A.mask));
     u64 w0 = ld_sys64( ep ), w1 = ld_sys64( ep + 1 );
     e_src = (u32)w0; e_out = (u32)(w0 >> 32); e_sz = (u32)w1; e_k = (u32)(w1 >> 32);
   }
   /* 2. copy the frags in (tile_gather) */
-  tile_gather( A, k, l, e_src, e_out, e_sz, mir, pub, sig, txn );
-  if( l < k && !txn ) { off[l] = l * TILE_FRAME + 96u; sz[l] = e_sz - 96u; }
+  tile_gather( A, kf, l, e_src, e_out, e_sz, mir, pub, sig, txn );
+  if( l < kf && !txn ) { off[l] = l * TILE_FRAME + 96u; sz[l] = e_sz - 96u; }
   __syncthreads();
   /* TXN: parse and lay the chunk's signature slots out (n of them) */
   i8 * skp = (i8 *)(scr + S.skp);
   u32 * tx = (u32 *)(scr + S.tx);
-  u32 const n = txn ? tile_txn_layout( l, k, e_sz, e_k, mir, pub, sig, off, sz, skp, tx, (u32 *)&evl[0][0] ) : k;
+  u32 const n = txn ? tile_txn_layout( l, k, e_sz, e_k, mir, pub, sig, off, sz, skp, tx, (u32 *)&evl[0][0] ) : kf;
   if( txn ) __syncthreads();
   TILE_STAMP( 0 );
   /* 3. the verify pipeline on the chunk (k_prep, k_decomp, k_dsm / k_dsm8 / k_dsm4 bodies) */
@@ -2141,6 +2152,16 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, u32 mode, u8 * __restri
   if( n > 32u ) decomp_body( l + 64u, n, pub, sig, err, ws, L, true );
   __syncthreads();
   TILE_STAMP( 1 );
+  if( pair == 1u ) {
+    /* the pair's front is done: every lane's workspace writes out of this
+       XCD's L2 (agent-scope release), then the flag sub 1 waits on */
+    __builtin_amdgcn_fence( __ATOMIC_RELEASE, "agent" );
+    __syncthreads();
+    if( l == 0u ) st_dev32( A.pair_flag + ((pp >> 2) & A.pair_mask), (pp >> 2) + 1u );
+  }
+  /* this wave's signatures: all k, or a pair sub's 16 */
+  u32 const g0 = pair == 2u ? 64u : 0u;                 /* k_dsm4's lane index: signature (g0 + l) >> 2 */
+  u32 const nd = pair == 1u ? min( k, 16u ) : pair == 2u ? k : n;
 #if defined(FD_AMD_TILE_QUAD_LAST)   /* A/B: code placement of the three bodies */
   if( mode == TILE_MODE_THR )        dsm_lane_body( l, n, err, ws, L, 0, bi, evl, tc );
   else if( mode == TILE_MODE_LAT8 )  dsm8_body( l, n, err, ws, L, 0, bi, evl, tc );
@@ -2152,7 +2173,7 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, u32 mode, u8 * __restri
 #else
   if( mode == TILE_MODE_LAT8 )       dsm8_body( l, n, err, ws, L, 0, bi, evl, tc );
 #ifndef FD_AMD_TILE_NO_QUAD   /* A/B only: the tile kernel without the quad body (quad chunks run 1 lane each) */
-  else if( mode == TILE_MODE_QUAD4 ) dsm4_body( l, n, err, ws, L, 0, bi, evl, tc );
+  else if( mode == TILE_MODE_QUAD4 ) dsm4_body( g0 + l, nd, err, ws, L, 0, bi, evl, tc );
 #endif
   else                               dsm_lane_body( l, n, err, ws, L, 0, bi, evl, tc );
 #endif
@@ -2164,10 +2185,12 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, u32 mode, u8 * __restri
         verdict is its parse failure, else the first failing signature's
         code in signature order, else 0 (k_txn_reduce); its tag is its first
         signature's */
-  u64 const idx = c0 + l, j = idx & A.mask;
+  u32 const e0 = pair == 2u ? 16u : 0u, e1 = pair == 1u ? min( k, 16u ) : k;   /* this wave's entries */
+  u32 const q = e0 + l;
+  u64 const idx = c0 + q, j = idx & A.mask;
   u64 tag = 0UL; i8 v = 0;
-  if( l < k ) {
-    if( !txn ) { tag = ((u64 const *)(ws + L.tag))[l]; v = err[l]; }
+  if( q < e1 ) {
+    if( !txn ) { tag = ((u64 const *)(ws + L.tag))[q]; v = err[q]; }
     else {
       u32 const w = tx[l], b = w & 0xffu, kk = (w >> 8) & 0xffu;
       if( !(w >> 31) ) v = (i8)TXN_ERR_PARSE;
@@ -2176,11 +2199,11 @@ tile_chunk( fd_amd_tile_args_t const & A, u64 c0, u32 k, u32 mode, u8 * __restri
     }
     st_sys64( A.res_tag + j, tag );
   }
-  if( A.res_time && l < k ) st_sys64( A.res_time + j, (u64)(u32)tc | ((u64)(u32)__builtin_amdgcn_s_memrealtime() << 32) );
+  if( A.res_time && q < e1 ) st_sys64( A.res_time + j, (u64)(u32)tc | ((u64)(u32)__builtin_amdgcn_s_memrealtime() << 32) );
   __builtin_amdgcn_fence( __ATOMIC_RELEASE, "" );
   asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
   u64 const wd = ((idx + 1UL) << 8) | (u64)(u8)v;
-  if( l < k ) st_sys64( A.res_word + j, wd );
+  if( q < e1 ) st_sys64( A.res_word + j, wd );
   TILE_STAMP( 3 );
 # undef TILE_STAMP
 }
@@ -2260,20 +2283,38 @@ k_tile_persist( fd_amd_tile_args_t A ) {
       c = ld_sys64( dp ); cm = ld_sys64( dp + 1 );
     }
     c = rfl64( c ); cm = rfl64( cm );
-    u32 const take = (u32)cm & 0x3fffffffu;
+    u32 const take = FD_AMD_TILE_COUNT( (u32)cm );
     u32 const md = ((u32)cm & FD_AMD_TILE_LAT) ? TILE_MODE_LAT8 : ((u32)cm & FD_AMD_TILE_QUAD) ? TILE_MODE_QUAD4 : TILE_MODE_THR;
+    /* quad pair: its shared workspace and flag; sub 1 first waits for sub 0's front */
+    u32 const pr = ((u32)cm & FD_AMD_TILE_PAIR) && A.pair_ws && !A.txn && md == TILE_MODE_QUAD4 ? 1u + (u32)((cm >> 32) & 1UL) : 0u;
+    u32 const pseq = (u32)(cm >> 33) & 0x3fffffffu;
+    u8 * cscr = pr ? A.pair_ws + (size_t)(pseq & A.pair_mask) * S.total : scr;
+    u32 * pf = pr ? A.pair_flag + (pseq & A.pair_mask) : (u32 *)0;
+    bool pok = true;
+    if( pr == 2u ) {
+      u64 const tp = __builtin_amdgcn_s_memrealtime();
+      for( ;; ) {
+        u32 const f = (u32)__builtin_amdgcn_readfirstlane( (int)(l == 0u ? ld_dev32( pf ) : 0u) );
+        if( f == pseq + 1u ) break;
+        u64 const w = rfl64( l == 0u ? ld_dev64( mw ) : 0UL );
+        if( (w & TILE_MW_ERR) || __builtin_amdgcn_s_memrealtime() - tp > A.watchdog ) { pok = false; break; }
+        __builtin_amdgcn_s_sleep( 2 );
+      }
+      __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "agent" );   /* sub 0's workspace writes (another XCD's L2) */
+    }
     /* the frames were written by the host (copy mode) or the producer
        (zero-copy) into host memory: drop this CU's stale lines first */
     u64 const tf = prof ? __builtin_amdgcn_s_memrealtime() : 0UL;
     __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "" );
     asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
     if( prof && !l ) pt[5] += __builtin_amdgcn_s_memrealtime() - tf;
-    if( take && take <= 64u ) tile_chunk( A, c, take, md, scr, L, S, bi, evl, pt, tc );
+    if( take && take <= 64u && pok && (!pr || (take > 16u && take <= 32u)) )
+      tile_chunk( A, c, take, md, cscr, L, S, bi, evl, pt, tc, pr | pseq << 2 );
     if( !l ) {
-      /* dctl->stat slots: chunks, frags -- latency 0, 2; throughput 1, 3; quad 4, 5 */
+      /* dctl->stat slots: chunks, frags -- latency 0, 2; throughput 1, 3; quad 4, 5 (a pair sub is a quad chunk) */
       u32 const tc_ = md == TILE_MODE_LAT8 ? 0u : md == TILE_MODE_THR ? 1u : 4u;
       u32 const tf_ = md == TILE_MODE_LAT8 ? 2u : md == TILE_MODE_THR ? 3u : 5u;
-      s_tally[8u + tc_] += 1UL; s_tally[8u + tf_] += take;
+      s_tally[8u + tc_] += 1UL; s_tally[8u + tf_] += pr == 1u ? 16u : pr == 2u ? take - 16u : take;
       atomicAdd( (unsigned long long *)&D->done, 1ULL );   /* progress, mirrored to the host by the scout */
     }
   }

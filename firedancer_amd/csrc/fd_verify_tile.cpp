@@ -350,6 +350,15 @@ struct fd_verify_amd_tile {
   fd_amd_tile_dctl_t * dctl;
   fd_amd_tile_dctl_t   d0;          /* its seed (host copy, alive while the copy is queued) */
   uint8_t *            scratch;
+  /* quad pairs (FD_AMD_TILE_PAIR): pair_cnt shared workspaces + flags, the
+     next pair's sequence number, and per workspace the ring index after the
+     frags of the pair that last used it (free once published) */
+  uint8_t *            pair_ws;
+  uint32_t *           pair_flag;
+  ulong                pair_cnt, pair_seq;
+  std::vector<ulong>   pair_end;
+  std::vector<uint32_t> pair_zero;  /* the flags' seed (alive while its copy is queued) */
+  ulong                n_pair;     /* the last run's pairs */
   ulong                R;          /* ring size (power of 2) */
   ulong                window;     /* frags in flight at most (handed to the GPU, not yet published) */
   uint32_t             waves;      /* grid of a run (the share), fixed at the first run */
@@ -512,8 +521,10 @@ tile_persist_free( fd_verify_amd_tile_t * t ) {
   if( t->res )     (void)hipHostFree( t->res );
   if( t->dctl )    (void)hipFree( t->dctl );
   if( t->scratch ) (void)hipFree( t->scratch );
+  if( t->pair_ws ) (void)hipFree( t->pair_ws );
+  if( t->pair_flag ) (void)hipFree( t->pair_flag );
   t->pst = NULL; t->pdone = NULL; t->hctl = NULL; t->ring = NULL; t->desc = NULL; t->res = NULL;
-  t->dctl = NULL; t->scratch = NULL;
+  t->dctl = NULL; t->scratch = NULL; t->pair_ws = NULL; t->pair_flag = NULL; t->pair_cnt = 0UL;
   t->persist_ok = false;
 }
 
@@ -612,6 +623,29 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
   memset( t->ring, 0, R * sizeof(fd_amd_tile_ent_t) );
   memset( t->desc, 0, R * sizeof(fd_amd_tile_desc_t) );
   memset( t->res,  0, 3UL * R * sizeof(uint64_t) );   /* word 0 never matches an index + 1 */
+  /* quad pairs: as many workspaces as half the waves could run at once
+     (each pair is two quad chunks); optional -- without them quad chunks
+     run unpaired.  FD_AMD_TILE_PAIRS=0 turns them off (A/B). */
+  {
+    char const * e = getenv( "FD_AMD_TILE_PAIRS" );
+    ulong pc = 64UL; while( pc < (ulong)waves / 2UL ) pc <<= 1;
+    if( !(e && *e == '0') &&
+        hipMalloc( (void **)&t->pair_ws, pc * fd_amd_tile_scratch_stride() ) == hipSuccess &&
+        hipMalloc( (void **)&t->pair_flag, pc * sizeof(uint32_t) ) == hipSuccess &&
+        /* zeroed by a copy queued ahead of the first kernel on the tile's
+           stream (no device-wide sync: another tile's kernel may be running) */
+        ( t->pair_zero.assign( pc, 0u ),
+          hipMemcpyAsync( t->pair_flag, t->pair_zero.data(), pc * sizeof(uint32_t), hipMemcpyHostToDevice, t->pst ) == hipSuccess ) ) {
+      t->pair_cnt = pc;
+    } else {
+      (void)hipGetLastError();
+      if( t->pair_ws ) (void)hipFree( t->pair_ws );
+      if( t->pair_flag ) (void)hipFree( t->pair_flag );
+      t->pair_ws = NULL; t->pair_flag = NULL; t->pair_cnt = 0UL;
+    }
+    t->pair_seq = 0UL;
+    t->pair_end.assign( t->pair_cnt, 0UL );
+  }
   t->desc_seq = 0UL;
   t->ppend.assign( R, pending_t{} );
   t->desc_end.assign( R, 0UL );
@@ -932,6 +966,8 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   A.scratch = t->scratch;
   A.watchdog = 500000000UL;   /* 5 s of s_memrealtime (100 MHz) without a heartbeat */
   A.txn = txn ? 1u : 0u;
+  A.pair_ws = t->pair_ws; A.pair_flag = t->pair_flag; A.pair_mask = t->pair_cnt ? (uint32_t)(t->pair_cnt - 1UL) : 0u;
+  t->n_pair = 0UL;
 #ifdef FD_AMD_DIAG
   { char const * e = getenv( "FD_AMD_TILE_PROF" ); A.prof = e && *e && *e != '0'; }   /* diagnostics build only */
 #endif
@@ -1310,7 +1346,12 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
          into part-filled chunks (47 frags per 64-lane chunk at 16384 zero
          copy, profiles/r05_tile_cut_full_ab.txt) */
       bool const flush = done_in || (full && handed == pubd);
-      ulong const upto_sl = fd_verify_amd_tile_cut( &cc, staged_sl, handed_sl, t->desc_seq - cdone, thr, waited, flush );
+      ulong upto_sl = fd_verify_amd_tile_cut( &cc, staged_sl, handed_sl, t->desc_seq - cdone, thr, waited, flush );
+      /* quad pairs: the cut's whole quad chunks go as whole pairs (32 frags;
+         the 16 held back wait at most ~16 frags' arrival, or the cut's
+         lat_fill_ns, then go with the rest) */
+      if( thr == FD_VERIFY_AMD_LVL_QUAD && !txn && t->pair_cnt && upto_sl != staged_sl )
+        upto_sl = handed_sl + ((upto_sl - handed_sl) & ~(2UL * QUAD_SLOTS - 1UL));
       /* whole entries up to that slot count (PUB_SIG_MSG: one slot per entry) */
       ulong upto = handed;
       if( upto_sl == staged_sl ) upto = staged;
@@ -1338,7 +1379,27 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
              many signatures) runs 1 lane per signature */
           bool const lat_chunk  = thr == FD_VERIFY_AMD_LVL_LAT  && nsl <= LAT_SLOTS;
           bool const quad_chunk = thr == FD_VERIFY_AMD_LVL_QUAD && nsl <= QUAD_SLOTS;
+          /* quad pair: 17..32 frags as two quad chunks on one front pass
+             (sub 0 hashes and decompresses all of them) when a pair
+             workspace is free (its last pair's frags all published) */
+          if( quad_chunk && !txn && t->pair_cnt && avail > QUAD_SLOTS &&
+              t->pair_end[t->pair_seq & (t->pair_cnt - 1UL)] <= pubd ) {
+            ulong const pn = std::min( avail, 2UL * QUAD_SLOTS ), sq = t->pair_seq++;
+            t->pair_end[sq & (t->pair_cnt - 1UL)] = c + pn;
+            for( uint32_t sub = 0u; sub < 2u; sub++ ) {
+              fd_amd_tile_desc_t * pd = t->desc + (ds & mask);
+              pd->first = c;
+              pd->count = (uint32_t)pn | FD_AMD_TILE_QUAD | FD_AMD_TILE_PAIR;
+              pd->pad   = sub | (uint32_t)((sq & 0x3fffffffUL) << 1);   /* the kernel's flag value: seq + 1 (30 bits) */
+              t->desc_end[ds & mask] = c + pn;
+              ds++;
+            }
+            for( ulong q = 0; q < pn; q++ ) t->ppend[(c + q) & mask].t_hand = th | 1u;
+            c += pn; t->n_pair++;
+            continue;
+          }
           fd_amd_tile_desc_t * dd = t->desc + (ds & mask);
+          dd->pad = 0u;
           dd->first = c;
           dd->count = (uint32_t)cnt | (lat_chunk ? FD_AMD_TILE_LAT : 0u) | (quad_chunk ? FD_AMD_TILE_QUAD : 0u);
           t->desc_end[ds & mask] = c + cnt;
@@ -1432,6 +1493,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   diag->gpu_chunk_lat_cnt += st[0]; diag->gpu_chunk_thr_cnt += st[1];
   diag->gpu_frag_lat_cnt  += st[2]; diag->gpu_frag_thr_cnt  += st[3];
   diag->gpu_chunk_quad_cnt += st[4]; diag->gpu_frag_quad_cnt += st[5];
+  diag->quad_pair_cnt += t->n_pair;
   diag->ovrn_cnt += ovrn + r.d.ovrn_cnt; diag->bad_frag_cnt += bad;
   diag->ha_filt_cnt += ha; diag->ha_filt_sz += ha_sz;
   diag->sv_filt_cnt += r.d.sv_filt_cnt; diag->sv_filt_sz += r.d.sv_filt_sz;
@@ -1818,10 +1880,10 @@ fd_verify_amd_bench_stream( int device, ulong batch_max, ulong batch_wait_ns, do
   free( dcache );
   if( rc ) return rc;
   ulong n = std::min( (ulong)diag.out_cnt, frag_cnt );
-  for( int k=0; k<48; k++ ) out[k] = 0.0;
+  for( int k=0; k<49; k++ ) out[k] = 0.0;
   for( int k=0; k<4; k++ ) out[44 + k] = ph_ns[k];
   out[41] = (double)n_steal;
-  out[42] = (double)diag.gpu_chunk_quad_cnt; out[43] = (double)diag.gpu_frag_quad_cnt;
+  out[42] = (double)diag.gpu_chunk_quad_cnt; out[43] = (double)diag.gpu_frag_quad_cnt; out[48] = (double)diag.quad_pair_cnt;
   if( t90 > t10 && t10 && s90 > s10 ) out[40] = (double)(s90 - s10) / ((double)(t90 - t10) * 1e-9);
   /* decomposition (before lat is sorted: the samples are per published frag) */
   /* paced runs: percentiles over the steady state (n_st samples); the

@@ -18,7 +18,8 @@ CHUNK_SZ = 64
 DIAG_FIELDS = ("in_cnt", "ha_filt_cnt", "ha_filt_sz", "sv_filt_cnt", "sv_filt_sz", "out_cnt", "out_sz",
                "ovrn_cnt", "backp_cnt", "batch_cnt", "batch_sig_cnt", "bad_frag_cnt", "gpu_chunk_lat_cnt",
                "gpu_chunk_thr_cnt", "gpu_frag_lat_cnt", "gpu_frag_thr_cnt", "sv_filt_sig_cnt", "sv_filt_pubkey_cnt",
-               "sv_filt_msg_cnt", "halt_drop_cnt", "mode_switch_cnt", "gpu_chunk_quad_cnt", "gpu_frag_quad_cnt")
+               "sv_filt_msg_cnt", "halt_drop_cnt", "mode_switch_cnt", "gpu_chunk_quad_cnt", "gpu_frag_quad_cnt",
+               "quad_pair_cnt")
 CHUNK_AUTO, CHUNK_LATENCY, CHUNK_THROUGHPUT, CHUNK_QUAD = 0, 1, 2, 3
 LVL_LAT, LVL_THR, LVL_QUAD = 0, 1, 2
 PUBLISH_AUTO, PUBLISH_INLINE = -2, -1
@@ -176,7 +177,7 @@ def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, bl
     """fd_verify_amd_bench_stream: producer (rate frags/s, 0 = saturate) -> tile -> consumer; returns
     dict(frags_per_s, p50_ns, p99_ns, p999_ns, mean_batch, published, sv_filt, ovrn, mismatches, checked).
     With expect_err/expect_tag (per pool entry) the consumer checks every published frag."""
-    out = (ctypes.c_double * 48)()
+    out = (ctypes.c_double * 49)()
     p = [np.ascontiguousarray(a) for a in (pub, sig, msg_off, msg_sz, blob)]
     ee = np.ascontiguousarray(expect_err, np.int8) if expect_err is not None else None
     et = np.ascontiguousarray(expect_tag, np.uint64) if expect_tag is not None else None
@@ -200,5 +201,5 @@ def bench_stream(device, batch_max, batch_wait_ns, pub, sig, msg_off, msg_sz, bl
             "service_lat_chunk_p50_ns", "service_thr_chunk_p50_ns", "mode_switches", "traced", "producer_credit_wait_max_ns", "passes",
             "hand_offs", "stop_window", "stop_frames", "stop_batch_max", "stop_pass_bound", "all_p50_ns", "all_p99_ns", "steady_frags_per_s", "copy_steals",
             "gpu_chunks_quad", "gpu_frags_quad", "stager_list_ns", "stager_copy_ns", "stager_stage_ns",
-            "stager_hand_ns")
+            "stager_hand_ns", "quad_pairs")
     return dict(zip(keys, list(out)))

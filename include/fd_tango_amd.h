@@ -111,6 +111,8 @@ typedef struct {
   ulong mode_switch_cnt;     /* switches between chunk levels (latency / quad / throughput) */
   ulong gpu_chunk_quad_cnt;  /* chunks the GPU verified 4 lanes per signature (quad chunks) */
   ulong gpu_frag_quad_cnt;   /* frags in those chunks */
+  ulong quad_pair_cnt;       /* quad chunk pairs handed over: two quad chunks over 17..32 frags sharing one front
+                                pass (hash + decompression); each counts as two quad chunks above */
 } fd_verify_amd_diag_t;
 
 typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
@@ -448,8 +450,8 @@ fd_verify_amd_tile_pack( uint const * slots, ulong cnt, int thr, ulong * nsl );
    out[43] = the GPU's quad chunks and the frags in them; out[44..47] =
    the tile thread's time per staged frag (ns, over its passes that staged
    something): listing the pass's frags, copying them (copy mode),
-   re-checking and staging them, handing chunks over.  out holds 48
-   doubles.
+   re-checking and staging them, handing chunks over; out[48] = the quad
+   chunk pairs handed over (diag quad_pair_cnt).  out holds 49 doubles.
    Threads: producer, tile, the tile's publisher and consumer each pinned
    to a CPU of their own when the process may use 5 or more (else unpinned,
    publisher inline); copy mode adds the tile's copy helper on a fifth CPU

@@ -409,6 +409,7 @@ def test_tile_txn_mixed_vs_oracle_per_chunk_mode(chunk_mode):
     if chunk_mode == 3:
         assert diag["gpu_chunk_quad_cnt"] > 0 and diag["gpu_chunk_lat_cnt"] == 0
         assert diag["gpu_frag_quad_cnt"] <= 16 * diag["gpu_chunk_quad_cnt"]
+        assert diag["quad_pair_cnt"] == 0          # pairs are PUB_SIG_MSG only
 
 
 def test_tile_txn_many_signers_at_the_head_go_at_once():
@@ -601,6 +602,34 @@ def test_tile_golden_codes_per_chunk_mode(golden, chunk_mode, zero_copy):
     key = {1: "gpu_frag_lat_cnt", 2: "gpu_frag_thr_cnt", 3: "gpu_frag_quad_cnt"}[chunk_mode]
     assert diag[key] == n
     assert all(int(mc_out[o]["seq"]) == o for o in range(diag["out_cnt"]))
+    if chunk_mode == 3:
+        # the whole set is staged at once: quad chunks go as pairs (17..32 frags, one front pass)
+        assert diag["quad_pair_cnt"] > 0 and 2 * diag["quad_pair_cnt"] <= diag["gpu_chunk_quad_cnt"]
+
+
+@pytest.mark.parametrize("pairs", ["0", "1"])
+def test_tile_quad_pairs_vs_oracle(monkeypatch, pairs):
+    """Quad chunks with and without pairs (FD_AMD_TILE_PAIRS=0: no pair
+    workspaces, every quad chunk runs its own front).  A pair's sub 1 waits
+    for sub 0's front on another wave (often another XCD) and verifies
+    entries 16..31 from sub 0's workspace: a stream of fresh signatures with
+    10 % corrupted frags at a ragged length (pairs of 17..32, a lone quad
+    chunk at the tail) publishes exactly the oracle's accepted set, in order,
+    with the right tags, either way."""
+    from firedancer_amd import tango
+    monkeypatch.setenv("FD_AMD_TILE_PAIRS", pairs)
+    pub, sig, off, sz, blob, err, tag = _stream_pool(9100 + int(pairs), 4096, 400)
+    nf = 3 * 4096 + 17 * 29 + 5
+    r = tango.bench_stream(0, 4096, 0, pub, sig, off, sz, blob, nf, zero_copy=pairs == "1", expect_err=err,
+                           expect_tag=tag, chunk_mode=3)
+    want = int((err[np.arange(nf) % err.size] == 0).sum())
+    assert r["mismatches"] == 0 and r["ovrn"] == 0
+    assert r["checked"] == r["published"] == want and r["sv_filt"] == nf - want
+    assert r["gpu_frags_quad"] == nf and r["gpu_frags_quad"] <= 16 * r["gpu_chunks_quad"]
+    if pairs == "1":
+        assert r["quad_pairs"] > 0 and 2 * r["quad_pairs"] <= r["gpu_chunks_quad"]
+    else:
+        assert r["quad_pairs"] == 0
 
 
 def _signed_feed(seed, count, depth):

@@ -5,12 +5,12 @@ latency at fixed offered rates -- the numbers the tile's quad thresholds
 run.
 
 usage: python tools/quad_probe.py [sat|paced|all] > gpurun_out/quad_probe.jsonl
-env FD_AMD_BENCH_LEVELS="quad_hi,quad_lo,thr_hi,thr_lo" overrides the level thresholds (slots/s).
+env FD_AMD_BENCH_LEVELS="quad_hi,quad_lo,thr_hi,thr_lo" overrides the level thresholds (slots/s);
+QP_PAIRS="0,1" runs every line with quad pairs off and on (FD_AMD_TILE_PAIRS, read per tile).
 """
 import json
 import os
 import sys
-import time
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import numpy as np  # noqa: E402
@@ -40,22 +40,32 @@ def keep(r):
             "service_p50_us_thr": r["service_thr_chunk_p50_ns"] / 1e3, "queue_p50_us": r["queue_p50_ns"] / 1e3,
             "chunks": [int(r["gpu_chunks_lat"]), int(r["gpu_chunks_quad"]), int(r["gpu_chunks_thr"])],
             "switches": int(r["mode_switches"]), "mismatches": int(r["mismatches"]),
-            "stager_ns": [round(r[k], 1) for k in ("stager_list_ns", "stager_copy_ns", "stager_stage_ns", "stager_hand_ns")]}
+            "stager_ns": [round(r[k], 1) for k in ("stager_list_ns", "stager_copy_ns", "stager_stage_ns", "stager_hand_ns")],
+            "quad_pairs": int(r.get("quad_pairs", 0)), "pairs_env": os.environ.get("FD_AMD_TILE_PAIRS", "1")}
+
+
+pair_set = os.environ.get("QP_PAIRS", "1").split(",")
+
+
+def bench_stream(*a, **kw):
+    """tango.bench_stream once per QP_PAIRS setting; yields the results."""
+    for ps in pair_set:
+        os.environ["FD_AMD_TILE_PAIRS"] = ps
+        yield tango.bench_stream(*a, **kw)
 
 
 if what in ("sat", "all"):
     for bmax in (1024, 4096):
         for mode in (1, 3, 2):
-            t0 = time.time()
-            r = tango.bench_stream(0, bmax, 0, *pool, 1 << 22, zero_copy=True, chunk_mode=mode)
-            line(kind="saturated", bmax=bmax, mode=names[mode], s=time.time() - t0, **keep(r))
+            for r in bench_stream(0, bmax, 0, *pool, 1 << 22, zero_copy=True, chunk_mode=mode):
+                line(kind="saturated", bmax=bmax, mode=names[mode], **keep(r))
     for zc in (False, True):   # AUTO, both stagings: the stager's time per frag by phase
-        r = tango.bench_stream(0, 4096, 0, *pool, 1 << 22, zero_copy=zc)
-        line(kind="saturated", bmax=4096, mode="auto", staging="zero_copy" if zc else "copy", **keep(r))
+        for r in bench_stream(0, 4096, 0, *pool, 1 << 22, zero_copy=zc):
+            line(kind="saturated", bmax=4096, mode="auto", staging="zero_copy" if zc else "copy", **keep(r))
 if what in ("paced", "all"):
     for bmax in (4096,):
         for rate in rates:
             for mode in (0, 3):
                 nf = int(max(50000, rate * 0.3))
-                r = tango.bench_stream(0, bmax, 0, *pool, nf, rate=rate, zero_copy=True, chunk_mode=mode)
-                line(kind="paced", bmax=bmax, mode=names[mode], offered=rate, **keep(r))
+                for r in bench_stream(0, bmax, 0, *pool, nf, rate=rate, zero_copy=True, chunk_mode=mode):
+                    line(kind="paced", bmax=bmax, mode=names[mode], offered=rate, **keep(r))
