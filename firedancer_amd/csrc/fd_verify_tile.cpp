@@ -624,12 +624,15 @@ tile_persist_alloc( fd_verify_amd_tile_t * t ) {
   memset( t->desc, 0, R * sizeof(fd_amd_tile_desc_t) );
   memset( t->res,  0, 3UL * R * sizeof(uint64_t) );   /* word 0 never matches an index + 1 */
   /* quad pairs: as many workspaces as half the waves could run at once
-     (each pair is two quad chunks); optional -- without them quad chunks
-     run unpaired.  FD_AMD_TILE_PAIRS=0 turns them off (A/B). */
+     (each pair is two quad chunks).  Opt-in (FD_AMD_TILE_PAIRS=1): sub 1's
+     wave sleeps through sub 0's front, so a pair frees SIMD issue slots but
+     not wave slots, and measured it moved quad capacity by < 2 % and p50 at
+     30 M frags/s by -6 %, p99 at 20 M auto +60 % through extra level
+     switches (profiles/r06_quad_pairs_ab.txt) -- not worth its default. */
   {
     char const * e = getenv( "FD_AMD_TILE_PAIRS" );
     ulong pc = 64UL; while( pc < (ulong)waves / 2UL ) pc <<= 1;
-    if( !(e && *e == '0') &&
+    if( e && *e == '1' &&
         hipMalloc( (void **)&t->pair_ws, pc * fd_amd_tile_scratch_stride() ) == hipSuccess &&
         hipMalloc( (void **)&t->pair_flag, pc * sizeof(uint32_t) ) == hipSuccess &&
         /* zeroed by a copy queued ahead of the first kernel on the tile's

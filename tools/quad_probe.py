@@ -41,10 +41,10 @@ def keep(r):
             "chunks": [int(r["gpu_chunks_lat"]), int(r["gpu_chunks_quad"]), int(r["gpu_chunks_thr"])],
             "switches": int(r["mode_switches"]), "mismatches": int(r["mismatches"]),
             "stager_ns": [round(r[k], 1) for k in ("stager_list_ns", "stager_copy_ns", "stager_stage_ns", "stager_hand_ns")],
-            "quad_pairs": int(r.get("quad_pairs", 0)), "pairs_env": os.environ.get("FD_AMD_TILE_PAIRS", "1")}
+            "quad_pairs": int(r.get("quad_pairs", 0)), "pairs_env": os.environ.get("FD_AMD_TILE_PAIRS", "0")}
 
 
-pair_set = os.environ.get("QP_PAIRS", "1").split(",")
+pair_set = os.environ.get("QP_PAIRS", os.environ.get("FD_AMD_TILE_PAIRS", "0")).split(",")
 
 
 def bench_stream(*a, **kw):
