@@ -195,6 +195,11 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
 #define FD_VERIFY_AMD_CHUNK_LATENCY    (1)   /* every chunk a latency chunk */
 #define FD_VERIFY_AMD_CHUNK_THROUGHPUT (2)   /* every chunk a throughput chunk */
 #define FD_VERIFY_AMD_CHUNK_QUAD       (3)   /* every chunk a quad chunk */
+/* Quad pairs (environment FD_AMD_TILE_PAIRS=1 when the tile first runs; off
+   by default): PUB_SIG_MSG quad chunks are handed over as pairs of two over
+   17..32 frags that share one front pass (hash, decompression) on the first
+   chunk's wave; the second waits for it.  Exact either way; measured to
+   move capacity < 2 %, so opt-in.  diag quad_pair_cnt. */
 /* chunk levels (fd_verify_amd_tile_level, the thr argument of _cut / _pack) */
 #define FD_VERIFY_AMD_LVL_LAT  (0)           /* 8 slots, 8 lanes per signature */
 #define FD_VERIFY_AMD_LVL_THR  (1)           /* 64 slots, 1 lane per signature */

@@ -91,7 +91,7 @@ def run(k, tiles):
     off64[1:] = np.cumsum(sz[:-1], dtype=np.int64)      # the generator's u32 offsets wrap past 4 GB
     exp = np.zeros(N, np.int8)
     got = {name: np.zeros(N, np.int8) for _, name in MODES}
-    chunks = {name: [0, 0, 0] for _, name in MODES}
+    chunks = {name: [0, 0, 0, 0] for _, name in MODES}
     t_tile = {name: 0.0 for _, name in MODES}
     t_cpu = 0.0
     for c0 in range(0, N, CH):
@@ -126,6 +126,7 @@ def run(k, tiles):
                 chunks[name][0] += diag["gpu_chunk_lat_cnt"]
                 chunks[name][1] += diag["gpu_chunk_thr_cnt"]
                 chunks[name][2] += diag["gpu_chunk_quad_cnt"]
+                chunks[name][3] += diag.get("quad_pair_cnt", 0)
         print("  stream %d: %d/%d" % (seed, c1, N), file=sys.stderr, flush=True)
     out = []
     for _, name in MODES:
@@ -135,7 +136,7 @@ def run(k, tiles):
         out.append({"seed": seed, "szlo": szlo, "szhi": szhi, "signatures": N, "path": "k_tile_persist",
                     "staging": "zero_copy" if ZERO_COPY else ("copy+helper" if HELPER else "copy"),
                     "chunk_mode": name, "gpu_chunks": {"latency": chunks[name][0], "throughput": chunks[name][1],
-                                                             "quad": chunks[name][2]},
+                                                             "quad": chunks[name][2], "quad_pairs": chunks[name][3]},
                     "mismatches_vs_oracle": int(bad.size), "first_mismatches": [int(i) for i in bad[:5]],
                     "hist": hist, "hist_equals_reference": hist == ref_hist,
                     "false_rejects": int(((fk == 0) & (err == -3)).sum()),
