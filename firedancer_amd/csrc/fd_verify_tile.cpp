@@ -1067,6 +1067,20 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   uchar const * in_chunk0b = (uchar const *)in_chunk0;
   fd_verify_amd_tile_cfg_t cc = t->cfg;   /* the cut rule's parameters */
   std::vector<uint> pk_slots( 64 );
+  /* listing prefetch distances (frags ahead): mcache lines, and the frag
+     bytes the copy / HA tag / TXN count read next.  32 / 24 (were 16 / 8):
+     copy mode +8-15 % interleaved over seven rounds in two GPU calls, zero copy
+     unchanged within noise (profiles/r06_listing_prefetch_ab_a/b.jsonl).
+     FD_AMD_TILE_PF="mc,data" overrides them (A/B only) */
+  ulong pf_mc = 32UL, pf_dt = 24UL;
+  {
+    char const * e = getenv( "FD_AMD_TILE_PF" );
+    if( e && *e ) {
+      char * q = NULL; ulong a = strtoul( e, &q, 0 ), b = (q && *q == ',') ? strtoul( q + 1, NULL, 0 ) : pf_dt;
+      if( a >= 1UL && a <= 256UL ) pf_mc = a;
+      if( b >= 1UL && b <= 256UL ) pf_dt = b;
+    }
+  }
 
   /* reserve the next output frame (cyclic): free -- not staged, in flight
      or orphaned -- and no longer read by a consumer that honours flow
@@ -1219,7 +1233,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       if( frag_cnt && in_seq - in_seq0 >= frag_cnt ) break;
       if( staged + pnj + nj - pubd >= W ) { full = true; n_stop_window++; break; }
       fd_frag_meta_t const * m = in_mcache + (in_seq & (in_depth-1UL));
-      __builtin_prefetch( in_mcache + ((in_seq + 16UL) & (in_depth-1UL)) );
+      __builtin_prefetch( in_mcache + ((in_seq + pf_mc) & (in_depth-1UL)) );
       ulong seq_found = __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE );
       long  d = (long)(seq_found - in_seq);
       if( d < 0 ) break;                                                  /* not yet published */
@@ -1233,11 +1247,11 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       }
       uchar const * p = (uchar const *)fd_chunk_to_laddr_const( in_chunk0b, chunk );
       if( !zc_dev || t->tc.depth || txn ) {
-        /* the frag 8 ahead: its bytes are read next (copy; the HA tag; TXN's signature count).
+        /* the frag pf_dt ahead: its bytes are read next (copy; the HA tag; TXN's signature count).
            Kept for the copy helper's passes too: without it the helper's copy took 11-12 ns per
            frag instead of 2-5 and copy mode fell from 52-58 to 40-43 M frags/s
            (profiles/r06_copy_prefetch_ab.jsonl) */
-        fd_frag_meta_t const * m8 = in_mcache + ((in_seq + 8UL) & (in_depth-1UL));
+        fd_frag_meta_t const * m8 = in_mcache + ((in_seq + pf_dt) & (in_depth-1UL));
         uchar const * p8 = (uchar const *)fd_chunk_to_laddr_const( in_chunk0b, __atomic_load_n( &m8->chunk, __ATOMIC_RELAXED ) );
         ulong const n8 = zc_dev ? 1UL : std::min( (ulong)__atomic_load_n( &m8->sz, __ATOMIC_RELAXED ), (ulong)FD_VERIFY_AMD_FRAME_SZ );
         for( ulong o = 0; o < n8; o += 64UL ) __builtin_prefetch( p8 + o );

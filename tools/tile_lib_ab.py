@@ -4,7 +4,8 @@ checked frag by frag (the bench's configs[4] pool: 2^16 signatures of 200 B,
 plus paced runs at fixed offered rates (zero copy 4096).  Each build runs in
 its own process (FD_AMD_LIB); one JSON line per run.
 
-usage: python tools/tile_lib_ab.py <rounds> <frags> lib1.so [lib2.so ...]   (a lib "-" = the product)
+usage: python tools/tile_lib_ab.py <rounds> <frags> lib1.so [lib2.so ...]   (a lib "-" = the product;
+       "-@VAR=val;VAR2=val2" = the product with those environment variables)
 env: AB_RATES="27e6, 43e6" paced rates (empty: none), AB_SAT="((4096, True),)" saturated (batch_max, zero copy)
      runs, AB_CONTINUE=1 records a failing build and goes on (an experiment's control)
 """
@@ -56,7 +57,9 @@ if __name__ == "__main__":
     for r in range(rounds):
         for lib in libs:
             env = dict(os.environ)
-            if lib != "-":
+            if lib.startswith("-@"):
+                env.update(kv.split("=", 1) for kv in lib[2:].split(";") if kv)
+            elif lib != "-":
                 env["FD_AMD_LIB"] = os.path.abspath(lib)
             sat = os.environ.get("AB_SAT", "((4096, True), (16384, True), (16384, False))")
             p = subprocess.run([sys.executable, "-c", CHILD % {"root": ROOT, "frags": frags, "rates": rates, "sat": sat}],
