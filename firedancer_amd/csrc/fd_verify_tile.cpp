@@ -1069,8 +1069,9 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   std::vector<uint> pk_slots( 64 );
   /* listing prefetch distances (frags ahead): mcache lines, and the frag
      bytes the copy / HA tag / TXN count read next.  32 / 24 (were 16 / 8):
-     copy mode +8-15 % interleaved over seven rounds in two GPU calls, zero copy
-     unchanged within noise (profiles/r06_listing_prefetch_ab_a/b.jsonl).
+     copy mode +8-15 % interleaved in two A/Bs, equal within noise in a third
+     on the same kind of noisy box; zero copy unchanged
+     (profiles/r06_listing_prefetch_ab_a/b/c.jsonl).
      FD_AMD_TILE_PF="mc,data" overrides them (A/B only) */
   ulong pf_mc = 32UL, pf_dt = 24UL;
   {
