@@ -170,7 +170,8 @@ inline ulong now_ns( void ) {
 #define QUAD_SVC_S    (0.97e-3)
 #define QUAD_FLIGHT_S (1.1e-3)
 
-/* a lower chunk level is taken only once the rule asked for it this long */
+/* a lower chunk level is taken only once the rule asked for it this long,
+   and throughput chunks instead of quad chunks too (fd_verify_amd_tile_level_step) */
 #define LVL_HOLD_NS (2000000UL)
 
 /* order of the chunk levels by capacity: latency < quad < throughput */
@@ -574,9 +575,12 @@ tile_set_levels( fd_verify_amd_tile_t * t ) {
   if( t->quad_lo > t->quad_hi ) t->quad_lo = t->quad_hi;
   /* quad chunks serve up to ~90 % of their capacity at p50 ~0.8 ms (0.80 ms
      at 30 M frags/s, against 1.28 ms in throughput chunks; 0.67 ms at 25 M),
-     so they hold until 92 % of it */
+     so they hold until 92 % of it, and are taken back below 90 % (was 80 %:
+     half load on a 55 M frags/s box, 27.9 M, sat inside that band, so one
+     stall's burst left it in throughput chunks for good); the holds of
+     fd_verify_amd_tile_level_step damp the narrow band */
   t->rate_hi = t->cfg.thr_rate_hi ? (double)t->cfg.thr_rate_hi : thr_ok ? (quad_ok ? 0.92 : 0.55) * below : HUGE_VAL;
-  t->rate_lo = t->cfg.thr_rate_lo ? (double)t->cfg.thr_rate_lo : thr_ok ? (quad_ok ? 0.80 : 0.40) * below : HUGE_VAL;
+  t->rate_lo = t->cfg.thr_rate_lo ? (double)t->cfg.thr_rate_lo : thr_ok ? (quad_ok ? 0.90 : 0.40) * below : HUGE_VAL;
   if( t->rate_lo > t->rate_hi ) t->rate_lo = t->rate_hi;
 }
 
@@ -739,6 +743,36 @@ fd_verify_amd_tile_level( int chunk_mode, int lvl, double rate, double quad_hi, 
   if( rate > rate_hi ) return FD_VERIFY_AMD_LVL_THR;
   if( lvl == FD_VERIFY_AMD_LVL_QUAD ) return rate >= quad_lo ? FD_VERIFY_AMD_LVL_QUAD : FD_VERIFY_AMD_LVL_LAT;
   return rate > quad_hi ? FD_VERIFY_AMD_LVL_QUAD : FD_VERIFY_AMD_LVL_LAT;
+}
+
+/* The level step with its holds (pure; the CPU tests call it).  A lower
+   level, and throughput chunks in place of quad chunks, only once the rule
+   has asked for it for hold_ns: a host stall of a few hundred us dips the
+   rate EWMA (the way down), and the burst that stages its backlog afterwards
+   lifts it over rate_hi for ~1 ms (the way up) -- at half load on a 55 M
+   frags/s box such a burst moved quad chunks (p50 ~0.7 ms) to throughput
+   chunks (p50 1.26 ms) for the rest of the run.  Latency to quad (and
+   latency to throughput) stays immediate: the lower level has a third of the
+   capacity; so does quad back to throughput within 5 hold times of leaving
+   throughput chunks (a dip at 80 % load is undone at once, not after
+   another hold's backlog).  st: [0] 1 + since when the rule has asked for a
+   lower level, [1] ... for throughput from quad (0: it has not), [2] 1 + when
+   the tile last left throughput chunks (0: never); zero it at the start. */
+extern "C" int
+fd_verify_amd_tile_level_step( int lvl, int want, ulong now_ns, ulong hold_ns, ulong * st ) {
+  bool const down = lvl_rank( want ) < lvl_rank( lvl );
+  bool const q2t  = lvl == FD_VERIFY_AMD_LVL_QUAD && want == FD_VERIFY_AMD_LVL_THR &&
+                    !( st[2] && now_ns + 1UL - st[2] < 5UL * hold_ns );
+  if( !down ) st[0] = 0UL;
+  if( !q2t )  st[1] = 0UL;
+  if( down || q2t ) {
+    ulong * t = down ? st : st + 1;
+    if( !*t ) *t = now_ns + 1UL;
+    if( now_ns + 1UL - *t < hold_ns ) return lvl;
+    *t = 0UL;
+  }
+  if( lvl == FD_VERIFY_AMD_LVL_THR && want != lvl ) st[2] = now_ns + 1UL;
+  return want;
 }
 
 /* Chunk packing (pure; the CPU tests call it): from ring entries with
@@ -1062,7 +1096,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   double rate = 0.0;
   int thr = fd_verify_amd_tile_level( t->cfg.chunk_mode, FD_VERIFY_AMD_LVL_LAT, 0.0, t->quad_hi, t->quad_lo, t->rate_hi,
                                       t->rate_lo );   /* chunk level, FD_VERIFY_AMD_LVL_* */
-  ulong t_down = 0UL;                    /* since when the rule has asked for a lower level (0: it has not) */
+  ulong lvl_st[3] = { 0UL, 0UL, 0UL };   /* the level holds' state (fd_verify_amd_tile_level_step) */
   bool halted = false;
   uchar const * in_chunk0b = (uchar const *)in_chunk0;
   fd_verify_amd_tile_cfg_t cc = t->cfg;   /* the cut rule's parameters */
@@ -1338,16 +1372,14 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       rate = rate > 0.0 ? 0.75 * rate + 0.25 * inst : inst;   /* ~0.8 ms memory: a burst does not flip the mode */
       r_t0 = t3; r_n0 = staged_sl; r_blk = false;
       int nthr = fd_verify_amd_tile_level( t->cfg.chunk_mode, thr, rate, t->quad_hi, t->quad_lo, t->rate_hi, t->rate_lo );
-      /* up at once, down only after the rate stayed low for LVL_HOLD_NS: a
-         producer stall of a few hundred us dips the EWMA below the lower
-         threshold, and a dip from throughput into quad chunks at 80 % load
-         left a backlog that flipped the level dozens of times per run
-         (p99 5.8 ms; profiles/r06_bench_quad_a_detail.json) */
-      if( lvl_rank( nthr ) < lvl_rank( thr ) ) {
-        if( !t_down ) t_down = t3;
-        if( t3 - t_down < LVL_HOLD_NS ) nthr = thr;
-        else t_down = 0UL;
-      } else t_down = 0UL;
+      /* down, and quad -> throughput, only after the rule asked for it for
+         LVL_HOLD_NS: a producer stall of a few hundred us dips the EWMA below
+         the lower threshold, and a dip from throughput into quad chunks at 80 %
+         load left a backlog that flipped the level dozens of times per run
+         (p99 5.8 ms; profiles/r06_bench_quad_a_detail.json); the burst after a
+         stall lifted half load into throughput chunks for good (p50 1.26 ms,
+         profiles/r06_level_hold_ab.txt) */
+      nthr = fd_verify_amd_tile_level_step( thr, nthr, t3, LVL_HOLD_NS, lvl_st );
       switches += nthr != thr;
       thr = nthr;
     }

@@ -141,7 +141,8 @@ def lib():
     # entry points added in round 6 (an A/B build of an earlier round, FD_AMD_LIB, lacks them)
     opt = {"fd_ed25519_amd_dropin_set_device": ([i], i), "fd_ed25519_amd_dropin_device": ([], i),
            "fd_ed25519_amd_dropin_pick": ([ctypes.POINTER(i), i, i, ul], i),
-           "fd_verify_amd_tile_level": ([i, i] + [ctypes.c_double] * 5, i)}
+           "fd_verify_amd_tile_level": ([i, i] + [ctypes.c_double] * 5, i),
+           "fd_verify_amd_tile_level_step": ([i, i, ul, ul, ctypes.POINTER(ul)], i)}
     for name, (args, res) in opt.items():
         if hasattr(L, name) or not os.environ.get("FD_AMD_LIB"):
             f = getattr(L, name)

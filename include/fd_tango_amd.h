@@ -145,11 +145,12 @@ typedef struct fd_verify_amd_tile fd_verify_amd_tile_t;
    slots than its level's chunk holds makes a 1-lane chunk of its own, handed
    over at once.  All rates and counts below are in slots.
    chunk_mode AUTO picks the level by the staging rate (EWMA over ~0.8 ms;
-   fd_verify_amd_tile_level; a higher level at once, a lower one only after
-   the rule asked for it for 2 ms): quad chunks above quad_rate_hi, latency chunks
+   fd_verify_amd_tile_level; a higher level at once, except quad to
+   throughput, and a lower one only after the rule asked for it for 2 ms,
+   fd_verify_amd_tile_level_step): quad chunks above quad_rate_hi, latency chunks
    again below quad_rate_lo (0: 55 % / 40 % of the latency chunks' capacity,
    min(min(waves, 4 x CUs) x 8 / 0.45 ms, window / 0.55 ms)); throughput
-   chunks above thr_rate_hi, back below thr_rate_lo (0: 92 % / 80 % of the
+   chunks above thr_rate_hi, back below thr_rate_lo (0: 92 % / 90 % of the
    quad chunks' capacity, min(min(waves, 8 x CUs) x 16 / 0.97 ms, window /
    1.1 ms), x 0.75 in TXN framing, whose whole transactions fill ~3/4 of a
    quad chunk's slots).  Quad chunks are skipped (quad thresholds infinite, the
@@ -386,6 +387,15 @@ fd_verify_amd_tile_mode( int chunk_mode, int thr, double rate, double rate_hi, d
 int
 fd_verify_amd_tile_level( int chunk_mode, int lvl, double rate, double quad_hi, double quad_lo, double rate_hi,
                           double rate_lo );
+
+/* The level step with its holds (pure): the level to run next when the rule
+   above asks for `want` at level lvl at time now_ns.  A lower level, and
+   throughput chunks in place of quad chunks, only once the rule has asked for
+   it for hold_ns -- except quad back to throughput within 5 x hold_ns of
+   leaving throughput chunks; every other move at once.  st: 3 words of state
+   the caller zeroes at the start of a run. */
+int
+fd_verify_amd_tile_level_step( int lvl, int want, ulong now_ns, ulong hold_ns, ulong * st );
 
 /* The chunk packing rule (pure): of cnt staged frags carrying slots[i]
    signature slots each, the next chunk takes the first n (returned; *nsl =

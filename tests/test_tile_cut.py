@@ -127,3 +127,33 @@ def test_level_rule_three_way_hysteresis():
     assert level(tango.CHUNK_LATENCY, T, 50e6) == L
     assert level(tango.CHUNK_THROUGHPUT, L, 0.0) == T
     assert level(tango.CHUNK_QUAD, T, 0.0) == Q and level(tango.CHUNK_QUAD, L, 50e6) == Q
+
+
+def test_level_step_holds():
+    """fd_verify_amd_tile_level_step: down moves and quad -> throughput wait out
+    the hold; latency -> quad / throughput go at once; quad -> throughput at once
+    within 5 holds of leaving throughput chunks."""
+    import ctypes
+    L, Q, T = tango.LVL_LAT, tango.LVL_QUAD, tango.LVL_THR
+    st = (ctypes.c_ulong * 3)()
+    step = ed25519.lib().fd_verify_amd_tile_level_step
+    H = 2_000_000
+
+    def s(lvl, want, now):
+        return step(lvl, want, now, H, st)
+
+    assert s(L, Q, 100) == Q and s(L, T, 100) == T        # up from latency chunks: at once
+    assert s(Q, Q, 0) == Q
+    # a burst: the rule asks for throughput for less than the hold, then not
+    assert s(Q, T, 1_000_000) == Q and s(Q, T, 2_900_000) == Q
+    assert s(Q, Q, 3_000_000) == Q                          # the ask lapsed: the hold restarts
+    assert s(Q, T, 3_100_000) == Q and s(Q, T, 5_099_999) == Q and s(Q, T, 5_100_000) == T
+    # down from throughput: only after the hold
+    assert s(T, Q, 10_000_000) == T and s(T, Q, 11_999_999) == T and s(T, Q, 12_000_000) == Q
+    # back up within 5 holds of leaving throughput chunks: at once
+    assert s(Q, T, 12_500_000) == T
+    assert s(T, Q, 13_000_000) == T and s(T, Q, 15_000_000) == Q   # left again at 15 ms
+    assert s(Q, T, 15_000_000 + 5 * H) == Q                # 5 holds later the hold applies again
+    assert s(Q, L, 30_000_000) == Q and s(Q, L, 32_000_000) == L   # quad -> latency: the hold
+    st[0] = st[1] = st[2] = 0
+    assert s(T, L, 0) == T and s(T, L, H) == L             # time 0 is a time like any other

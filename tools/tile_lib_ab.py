@@ -7,7 +7,8 @@ its own process (FD_AMD_LIB); one JSON line per run.
 usage: python tools/tile_lib_ab.py <rounds> <frags> lib1.so [lib2.so ...]   (a lib "-" = the product;
        "-@VAR=val;VAR2=val2" = the product with those environment variables)
 env: AB_RATES="27e6, 43e6" paced rates (empty: none), AB_SAT="((4096, True),)" saturated (batch_max, zero copy)
-     runs, AB_CONTINUE=1 records a failing build and goes on (an experiment's control)
+     runs, AB_PACED="((4096, True),)" the paced runs' (batch_max, zero copy), AB_SECS=0.4 their length,
+     AB_CONTINUE=1 records a failing build and goes on (an experiment's control)
 """
 import json
 import os
@@ -43,11 +44,14 @@ for bmax, zc in %(sat)s:
                 "chunks": [int(r["gpu_chunks_lat"]), int(r.get("gpu_chunks_quad", 0)), int(r["gpu_chunks_thr"])],
                 "stager_ns": [round(r.get(k, 0.0), 2) for k in ("stager_list_ns", "stager_copy_ns", "stager_stage_ns",
                                                                   "stager_hand_ns")]})
-for rate in (%(rates)s):
-    r = tango.bench_stream(0, 4096, 0, *pool, int(rate * 0.4), rate=rate, zero_copy=True)
-    out.append({"kind": "paced", "offered_m": rate / 1e6, "p50_us": round(r["p50_ns"] / 1e3, 1),
-                "p99_us": round(r["p99_ns"] / 1e3, 1), "switches": int(r["mode_switches"]),
-                "chunks": [int(r["gpu_chunks_lat"]), int(r.get("gpu_chunks_quad", 0)), int(r["gpu_chunks_thr"])]})
+for bmax, zc in %(paced)s:
+    for rate in (%(rates)s):
+        r = tango.bench_stream(0, bmax, 0, *pool, int(rate * %(secs)s), rate=rate, zero_copy=zc)
+        out.append({"kind": "paced", "bmax": bmax, "zc": zc, "offered_m": rate / 1e6, "p50_us": round(r["p50_ns"] / 1e3, 1),
+                    "p99_us": round(r["p99_ns"] / 1e3, 1), "switches": int(r["mode_switches"]),
+                    "chunks": [int(r["gpu_chunks_lat"]), int(r.get("gpu_chunks_quad", 0)), int(r["gpu_chunks_thr"])],
+                    "stalls_us": [round(r[k] / 1e3, 1) for k in ("producer_late_max_ns", "tile_pass_max_ns",
+                                                                  "consumer_gap_max_ns")]})
 print(json.dumps(out))
 '''
 
@@ -62,7 +66,10 @@ if __name__ == "__main__":
             elif lib != "-":
                 env["FD_AMD_LIB"] = os.path.abspath(lib)
             sat = os.environ.get("AB_SAT", "((4096, True), (16384, True), (16384, False))")
-            p = subprocess.run([sys.executable, "-c", CHILD % {"root": ROOT, "frags": frags, "rates": rates, "sat": sat}],
+            paced = os.environ.get("AB_PACED", "((4096, True),)")
+            secs = float(os.environ.get("AB_SECS", "0.4"))
+            p = subprocess.run([sys.executable, "-c", CHILD % {"root": ROOT, "frags": frags, "rates": rates, "sat": sat,
+                                                               "paced": paced, "secs": secs}],
                                env=env, capture_output=True, text=True, timeout=300)
             if p.returncode:
                 print(json.dumps({"round": r, "lib": lib, "rc": p.returncode, "err": p.stderr[-800:]}), flush=True)
