@@ -755,23 +755,35 @@ fd_verify_amd_tile_level( int chunk_mode, int lvl, double rate, double quad_hi, 
    latency to throughput) stays immediate: the lower level has a third of the
    capacity; so does quad back to throughput within 5 hold times of leaving
    throughput chunks (a dip at 80 % load is undone at once, not after
-   another hold's backlog).  st: [0] 1 + since when the rule has asked for a
-   lower level, [1] ... for throughput from quad (0: it has not), [2] 1 + when
-   the tile last left throughput chunks (0: never); zero it at the start. */
+   another hold's backlog).  The way up counts an episode of asking, not one
+   unbroken ask: the episode ends only after hold_ns / 2 without an ask, since
+   a stall under real overload dips the EWMA under rate_hi for a few hundred
+   us too, and restarting the hold at every dip kept 80 % load in quad chunks
+   for 6-7 ms, a backlog that took the rest of the run to drain (p50 8-11 ms
+   in 2 of 18 runs, profiles/r06_level_hold_ab.txt).  st (zeroed at the start
+   of a run): [0] 1 + since when the rule has asked for a lower level (0: it
+   has not), [1] 1 + when the current episode of asking for throughput from
+   quad began (0: none), [2] 1 + when the tile last left throughput chunks
+   (0: never), [3] 1 + when the rule last asked for throughput from quad. */
 extern "C" int
 fd_verify_amd_tile_level_step( int lvl, int want, ulong now_ns, ulong hold_ns, ulong * st ) {
+  ulong const now1 = now_ns + 1UL;
   bool const down = lvl_rank( want ) < lvl_rank( lvl );
-  bool const q2t  = lvl == FD_VERIFY_AMD_LVL_QUAD && want == FD_VERIFY_AMD_LVL_THR &&
-                    !( st[2] && now_ns + 1UL - st[2] < 5UL * hold_ns );
+  bool const up   = lvl == FD_VERIFY_AMD_LVL_QUAD && want == FD_VERIFY_AMD_LVL_THR;
+  bool const fast = st[2] && now1 - st[2] < 5UL * hold_ns;      /* left throughput chunks just now */
   if( !down ) st[0] = 0UL;
-  if( !q2t )  st[1] = 0UL;
-  if( down || q2t ) {
-    ulong * t = down ? st : st + 1;
-    if( !*t ) *t = now_ns + 1UL;
-    if( now_ns + 1UL - *t < hold_ns ) return lvl;
-    *t = 0UL;
+  if( lvl != FD_VERIFY_AMD_LVL_QUAD || ( !up && st[3] && now1 - st[3] >= hold_ns / 2UL ) ) st[1] = st[3] = 0UL;
+  if( down ) {
+    if( !st[0] ) st[0] = now1;
+    if( now1 - st[0] < hold_ns ) return lvl;
+    st[0] = 0UL;
+  } else if( up && !fast ) {
+    if( !st[1] ) st[1] = now1;
+    st[3] = now1;
+    if( now1 - st[1] < hold_ns ) return lvl;
+    st[1] = st[3] = 0UL;
   }
-  if( lvl == FD_VERIFY_AMD_LVL_THR && want != lvl ) st[2] = now_ns + 1UL;
+  if( lvl == FD_VERIFY_AMD_LVL_THR && want != lvl ) st[2] = now1;
   return want;
 }
 
@@ -1096,7 +1108,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   double rate = 0.0;
   int thr = fd_verify_amd_tile_level( t->cfg.chunk_mode, FD_VERIFY_AMD_LVL_LAT, 0.0, t->quad_hi, t->quad_lo, t->rate_hi,
                                       t->rate_lo );   /* chunk level, FD_VERIFY_AMD_LVL_* */
-  ulong lvl_st[3] = { 0UL, 0UL, 0UL };   /* the level holds' state (fd_verify_amd_tile_level_step) */
+  ulong lvl_st[4] = { 0UL, 0UL, 0UL, 0UL };   /* the level holds' state (fd_verify_amd_tile_level_step) */
   bool halted = false;
   uchar const * in_chunk0b = (uchar const *)in_chunk0;
   fd_verify_amd_tile_cfg_t cc = t->cfg;   /* the cut rule's parameters */

@@ -389,10 +389,11 @@ fd_verify_amd_tile_level( int chunk_mode, int lvl, double rate, double quad_hi, 
                           double rate_lo );
 
 /* The level step with its holds (pure): the level to run next when the rule
-   above asks for `want` at level lvl at time now_ns.  A lower level, and
-   throughput chunks in place of quad chunks, only once the rule has asked for
-   it for hold_ns -- except quad back to throughput within 5 x hold_ns of
-   leaving throughput chunks; every other move at once.  st: 3 words of state
+   above asks for `want` at level lvl at time now_ns.  A lower level only once
+   the rule has asked for it for hold_ns without a break; throughput chunks in
+   place of quad chunks once an episode of asking for them (asks less than
+   hold_ns / 2 apart) has lasted hold_ns -- at once within 5 x hold_ns of
+   leaving throughput chunks; every other move at once.  st: 4 words of state
    the caller zeroes at the start of a run. */
 int
 fd_verify_amd_tile_level_step( int lvl, int want, ulong now_ns, ulong hold_ns, ulong * st );

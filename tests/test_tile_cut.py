@@ -130,30 +130,37 @@ def test_level_rule_three_way_hysteresis():
 
 
 def test_level_step_holds():
-    """fd_verify_amd_tile_level_step: down moves and quad -> throughput wait out
-    the hold; latency -> quad / throughput go at once; quad -> throughput at once
-    within 5 holds of leaving throughput chunks."""
+    """fd_verify_amd_tile_level_step: a lower level only after an unbroken 2 ms
+    ask; quad -> throughput once an episode of asks (gaps under 1 ms) has lasted
+    2 ms; latency -> quad / throughput at once; quad -> throughput at once within
+    5 holds of leaving throughput chunks."""
     import ctypes
     L, Q, T = tango.LVL_LAT, tango.LVL_QUAD, tango.LVL_THR
-    st = (ctypes.c_ulong * 3)()
+    st = (ctypes.c_ulong * 4)()
     step = ed25519.lib().fd_verify_amd_tile_level_step
-    H = 2_000_000
+    H, ms = 2_000_000, 1_000_000
 
     def s(lvl, want, now):
-        return step(lvl, want, now, H, st)
+        return step(lvl, want, int(now), H, st)
 
     assert s(L, Q, 100) == Q and s(L, T, 100) == T        # up from latency chunks: at once
     assert s(Q, Q, 0) == Q
-    # a burst: the rule asks for throughput for less than the hold, then not
-    assert s(Q, T, 1_000_000) == Q and s(Q, T, 2_900_000) == Q
-    assert s(Q, Q, 3_000_000) == Q                          # the ask lapsed: the hold restarts
-    assert s(Q, T, 3_100_000) == Q and s(Q, T, 5_099_999) == Q and s(Q, T, 5_100_000) == T
-    # down from throughput: only after the hold
-    assert s(T, Q, 10_000_000) == T and s(T, Q, 11_999_999) == T and s(T, Q, 12_000_000) == Q
+    # a stall's burst: the rule asks for throughput for 1 ms, then stops for 1 ms: the episode ends
+    assert all(s(Q, T, t * ms) == Q for t in (1.0, 1.5, 2.0))
+    assert s(Q, Q, 2.5 * ms) == Q and s(Q, Q, 3.0 * ms) == Q
+    assert all(s(Q, T, t * ms) == Q for t in (3.1, 3.6, 4.1, 4.6, 5.0))   # a new episode from 3.1 ms
+    assert s(Q, T, 5.1 * ms) == T
+    # real overload with a dip: the dip (0.5 ms without an ask) does not restart the episode
+    st[0] = st[1] = st[2] = st[3] = 0
+    assert s(Q, T, 10 * ms) == Q and s(Q, Q, 10.5 * ms) == Q and s(Q, T, 11 * ms) == Q
+    assert s(Q, T, 12 * ms) == T
+    # down from throughput: only after an unbroken hold
+    assert s(T, Q, 20 * ms) == T and s(T, T, 21 * ms) == T          # the ask broke: the hold restarts
+    assert s(T, Q, 21.5 * ms) == T and s(T, Q, 23.4 * ms) == T and s(T, Q, 23.5 * ms) == Q
     # back up within 5 holds of leaving throughput chunks: at once
-    assert s(Q, T, 12_500_000) == T
-    assert s(T, Q, 13_000_000) == T and s(T, Q, 15_000_000) == Q   # left again at 15 ms
-    assert s(Q, T, 15_000_000 + 5 * H) == Q                # 5 holds later the hold applies again
-    assert s(Q, L, 30_000_000) == Q and s(Q, L, 32_000_000) == L   # quad -> latency: the hold
-    st[0] = st[1] = st[2] = 0
+    assert s(Q, T, 24 * ms) == T
+    assert s(T, Q, 25 * ms) == T and s(T, Q, 27 * ms) == Q          # left again at 27 ms
+    assert s(Q, T, 37 * ms) == Q                                    # 5 holds later the hold applies again
+    assert s(Q, L, 40 * ms) == Q and s(Q, L, 42 * ms) == L          # quad -> latency: the hold
+    st[0] = st[1] = st[2] = st[3] = 0
     assert s(T, L, 0) == T and s(T, L, H) == L             # time 0 is a time like any other
