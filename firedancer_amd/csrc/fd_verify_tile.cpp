@@ -1105,6 +1105,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
   ulong t_chk = pass_t, g_seen = 0UL, t_prog = pass_t, gc_first = 0UL, gc_last = 0UL, gc_host = 0UL;
   ulong r_t0 = pass_t, r_n0 = 0UL;
   bool  r_blk = false;                   /* staging stopped on the window / frames / credit this interval */
+  bool  r_win = false;                   /* ... on the window or the frames (the GPU's chunks do not keep up) */
   double rate = 0.0;
   int thr = fd_verify_amd_tile_level( t->cfg.chunk_mode, FD_VERIFY_AMD_LVL_LAT, 0.0, t->quad_hi, t->quad_lo, t->rate_hi,
                                       t->rate_lo );   /* chunk level, FD_VERIFY_AMD_LVL_* */
@@ -1264,7 +1265,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
           mode lists the pass's copies first (a frame reserved per frag),
           copies them -- with the helper when there is one -- and then
           re-checks and stages each frag in input order */
-    bool full = false;
+    bool full = false, wfull = false;
     ulong const stage_end = staged + STAGE_PASS;
     ulong const staged_a = staged, pt0 = __rdtsc();
     ulong pt1 = 0UL, pt2 = 0UL;
@@ -1278,7 +1279,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
     ulong const pnj = pend.on ? pend.nj : 0UL, psl = pend.on ? pend.sl : 0UL;   /* the posted pass, not staged yet */
     while( !done_in && staged_sl + psl + sl_pass - handed_sl < t->batch_max && staged + nj != stage_end ) {
       if( frag_cnt && in_seq - in_seq0 >= frag_cnt ) break;
-      if( staged + pnj + nj - pubd >= W ) { full = true; n_stop_window++; break; }
+      if( staged + pnj + nj - pubd >= W ) { full = wfull = true; n_stop_window++; break; }
       fd_frag_meta_t const * m = in_mcache + (in_seq & (in_depth-1UL));
       __builtin_prefetch( in_mcache + ((in_seq + pf_mc) & (in_depth-1UL)) );
       ulong seq_found = __atomic_load_n( &m->seq, __ATOMIC_ACQUIRE );
@@ -1311,7 +1312,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       ulong tag = 0UL;
       if( t->tc.depth && k2 ) memcpy( &tag, p + (txn ? 1UL : 32UL), 8 );
       uint f; bool credit;
-      if( !reserve( &f, &credit ) ) { full = true; if( credit ) backp++; else n_stop_frames++; break; }
+      if( !reserve( &f, &credit ) ) { full = true; if( credit ) backp++; else { wfull = true; n_stop_frames++; } break; }
       if( !zc_dev ) {
         /* copy mode: the frame is the tile's copy */
         jobs[nj++] = copy_job_t{ t->out_base + (ulong)f * FD_VERIFY_AMD_FRAME_SZ, p, m, in_seq, sz, tag, f, (uint)tsorig,
@@ -1360,6 +1361,7 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
       ph_frags += staged - staged_a;
     }
     r_blk = r_blk || full;
+    r_win = r_win || wfull;
     n_stop_bmax += staged_sl - handed_sl >= t->batch_max;
     n_stop_pass += staged == stage_end || nj == STAGE_PASS;
     __atomic_store_n( &diag->in_cnt, in_cnt, __ATOMIC_RELEASE );
@@ -1382,8 +1384,15 @@ tile_run_persist( fd_verify_amd_tile_t * t, fd_frag_meta_t const * in_mcache, ul
          capacity -- and the backlog grows) */
       if( r_blk ) inst = std::max( inst, rate );
       rate = rate > 0.0 ? 0.75 * rate + 0.25 * inst : inst;   /* ~0.8 ms memory: a burst does not flip the mode */
-      r_t0 = t3; r_n0 = staged_sl; r_blk = false;
       int nthr = fd_verify_amd_tile_level( t->cfg.chunk_mode, thr, rate, t->quad_hi, t->quad_lo, t->rate_hi, t->rate_lo );
+      /* staging that stopped on the window or the frames in quad chunks: they
+         do not keep up, whatever the rate says -- it then measures their
+         completions, which on a slow or busy box stay under rate_hi (a
+         saturated run on such a box stayed in quad chunks at 17-25 M frags/s,
+         profiles/r06_level_hold_ab.txt) */
+      if( thr == FD_VERIFY_AMD_LVL_QUAD && r_win && t->cfg.chunk_mode == FD_VERIFY_AMD_CHUNK_AUTO && t->rate_hi < HUGE_VAL )
+        nthr = FD_VERIFY_AMD_LVL_THR;
+      r_t0 = t3; r_n0 = staged_sl; r_blk = false; r_win = false;
       /* down, and quad -> throughput, only after the rule asked for it for
          LVL_HOLD_NS: a producer stall of a few hundred us dips the EWMA below
          the lower threshold, and a dip from throughput into quad chunks at 80 %
