@@ -218,6 +218,28 @@ def test_tile_large_batches_vs_oracle(batch_max, zero_copy):
     assert r["gpu_frags_quad"] <= 16 * r["gpu_chunks_quad"]
 
 
+@pytest.mark.parametrize("zero_copy", [False, True])
+def test_tile_auto_levels_vs_oracle(zero_copy):
+    """The AUTO level rule end to end, every frag checked: a saturated
+    stream ends up in throughput chunks (the window-full rule and the 2 ms
+    episode of fd_verify_amd_tile_level_step), a stream paced at 20 M frags/s
+    (above the latency chunks' capacity, well under the quad chunks') runs
+    mostly in quad chunks; both publish exactly the oracle's accepted set."""
+    from firedancer_amd import tango
+    pub, sig, off, sz, blob, err, tag = _stream_pool(6060 + zero_copy, 8192, 400)
+    for rate, nf in ((0.0, 1 << 20), (20e6, 1 << 20)):
+        r = tango.bench_stream(0, 4096, 0, pub, sig, off, sz, blob, nf, rate=rate, zero_copy=zero_copy,
+                               expect_err=err, expect_tag=tag)
+        want = int((err[np.arange(nf) % err.size] == 0).sum())
+        assert r["mismatches"] == 0 and r["ovrn"] == 0
+        assert r["checked"] == r["published"] == want and r["sv_filt"] == nf - want
+        assert r["gpu_frags_lat"] + r["gpu_frags_quad"] + r["gpu_frags_thr"] == nf
+        if rate:
+            assert r["gpu_frags_quad"] > nf // 2, r
+        else:
+            assert r["gpu_frags_thr"] > nf // 2, r
+
+
 def test_tile_copy_without_helper_vs_oracle():
     """Copy mode with every copy on the stager (cfg.copy_cpu = COPY_INLINE;
     the bench's default gives copy mode a helper thread when the process has
