@@ -767,6 +767,7 @@ fd_verify_amd_tile_level( int chunk_mode, int lvl, double rate, double quad_hi, 
    (0: never), [3] 1 + when the rule last asked for throughput from quad. */
 extern "C" int
 fd_verify_amd_tile_level_step( int lvl, int want, ulong now_ns, ulong hold_ns, ulong * st ) {
+  if( !st ) return want;   /* no state: no holds */
   ulong const now1 = now_ns + 1UL;
   bool const down = lvl_rank( want ) < lvl_rank( lvl );
   bool const up   = lvl == FD_VERIFY_AMD_LVL_QUAD && want == FD_VERIFY_AMD_LVL_THR;

@@ -394,7 +394,7 @@ fd_verify_amd_tile_level( int chunk_mode, int lvl, double rate, double quad_hi, 
    place of quad chunks once an episode of asking for them (asks less than
    hold_ns / 2 apart) has lasted hold_ns -- at once within 5 x hold_ns of
    leaving throughput chunks; every other move at once.  st: 4 words of state
-   the caller zeroes at the start of a run. */
+   the caller zeroes at the start of a run (NULL: no holds, want is returned). */
 int
 fd_verify_amd_tile_level_step( int lvl, int want, ulong now_ns, ulong hold_ns, ulong * st );
 

@@ -164,3 +164,4 @@ def test_level_step_holds():
     assert s(Q, L, 40 * ms) == Q and s(Q, L, 42 * ms) == L          # quad -> latency: the hold
     st[0] = st[1] = st[2] = st[3] = 0
     assert s(T, L, 0) == T and s(T, L, H) == L             # time 0 is a time like any other
+    assert step(Q, T, 0, H, None) == T and step(T, L, 0, H, None) == L   # no state: no holds
