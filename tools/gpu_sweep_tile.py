@@ -28,6 +28,9 @@ from gpu_sweep import STREAMS, N, CH  # noqa: E402
 
 SUB = 1 << 20          # frags per tile run
 MODES = ((tango.CHUNK_LATENCY, "latency"), (tango.CHUNK_THROUGHPUT, "throughput"), (tango.CHUNK_QUAD, "quad"))
+# the AUTO rule (the product default) on request only: FD_SWEEP_TILE_MODES=auto
+if "auto" in os.environ.get("FD_SWEEP_TILE_MODES", "").split(","):
+    MODES = MODES + ((tango.CHUNK_AUTO, "auto"),)
 # copy mode with the copy helper (cfg.copy_cpu) on the last CPU this process may use, when FD_SWEEP_TILE_HELPER=1
 HELPER = {"copy_cpu": max(os.sched_getaffinity(0))} if os.environ.get("FD_SWEEP_TILE_HELPER") else {}
 if os.environ.get("FD_SWEEP_TILE_MODES"):   # e.g. "quad" or "latency,quad"
