@@ -379,6 +379,28 @@ def worst_of(rs):
     return worst, (max(x["p99_over_p50"] for x in clean) if clean else None), len(rs) - len(clean)
 
 
+TOPUP_MAX = 3   # extra paced runs per load, only while fewer than three runs are free of harness stalls
+
+
+def top_up(rs, run):
+    """Run more paced runs (run() -> one run) while fewer than three of rs are free of harness stalls,
+    at most TOPUP_MAX of them: a producer descheduled for 0.1-0.3 s (seen on busy boxes) otherwise decides
+    the row's median p50 when it hits two of three runs.  Every run, extra ones included, stays in rs and
+    in the all-runs tail check."""
+    extra = 0
+    while sum(not harness_stalled(x) for x in rs) < 3 and extra < TOPUP_MAX:
+        rs.append(run())
+        extra += 1
+    return extra
+
+
+def p50_run(rs):
+    """The run whose p50 is the row's: the median over the runs free of harness stalls (all runs when
+    none is)."""
+    clean = [x for x in rs if not harness_stalled(x)] or rs
+    return sorted(clean, key=lambda x: x["p50_us"])[len(clean) // 2]
+
+
 def unstalled_ok(loads):
     """Every load's stall-free runs within 2.5 x p50; a load whose every run had a harness stall vouches for
     nothing, so it fails the check (VERDICT/ADVICE r05: it used to pass)."""
@@ -728,20 +750,23 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
                 for load in (0.5, 0.8):
                     runs[load].append(paced(bmax, zc, load * sat["frags_per_s"]))
             for load, rs in runs.items():
-                # p50 is the median of the three runs' p50; the tail is the WORST run's p99 / p50 (a
+                # p50 is the median of the runs' p50 (over the runs free of harness stalls, topped up to
+                # three when a stall hit some); the tail is the WORST run's p99 / p50 over every run (a
                 # single bad run must fail the row: VERDICT r04 weak 2, 9); every run is kept whole
-                med = sorted(rs, key=lambda x: x["p50_us"])[1]
+                extra = top_up(rs, lambda: paced(bmax, zc, load * sat["frags_per_s"]))
+                med = p50_run(rs)
                 worst, worst_clean, nstall = worst_of(rs)
                 r = {"p50_us": med["p50_us"], "frags_per_s": med["frags_per_s"],
                      "offered_frags_per_s": med["offered_frags_per_s"],
                      "worst_p99_us": worst["p99_us"], "worst_p99_over_p50": worst["p99_over_p50"],
-                     "worst_run": rs.index(worst), "harness_stalled_runs": nstall,
+                     "worst_run": rs.index(worst), "harness_stalled_runs": nstall, "extra_runs": extra,
                      "worst_p99_over_p50_unstalled": worst_clean, "runs": rs}
                 rr["at_%d%%" % int(load * 100)] = r
             lo, hi = rr["at_50%"], rr["at_80%"]
-            # medians of three runs; the only slack is the spread of the three 50 % runs' own p50s (the
+            # medians of three runs; the only slack is the spread of the 50 % runs' own p50s (the
             # measured run-to-run noise: copy-mode p50s barely move with load, 0.1-0.2 % either way)
-            sp = max(x["p50_us"] for x in lo["runs"]) - min(x["p50_us"] for x in lo["runs"])
+            lo_clean = [x for x in lo["runs"] if not harness_stalled(x)] or lo["runs"]
+            sp = max(x["p50_us"] for x in lo_clean) - min(x["p50_us"] for x in lo_clean)
             rr["p50_spread_us_50"] = sp
             rr["p50_nondecreasing_with_load"] = hi["p50_us"] >= lo["p50_us"] - sp
             rr["p99_within_2_5x_p50"] = max(lo["worst_p99_over_p50"], hi["worst_p99_over_p50"]) <= 2.5
@@ -770,7 +795,7 @@ def stream_rows(local, pub, sig, off, sz, blob, args, mac_per_sig=None, world=1,
            "every_row_p99_within_2_5x_p50_unstalled": all(r["p99_within_2_5x_p50_unstalled"] for r in allr),
            "harness_stall_rule_us": HARNESS_STALL_US,
            "every_row_p50_nondecreasing_with_load": all(r["p50_nondecreasing_with_load"] for r in allr),
-           "p50_rule": "median p50 at 80 % >= median p50 at 50 % minus the spread of the three 50 % runs' p50s",
+           "p50_rule": "median p50 at 80 % >= median p50 at 50 % minus the spread of the 50 % runs' p50s; medians over the runs free of harness stalls (topped up to three, at most 3 extra runs)",
            "rows": rows}
     if fixed:
         out["fixed_1M_frags_per_s_batch_max_4096"] = fixed
@@ -835,12 +860,13 @@ def txn_stream_row(local, args):
             for load in (0.5, 0.8):
                 runs[load].append(paced(bmax, load * sat["frags_per_s"]))
         for load, rs in runs.items():
-            med = sorted(rs, key=lambda x: x["p50_us"])[1]
+            extra = top_up(rs, lambda: paced(bmax, load * sat["frags_per_s"]))
+            med = p50_run(rs)
             worst, worst_clean, nstall = worst_of(rs)
             out["at_%d%%" % int(load * 100)] = {"p50_us": med["p50_us"], "txns_per_s": med["txns_per_s"],
                                                 "worst_p99_us": worst["p99_us"],
                                                 "worst_p99_over_p50": worst["p99_over_p50"],
-                                                "harness_stalled_runs": nstall,
+                                                "harness_stalled_runs": nstall, "extra_runs": extra,
                                                 "worst_p99_over_p50_unstalled": worst_clean, "runs": rs}
         out["p99_within_2_5x_p50"] = max(out["at_50%"]["worst_p99_over_p50"],
                                          out["at_80%"]["worst_p99_over_p50"]) <= 2.5

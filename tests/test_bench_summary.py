@@ -108,3 +108,24 @@ def test_roofline_from_rocprof_and_held_clock(tmp_path, monkeypatch):
     assert abs(r["frac_rocprof"] / r["frac"] - 13.0 / 13.6) < 1e-9
     assert abs(r["frac_at_held_clock"] / r["frac"] - 2.4 / 2.2) < 1e-9
     assert r["traffic"] == 2.0e10 and r["traffic_raw"] == 1.0e7 * 1024
+
+
+def test_stalled_runs_are_topped_up_and_left_out_of_the_median():
+    """A producer stall on two of three paced runs: more runs until three are
+    stall-free (at most TOPUP_MAX), the p50 is their median, and every run --
+    stalled and extra ones too -- stays in the all-runs tail check."""
+    rs = [_run(700, 800), _run(150000, 320000, late=300000.0), _run(152000, 330000, late=310000.0)]
+    fresh = iter([_run(710, 790), _run(690, 770), _run(720, 800)])
+    extra = bench.top_up(rs, lambda: next(fresh))
+    assert extra == 2 and len(rs) == 5
+    assert bench.p50_run(rs)["p50_us"] == 700                      # median of 700, 710, 690
+    worst, clean, nst = bench.worst_of(rs)
+    assert nst == 2 and worst["p99_us"] == 330000 and clean < 1.2  # the stalled runs still set the all-runs tail
+    # at most TOPUP_MAX extra runs, then the median over whatever is clean
+    rs2 = [_run(1000, 1100, late=5000.0)] * 3
+    stalled = iter([_run(1000, 1100, late=5000.0)] * bench.TOPUP_MAX)
+    assert bench.top_up(rs2, lambda: next(stalled)) == bench.TOPUP_MAX
+    assert bench.p50_run(rs2)["p50_us"] == 1000                    # none clean: the median of all
+    # three clean runs: nothing extra
+    rs3 = [_run(600, 700), _run(610, 700), _run(620, 700)]
+    assert bench.top_up(rs3, lambda: None) == 0 and bench.p50_run(rs3)["p50_us"] == 610
